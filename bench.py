@@ -1,0 +1,269 @@
+"""Env-step throughput of the MI355X humanoid engine (BASELINE.json metric).
+
+One "step" = one policy step of every env on every rank: actions -> PD targets -> 2 physics
+substeps at 1/60 s -> reward / reset / 934-float obs -> device-side reset of flagged envs
+(puffer_phc/clean_pufferl/env.py:109-183 semantics; env-steps/s definition env.py:217-230).
+
+Default workload = BASELINE configs[1]: 4096 SMPL-neutral humanoids per GPU, PD stand-still
+(zero reference motion, actions = 0). `--config imitation` = configs[2] (128 synthetic clips,
+one fixed U(-1,1) action sample), `--config dr` = configs[4] (mass/friction randomisation +
+3 terrains). Data: synthetic clips (AMASS / SMPL are not available offline).
+
+Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`; every rank owns
+its own 4096 envs (envs are independent: no data-path collective), barrier + synchronize around the
+timed region, max time over ranks, value = total env-steps of all ranks / that time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+# SURVEY.md §8(d) canonical algorithmic counts per env-step
+PHYS_FLOP_PER_ENV_STEP = 1_309_278          # dense-equivalent physics, 2 substeps, n_c = 8
+IMIT_BYTES_PER_ENV_STEP = 13_200            # fused imitation kernel share of the 16.0 KB/env-step
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--config", choices=["standstill", "imitation", "dr"], default="standstill")
+    ap.add_argument("--clips", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-envs", type=int, default=256)
+    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--max-contacts", type=int, default=24)
+    return ap.parse_args()
+
+
+def build_workload(args, model, rank):
+    from humanoid_amd import synthetic
+    from humanoid_amd.motion_lib import build_tables, MotionTables
+    n = args.num_envs
+    if args.config == "standstill":
+        clips = [synthetic.make_standstill_clip(model, num_frames=150)]
+        assign = np.zeros(n, np.int64)
+    else:
+        rng = np.random.default_rng(args.seed)
+        clips = [synthetic.make_clip(model, rng, num_frames=150) for _ in range(args.clips)]
+        assign = np.arange(n) % args.clips
+    base = build_tables(model, clips)
+    tables = MotionTables(gts=base.gts, grs=base.grs, lrs=base.lrs, gvs=base.gvs, gavs=base.gavs, dvs=base.dvs,
+                          num_frames=base.num_frames[assign], length_starts=base.length_starts[assign],
+                          lengths=base.lengths[assign], dt=base.dt[assign], fps=base.fps[assign])
+    rng = np.random.default_rng(args.seed + 1 + rank)
+    if args.config == "imitation":
+        actions = rng.uniform(-1, 1, (1, 69)).astype(np.float32).repeat(n, 0)  # env.py:221 one sample reused
+    else:
+        actions = np.zeros((n, 69), np.float32)
+    return tables, actions, rng
+
+
+class Rollout:
+    """Device-resident rollout state for one rank."""
+
+    def __init__(self, args, model, device_index, rank):
+        import torch
+        from humanoid_amd import _abi
+        from humanoid_amd.engine import Engine
+        from humanoid_amd.model import pd_action_offset_scale
+        from humanoid_amd.body_sets import frozen_dof_mask
+        self.args = args
+        n = args.num_envs
+        tables, actions, rng = build_workload(args, model, rank)
+        sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0)
+        self.eng = Engine(model, n, device=device_index, sim_params=sim, start_xy=rng.uniform(-1, 1, (n, 2)))
+        dev = self.eng.device
+        self.eng.load_motions(tables)
+        off, sc = pd_action_offset_scale(model)
+        self.eng.set_pd_params(off, sc, np.array(frozen_dof_mask(), np.int32), clip_actions=True)
+        if args.config == "dr":
+            self.ms = torch.as_tensor(rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32), device=dev)
+            self.fr = torch.as_tensor(rng.uniform(0.5, 1.25, n).astype(np.float32), device=dev)
+            self.tk = torch.as_tensor((np.arange(n) % 3).astype(np.int32), device=dev)
+            self.eng.set_env_properties(self.ms, self.fr, self.tk)
+        self.p = _abi.imitation_params()
+        self.mids = torch.arange(n, device=dev, dtype=torch.int64)
+        self.st = torch.zeros(n, device=dev)
+        self.so = torch.zeros(n, device=dev)
+        self.go = torch.zeros(n, 3, device=dev)
+        self.prog = torch.zeros(n, dtype=torch.int16, device=dev)
+        self.em = self.eng.env_motion(self.mids, self.st, self.so, self.go, self.prog)
+        self.obs = torch.zeros(n, 934, device=dev)
+        self.rew = torch.zeros(n, device=dev)
+        self.raw = torch.zeros(n, 5, device=dev)
+        self.reset = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.term = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.actions = torch.as_tensor(actions, device=dev)
+        self.seed = args.seed * 7919 + rank
+        self.step_index = 0
+        # HumanoidPHC.reset() of all envs (reference state init, humanoid_phc.py:90-103)
+        ids = torch.arange(n, dtype=torch.int32, device=dev)
+        phases = torch.as_tensor(rng.uniform(0, 1, n).astype(np.float32), device=dev)
+        self.eng.reset_envs(self.p, self.em, ids, phases, self.obs, self.reset, self.term)
+
+    def step(self, ev=None):
+        """ev: optional (start, mid, end) torch.cuda.Events around the two kernels."""
+        if ev is not None:
+            ev[0].record()
+        self.eng.step_actions(self.actions, 2)
+        if ev is not None:
+            ev[1].record()
+        self.eng.imitation_reset_step(self.p, self.em, self.obs, self.rew, self.raw, self.reset, self.term,
+                                      seed=self.seed, step_index=self.step_index)
+        if ev is not None:
+            ev[2].record()
+        self.step_index += 1
+
+
+def cpu_baseline(args, model):
+    """Oracle (C, OpenMP) full env step on a bounded sample: `cpu_envs` envs x `cpu_steps` steps."""
+    from humanoid_amd import _abi
+    from humanoid_amd.model import pd_action_offset_scale
+    from humanoid_amd.body_sets import frozen_dof_mask
+    from oracle import oracle as O
+    a = argparse.Namespace(**vars(args))
+    a.num_envs = args.cpu_envs
+    tables, actions, rng = build_workload(a, model, 0)
+    n = a.num_envs
+    hm = _abi.make_model(model)
+    sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0)
+    mt = O.MotionTables.from_tables(tables)
+    p = _abi.imitation_params()
+    off, sc = pd_action_offset_scale(model)
+    frozen = np.array(frozen_dof_mask(), bool)
+    tgt = (off + sc * np.clip(actions, -1, 1)).astype(np.float32)
+    tgt[:, frozen] = 0
+    st = dict(start_times=np.zeros(n, np.float32), start_offsets=np.zeros(n, np.float32),
+              global_offset=np.zeros((n, 3), np.float32), progress=np.zeros(n, np.int16),
+              root_states=np.zeros((n, 13), np.float32), dof_state=np.zeros((n, 69, 2), np.float32),
+              dof_targets=np.zeros((n, 69), np.float32), rb_state=np.zeros((n, 24, 13), np.float32),
+              contact_forces=np.zeros((n, 24, 3), np.float32), obs=np.zeros((n, 934), np.float32),
+              reset=np.zeros(n, np.uint8), terminate=np.zeros(n, np.uint8))
+    O.reset_envs(p, mt, np.arange(n), rng.uniform(0, 1, n).astype(np.float32), np.arange(n), st)
+    ms = fr = tk = None
+    if args.config == "dr":
+        ms = rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32)
+        fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
+        tk = (np.arange(n) % 3).astype(np.int32)
+    t0 = time.perf_counter()
+    for step in range(a.cpu_steps):
+        out = O.physics_step(hm, sim, st["root_states"], st["dof_state"], tgt, 2, mass_scale=ms, friction=fr,
+                             terrain_kind=tk)
+        im = O.imitation_step(p, mt, out["rb_state"], st["dof_state"][..., 1], out["dof_force"], st["progress"],
+                              np.arange(n), st["start_times"], st["start_offsets"], st["global_offset"])
+        st["progress"][:] = im["progress"]
+        st["rb_state"][:] = out["rb_state"]
+        st["obs"] = im["obs"]
+        ids = np.nonzero(im["reset"])[0]
+        if len(ids):
+            ph = np.array([O.hash_uniform(0, step, int(e)) for e in ids], np.float32)
+            O.reset_envs(p, mt, ids, ph, np.arange(n), st)
+    dt = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": n * a.cpu_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {a.cpu_steps} policy steps of the C oracle (fp64 physics + imitation + resets), "
+                      f"OpenMP over envs, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from humanoid_amd.model import load_default_model
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    model = load_default_model()
+    ro = Rollout(args, model, local, rank)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ro.step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ro.step(evs[k])
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n = args.num_envs
+    total_steps = n * args.steps * world
+    value = total_steps / elapsed
+    if rank == 0:
+        phys_tflops = PHYS_FLOP_PER_ENV_STEP * n / (phys_ms * 1e-3) / 1e12
+        imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tfile):
+            try:
+                tr = json.load(open(tfile))
+                key = f"{args.config}:{n}"
+                if key in tr:
+                    traffic = tr[key].get("physics_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "env-steps/sec (4096 SMPL humanoids per GPU)",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (AMASS-schema clips generated offline; random-free stand-still clip for configs[1])",
+            "config": {"workload": {"standstill": "configs[1]: 4096 SMPL-neutral humanoids, PD stand-still, zero ref motion",
+                                    "imitation": "configs[2]: 4096 humanoids over 128 synthetic clips, full PHC reward",
+                                    "dr": "configs[4]: 4096 envs, mass/friction randomisation + 3 terrains"}[args.config],
+                       "num_envs_per_gpu": n, "substeps": 2, "sim_dt": 1 / 60, "max_contacts": args.max_contacts,
+                       "parallelism": f"replicas{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
+                         "kernel": "physics_kernel (fp32 vector; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
+                         "avg_launch_ms": round(phys_ms, 4)},
+            "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(imit_gbs / HBM_PEAK_GBS, 5), "avg_launch_ms": round(imit_ms, 4)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                line["cpu_baseline"] = cpu_baseline(args, model)
+            except Exception as exc:  # report, never fake
+                line["cpu_baseline"] = {"value": None, "error": repr(exc)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+"""Build ``humanoid_amd/libhumanoid_engine.so`` for gfx950 with hipcc (in-tree, travels with the
+repo to the GPU box). Usage: ``python -m humanoid_amd.build [--force]``."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libhumanoid_engine.so")
+BUILD = os.path.join(HERE, "_build")
+ARCH = os.environ.get("HE_OFFLOAD_ARCH", "gfx950")
+
+# (source, extra flags): the imitation kernel must evaluate float32 expressions exactly as the
+# reference's torch ops do (no FMA contraction); the physics kernel may contract.
+SOURCES = [
+    ("he_imitation.hip", ["-ffp-contract=off"]),
+    ("he_physics.hip", []),
+    ("he_engine.cpp", ["-x", "hip"]),
+]
+HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h")]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def build(force=False, verbose=False):
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    common = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
+    hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
+    objs = []
+    rebuilt = False
+    for src, flags in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + ".o")
+        objs.append(o)
+        if force or _mtime(o) < max(_mtime(s), hdr_time):
+            cmd = [hipcc] + common + flags + ["-c", s, "-o", o]
+            if verbose:
+                print(" ".join(cmd))
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+            rebuilt = True
+    if force or rebuilt or _mtime(LIB) < max(_mtime(o) for o in objs):
+        cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

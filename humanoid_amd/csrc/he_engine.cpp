@@ -1,0 +1,454 @@
+// he_engine.cpp -- C-ABI implementation of libhumanoid_engine.so (include/humanoid_engine.h).
+// Owns the device state (hipMalloc), the device model/topology blobs and the device motion
+// library, and launches the gfx950 kernels on the caller's stream. No host synchronisation on
+// any compute entry point; allocation happens only in he_create_envs / he_load_motions.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/humanoid_engine.h"
+#include "he_kernels.h"
+#include "he_topo.h"
+
+size_t physics_lds_bytes(int max_contacts, int* mpad_out);
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return 1;
+}
+
+#define HE_CHECK(expr)                                                                         \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+    } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, size_t n) {
+    return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T) > 0 ? n * sizeof(T) : 16);
+}
+}  // namespace
+
+struct he_engine {
+    int device = 0;
+    he_sim_params params{};
+    he_model model{};
+    bool has_model = false;
+    he_model* d_model = nullptr;
+    PhysTopo* d_topo = nullptr;
+    int num_envs = 0;
+    float *root = nullptr, *dof_state = nullptr, *rb = nullptr, *cf = nullptr, *dof_force = nullptr, *targets = nullptr;
+    int32_t* num_contacts = nullptr;
+    const float *mass_scale = nullptr, *friction = nullptr;
+    const int32_t* terrain_kind = nullptr;
+    float *pd_offset = nullptr, *pd_scale = nullptr;
+    int32_t* frozen = nullptr;
+    int clip_actions = 1;
+    bool has_pd = false;
+    // motion library
+    float *m_hot = nullptr, *m_cold = nullptr, *m_lengths = nullptr, *m_dt = nullptr;
+    int64_t *m_starts = nullptr, *m_nframes = nullptr;
+    int64_t m_frames = 0;
+    int m_motions = 0;
+};
+
+extern "C" {
+
+const char* he_last_error(void) { return g_err.c_str(); }
+int he_version(void) { return 1; }
+
+int he_device_count(int* count) {
+    HE_CHECK(hipGetDeviceCount(count));
+    return 0;
+}
+
+int he_create(const he_sim_params* params, int device, he_engine** out) {
+    if (!params || !out) return fail("he_create: null argument");
+    int n = 0;
+    HE_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail("he_create: device %d out of range (%d devices)", device, n);
+    hipDeviceProp_t prop;
+    HE_CHECK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail("he_create: device %d is %s; this build targets gfx950 (MI355X)", device, prop.gcnArchName);
+    if (params->max_contacts < 1 || params->max_contacts > HE_MAX_CONTACTS)
+        return fail("he_create: max_contacts must be in [1, %d]", HE_MAX_CONTACTS);
+    if (params->dt <= 0.f) return fail("he_create: dt must be positive");
+    he_engine* h = new he_engine();
+    h->device = device;
+    h->params = *params;
+    *out = h;
+    return 0;
+}
+
+int he_set_model(he_engine* h, const he_model* model) {
+    if (!h || !model) return fail("he_set_model: null argument");
+    if (model->num_bodies != HE_NUM_BODIES || model->num_dof != HE_NUM_DOF)
+        return fail("he_set_model: engine is built for %d bodies / %d dofs (got %d / %d)", HE_NUM_BODIES, HE_NUM_DOF,
+                    model->num_bodies, model->num_dof);
+    if (model->num_pairs < 0 || model->num_pairs > HE_MAX_PAIRS) return fail("he_set_model: bad pair count");
+    if (model->parents[0] != -1) return fail("he_set_model: body 0 must be the root");
+    for (int b = 1; b < HE_NUM_BODIES; ++b)
+        if (model->parents[b] < 0 || model->parents[b] >= b) return fail("he_set_model: bodies must be in DFS order");
+    HE_CHECK(hipSetDevice(h->device));
+    h->model = *model;
+    PhysTopo topo{};
+    he_build_topo(*model, topo);
+    if (topo.nnz > HE_NNZ_MAX) return fail("he_set_model: mass-matrix pattern too large (%d)", topo.nnz);
+    if (!h->d_model) HE_CHECK(dalloc(&h->d_model, 1));
+    if (!h->d_topo) HE_CHECK(dalloc(&h->d_topo, 1));
+    HE_CHECK(hipMemcpy(h->d_model, model, sizeof(he_model), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->d_topo, &topo, sizeof(PhysTopo), hipMemcpyHostToDevice));
+    h->has_model = true;
+    return 0;
+}
+
+int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
+    if (!h) return fail("he_create_envs: null handle");
+    if (!h->has_model) return fail("he_create_envs: call he_set_model first");
+    if (num_envs <= 0) return fail("he_create_envs: num_envs must be positive");
+    if (h->num_envs) return fail("he_create_envs: envs already created");
+    HE_CHECK(hipSetDevice(h->device));
+    const int N = num_envs;
+    HE_CHECK(dalloc(&h->root, (size_t)N * 13));
+    HE_CHECK(dalloc(&h->dof_state, (size_t)N * HE_NUM_DOF * 2));
+    HE_CHECK(dalloc(&h->rb, (size_t)N * HE_NUM_BODIES * 13));
+    HE_CHECK(dalloc(&h->cf, (size_t)N * HE_NUM_BODIES * 3));
+    HE_CHECK(dalloc(&h->dof_force, (size_t)N * HE_NUM_DOF));
+    HE_CHECK(dalloc(&h->targets, (size_t)N * HE_NUM_DOF));
+    HE_CHECK(dalloc(&h->num_contacts, (size_t)N));
+    // humanoid_phc.py:340-347: start pose (x, y) + z 0.89, identity rotation, zero velocity
+    std::vector<float> root((size_t)N * 13, 0.f);
+    for (int e = 0; e < N; ++e) {
+        float* r = &root[(size_t)e * 13];
+        r[0] = host_start_xy ? host_start_xy[2 * e] : 0.f;
+        r[1] = host_start_xy ? host_start_xy[2 * e + 1] : 0.f;
+        r[2] = 0.89f;
+        r[6] = 1.f;
+    }
+    HE_CHECK(hipMemcpy(h->root, root.data(), root.size() * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemset(h->dof_state, 0, (size_t)N * HE_NUM_DOF * 2 * sizeof(float)));
+    HE_CHECK(hipMemset(h->rb, 0, (size_t)N * HE_NUM_BODIES * 13 * sizeof(float)));
+    HE_CHECK(hipMemset(h->cf, 0, (size_t)N * HE_NUM_BODIES * 3 * sizeof(float)));
+    HE_CHECK(hipMemset(h->dof_force, 0, (size_t)N * HE_NUM_DOF * sizeof(float)));
+    HE_CHECK(hipMemset(h->targets, 0, (size_t)N * HE_NUM_DOF * sizeof(float)));
+    HE_CHECK(hipMemset(h->num_contacts, 0, (size_t)N * sizeof(int32_t)));
+    h->num_envs = N;
+    return 0;
+}
+
+int he_destroy(he_engine* h) {
+    if (!h) return 0;
+    hipSetDevice(h->device);
+    void* ptrs[] = {h->d_model, h->d_topo, h->root, h->dof_state, h->rb, h->cf, h->dof_force, h->targets,
+                    h->num_contacts, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
+                    h->m_dt, h->m_starts, h->m_nframes};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    delete h;
+    return 0;
+}
+
+int he_get_buffer(he_engine* h, int kind, void** dptr, int64_t* shape, int* ndim, int* dtype) {
+    if (!h || !dptr || !shape || !ndim || !dtype) return fail("he_get_buffer: null argument");
+    if (!h->num_envs) return fail("he_get_buffer: no envs created");
+    const int64_t N = h->num_envs;
+    *dtype = HE_DTYPE_F32;
+    switch (kind) {
+        case HE_BUF_ROOT_STATE: *dptr = h->root; *ndim = 2; shape[0] = N; shape[1] = 13; break;
+        case HE_BUF_DOF_STATE: *dptr = h->dof_state; *ndim = 2; shape[0] = N * HE_NUM_DOF; shape[1] = 2; break;
+        case HE_BUF_RB_STATE: *dptr = h->rb; *ndim = 2; shape[0] = N * HE_NUM_BODIES; shape[1] = 13; break;
+        case HE_BUF_CONTACT_FORCE: *dptr = h->cf; *ndim = 2; shape[0] = N * HE_NUM_BODIES; shape[1] = 3; break;
+        case HE_BUF_DOF_FORCE: *dptr = h->dof_force; *ndim = 1; shape[0] = N * HE_NUM_DOF; break;
+        case HE_BUF_DOF_TARGET: *dptr = h->targets; *ndim = 2; shape[0] = N; shape[1] = HE_NUM_DOF; break;
+        case HE_BUF_NUM_CONTACTS: *dptr = h->num_contacts; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
+        default: return fail("he_get_buffer: unknown buffer kind %d", kind);
+    }
+    return 0;
+}
+
+int he_set_dof_targets(he_engine* h, const float* src, void* stream) {
+    if (!h || !src) return fail("he_set_dof_targets: null argument");
+    if (src == h->targets) return 0;
+    HE_CHECK(hipMemcpyAsync(h->targets, src, (size_t)h->num_envs * HE_NUM_DOF * sizeof(float),
+                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+namespace {
+__global__ void copy_rows_kernel(float* dst, const float* src, const int32_t* ids, int k, int row, int num_rows) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= k * row) return;
+    int i = t / row, c = t - i * row;
+    int id = ids[i];
+    if (id < 0 || id >= num_rows) return;
+    dst[(size_t)id * row + c] = src[(size_t)id * row + c];
+}
+
+int copy_rows(float* dst, const float* src, const int32_t* ids, int k, int row, int num_rows, void* stream,
+              const char* what) {
+    if (!src || !ids) return fail("%s: null argument", what);
+    if (k < 0) return fail("%s: negative count", what);
+    if (k == 0 || src == dst) return 0;
+    int total = k * row;
+    copy_rows_kernel<<<(total + 255) / 256, 256, 0, (hipStream_t)stream>>>(dst, src, ids, k, row, num_rows);
+    HE_CHECK(hipGetLastError());
+    return 0;
+}
+}  // namespace
+
+int he_set_root_state_indexed(he_engine* h, const float* src, const int32_t* ids, int k, void* stream) {
+    if (!h) return fail("he_set_root_state_indexed: null handle");
+    return copy_rows(h->root, src, ids, k, 13, h->num_envs, stream, "he_set_root_state_indexed");
+}
+int he_set_dof_state_indexed(he_engine* h, const float* src, const int32_t* ids, int k, void* stream) {
+    if (!h) return fail("he_set_dof_state_indexed: null handle");
+    return copy_rows(h->dof_state, src, ids, k, HE_NUM_DOF * 2, h->num_envs, stream, "he_set_dof_state_indexed");
+}
+int he_set_dof_targets_indexed(he_engine* h, const float* src, const int32_t* ids, int k, void* stream) {
+    if (!h) return fail("he_set_dof_targets_indexed: null handle");
+    return copy_rows(h->targets, src, ids, k, HE_NUM_DOF, h->num_envs, stream, "he_set_dof_targets_indexed");
+}
+
+int he_set_env_properties(he_engine* h, const float* mass_scale, const float* friction, const int32_t* terrain_kind) {
+    if (!h) return fail("he_set_env_properties: null handle");
+    h->mass_scale = mass_scale;
+    h->friction = friction;
+    h->terrain_kind = terrain_kind;
+    h->params.terrain = terrain_kind ? 1 : 0;
+    return 0;
+}
+
+int he_set_pd_params(he_engine* h, const float* host_offset, const float* host_scale, const int32_t* host_frozen_mask,
+                     int clip_actions) {
+    if (!h || !host_offset || !host_scale) return fail("he_set_pd_params: null argument");
+    HE_CHECK(hipSetDevice(h->device));
+    if (!h->pd_offset) HE_CHECK(dalloc(&h->pd_offset, HE_NUM_DOF));
+    if (!h->pd_scale) HE_CHECK(dalloc(&h->pd_scale, HE_NUM_DOF));
+    if (!h->frozen) HE_CHECK(dalloc(&h->frozen, HE_NUM_DOF));
+    std::vector<int32_t> fz(HE_NUM_DOF, 0);
+    if (host_frozen_mask) std::memcpy(fz.data(), host_frozen_mask, sizeof(int32_t) * HE_NUM_DOF);
+    HE_CHECK(hipMemcpy(h->pd_offset, host_offset, sizeof(float) * HE_NUM_DOF, hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->pd_scale, host_scale, sizeof(float) * HE_NUM_DOF, hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->frozen, fz.data(), sizeof(int32_t) * HE_NUM_DOF, hipMemcpyHostToDevice));
+    h->clip_actions = clip_actions;
+    h->has_pd = true;
+    return 0;
+}
+
+namespace {
+PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
+    PhysArgs a{};
+    a.p = h->params;
+    a.model = h->d_model;
+    a.topo = h->d_topo;
+    a.root_states = h->root;
+    a.dof_state = h->dof_state;
+    a.dof_targets = h->targets;
+    a.actions = actions;
+    a.pd_offset = h->pd_offset;
+    a.pd_scale = h->pd_scale;
+    a.frozen = h->frozen;
+    a.clip_actions = h->clip_actions;
+    a.rb_state = h->rb;
+    a.contact_forces = h->cf;
+    a.dof_force = h->dof_force;
+    a.num_contacts = h->num_contacts;
+    a.mass_scale = h->mass_scale;
+    a.friction = h->friction;
+    a.terrain_kind = h->terrain_kind;
+    a.num_envs = h->num_envs;
+    a.substeps = substeps;
+    return a;
+}
+}  // namespace
+
+int he_simulate(he_engine* h, int substeps, void* stream) {
+    if (!h || !h->num_envs) return fail("he_simulate: no envs");
+    if (substeps < 1) return fail("he_simulate: substeps must be >= 1");
+    HE_CHECK(launch_physics(phys_args(h, substeps, nullptr), (hipStream_t)stream));
+    return 0;
+}
+
+int he_step_actions(he_engine* h, const float* actions, int substeps, void* stream) {
+    if (!h || !h->num_envs || !actions) return fail("he_step_actions: bad arguments");
+    if (!h->has_pd) return fail("he_step_actions: call he_set_pd_params first");
+    if (substeps < 1) return fail("he_step_actions: substeps must be >= 1");
+    HE_CHECK(launch_physics(phys_args(h, substeps, actions), (hipStream_t)stream));
+    return 0;
+}
+
+int he_refresh(he_engine* h, void* stream) {
+    (void)stream;
+    if (!h) return fail("he_refresh: null handle");
+    return 0;
+}
+
+int he_load_motions(he_engine* h, int64_t F, int M, const float* gts, const float* grs, const float* lrs,
+                    const float* gvs, const float* gavs, const float* dvs, const int64_t* length_starts,
+                    const int64_t* num_frames, const float* lengths, const float* dt) {
+    if (!h) return fail("he_load_motions: null handle");
+    if (F <= 0 || M <= 0 || !gts || !grs || !lrs || !gvs || !gavs || !dvs || !length_starts || !num_frames ||
+        !lengths || !dt)
+        return fail("he_load_motions: bad arguments");
+    for (int i = 0; i < M; ++i) {
+        if (num_frames[i] < 1 || length_starts[i] < 0 || length_starts[i] + num_frames[i] > F)
+            return fail("he_load_motions: motion %d frames [%lld, +%lld) outside the %lld-frame table", i,
+                        (long long)length_starts[i], (long long)num_frames[i], (long long)F);
+    }
+    HE_CHECK(hipSetDevice(h->device));
+    const int B = HE_NUM_BODIES;
+    std::vector<float> hot((size_t)F * B * HE_MOTION_HOT), cold((size_t)F * B * HE_MOTION_COLD, 0.f);
+    for (int64_t f = 0; f < F; ++f)
+        for (int b = 0; b < B; ++b) {
+            float* r = &hot[((size_t)f * B + b) * HE_MOTION_HOT];
+            const size_t i3 = ((size_t)f * B + b) * 3, i4 = ((size_t)f * B + b) * 4;
+            r[0] = gts[i3]; r[1] = gts[i3 + 1]; r[2] = gts[i3 + 2];
+            r[3] = grs[i4]; r[4] = grs[i4 + 1]; r[5] = grs[i4 + 2]; r[6] = grs[i4 + 3];
+            r[7] = gvs[i3]; r[8] = gvs[i3 + 1]; r[9] = gvs[i3 + 2];
+            r[10] = gavs[i3]; r[11] = gavs[i3 + 1]; r[12] = gavs[i3 + 2];
+            float* c = &cold[((size_t)f * B + b) * HE_MOTION_COLD];
+            c[0] = lrs[i4]; c[1] = lrs[i4 + 1]; c[2] = lrs[i4 + 2]; c[3] = lrs[i4 + 3];
+            if (b > 0) {
+                const size_t d3 = ((size_t)f * (B - 1) + b - 1) * 3;
+                c[4] = dvs[d3]; c[5] = dvs[d3 + 1]; c[6] = dvs[d3 + 2];
+            }
+        }
+    void* old[] = {h->m_hot, h->m_cold, h->m_lengths, h->m_dt, h->m_starts, h->m_nframes};
+    for (void* p : old)
+        if (p) HE_CHECK(hipFree(p));
+    HE_CHECK(dalloc(&h->m_hot, hot.size()));
+    HE_CHECK(dalloc(&h->m_cold, cold.size()));
+    HE_CHECK(dalloc(&h->m_lengths, (size_t)M));
+    HE_CHECK(dalloc(&h->m_dt, (size_t)M));
+    HE_CHECK(dalloc(&h->m_starts, (size_t)M));
+    HE_CHECK(dalloc(&h->m_nframes, (size_t)M));
+    HE_CHECK(hipMemcpy(h->m_hot, hot.data(), hot.size() * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_cold, cold.data(), cold.size() * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_lengths, lengths, M * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_dt, dt, M * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_starts, length_starts, M * sizeof(int64_t), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_nframes, num_frames, M * sizeof(int64_t), hipMemcpyHostToDevice));
+    h->m_frames = F;
+    h->m_motions = M;
+    return 0;
+}
+
+namespace {
+MotionDev motion_dev(he_engine* h) {
+    return MotionDev{h->m_hot, h->m_cold, h->m_starts, h->m_nframes, h->m_lengths, h->m_dt};
+}
+
+int imit_common(he_engine* h, const he_imitation_params* p, const he_env_motion* em, ImitArgs& a, const char* what) {
+    if (!h || !p || !em) return fail("%s: null argument", what);
+    if (!h->num_envs) return fail("%s: no envs", what);
+    if (!h->m_motions) return fail("%s: call he_load_motions first", what);
+    if (!em->motion_ids || !em->start_times || !em->start_offsets || !em->global_offset || !em->progress)
+        return fail("%s: he_env_motion has null buffers", what);
+    a = ImitArgs{};
+    a.p = *p;
+    a.m = motion_dev(h);
+    a.root_states = h->root;
+    a.dof_state = h->dof_state;
+    a.rb_state = h->rb;
+    a.contact_forces = h->cf;
+    a.dof_force = h->dof_force;
+    a.dof_targets = h->targets;
+    a.motion_ids = em->motion_ids;
+    a.start_times = em->start_times;
+    a.start_offsets = em->start_offsets;
+    a.global_offset = em->global_offset;
+    a.progress = em->progress;
+    return 0;
+}
+}  // namespace
+
+int he_imitation_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, float* obs, float* rew,
+                      float* reward_raw, uint8_t* reset, uint8_t* terminate, void* stream) {
+    ImitArgs a;
+    if (imit_common(h, p, em, a, "he_imitation_step")) return 1;
+    if (!obs || !rew || !reward_raw || !reset || !terminate) return fail("he_imitation_step: null output");
+    a.obs = obs; a.rew = rew; a.reward_raw = reward_raw; a.reset = reset; a.terminate = terminate;
+    a.count = h->num_envs;
+    a.mode = 0;
+    HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    return 0;
+}
+
+int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motion* em, const int32_t* env_ids, int k,
+                  const float* phases, float* obs, uint8_t* reset, uint8_t* terminate, void* stream) {
+    ImitArgs a;
+    if (imit_common(h, p, em, a, "he_reset_envs")) return 1;
+    if (k < 0) return fail("he_reset_envs: negative count");
+    if (k == 0) return 0;
+    if (!env_ids || !phases || !obs || !reset || !terminate) return fail("he_reset_envs: null argument");
+    a.obs = obs; a.reset = reset; a.terminate = terminate;
+    a.env_ids = env_ids;
+    a.count = k;
+    a.phases = phases;
+    a.mode = 2;
+    HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    return 0;
+}
+
+int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, const float* actions,
+                int substeps, uint64_t seed, uint64_t step_index, float* obs, float* rew, float* reward_raw,
+                uint8_t* reset, uint8_t* terminate, void* stream) {
+    if (he_step_actions(h, actions, substeps, stream)) return 1;
+    return he_imitation_reset_step(h, p, em, seed, step_index, obs, rew, reward_raw, reset, terminate, stream);
+}
+
+int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, uint64_t seed,
+                            uint64_t step_index, float* obs, float* rew, float* reward_raw, uint8_t* reset,
+                            uint8_t* terminate, void* stream) {
+    ImitArgs a;
+    if (imit_common(h, p, em, a, "he_imitation_reset_step")) return 1;
+    if (!obs || !rew || !reward_raw || !reset || !terminate) return fail("he_imitation_reset_step: null output");
+    a.obs = obs; a.rew = rew; a.reward_raw = reward_raw; a.reset = reset; a.terminate = terminate;
+    a.count = h->num_envs;
+    a.mode = 1;
+    a.seed = seed;
+    a.step = step_index;
+    HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    return 0;
+}
+
+int he_motion_state(he_engine* h, int k, const int64_t* ids, const float* times, const float* offset, float* rg_pos,
+                    float* rb_rot, float* body_vel, float* body_ang_vel, float* dof_pos, float* dof_vel, void* stream) {
+    if (!h) return fail("he_motion_state: null handle");
+    if (!h->m_motions) return fail("he_motion_state: call he_load_motions first");
+    if (k < 0 || (k > 0 && (!ids || !times))) return fail("he_motion_state: bad arguments");
+    MotionStateArgs a{};
+    a.m = motion_dev(h);
+    a.k = k;
+    a.ids = ids;
+    a.times = times;
+    a.offset = offset;
+    a.rg_pos = rg_pos; a.rb_rot = rb_rot; a.body_vel = body_vel; a.body_ang_vel = body_ang_vel;
+    a.dof_pos = dof_pos; a.dof_vel = dof_vel;
+    HE_CHECK(launch_motion_state(a, (hipStream_t)stream));
+    return 0;
+}
+
+float he_hash_uniform(uint64_t seed, uint64_t step, uint32_t env) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ull ^ (step + 0x632BE59BD9B4E019ull) * 0xBF58476D1CE4E5B9ull ^
+                 ((uint64_t)env + 0x2545F4914F6CDD1Dull) * 0x94D049BB133111EBull;
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+}  // extern "C"

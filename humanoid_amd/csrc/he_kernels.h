@@ -1,0 +1,82 @@
+// he_kernels.h -- kernel argument blocks and launchers shared by the engine TU and kernel TUs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/humanoid_engine.h"
+#include "he_topo.h"
+
+#define HE_MOTION_HOT 13   // per body: pos3 rot4 vel3 angvel3 (same layout as a rigid-body row)
+#define HE_MOTION_COLD 8   // per body: local rot4, dof vel3, pad
+
+// device motion library: interleaved per-frame records
+struct MotionDev {
+    const float* hot;             // [F][24][13]
+    const float* cold;            // [F][24][8]
+    const int64_t* length_starts; // [M]
+    const int64_t* num_frames;    // [M]
+    const float* lengths;         // [M]
+    const float* dt;              // [M]
+};
+
+struct ImitArgs {
+    he_imitation_params p;
+    MotionDev m;
+    float* root_states;      // [N,13]
+    float* dof_state;        // [N,69,2]
+    float* rb_state;         // [N,24,13]
+    float* contact_forces;   // [N,24,3]
+    const float* dof_force;  // [N,69]
+    float* dof_targets;      // [N,69]
+    const int64_t* motion_ids;
+    float* start_times;
+    float* start_offsets;
+    float* global_offset;
+    int16_t* progress;
+    float* obs;
+    float* rew;
+    float* reward_raw;
+    uint8_t* reset;
+    uint8_t* terminate;
+    const int32_t* env_ids;  // null = all envs [0, count)
+    int count;
+    int mode;                // 0 step, 1 step + fused device reset, 2 reset listed envs
+    const float* phases;     // mode 2: [count]
+    uint64_t seed, step;
+};
+
+struct MotionStateArgs {
+    MotionDev m;
+    int k;
+    const int64_t* ids;
+    const float* times;
+    const float* offset;
+    float *rg_pos, *rb_rot, *body_vel, *body_ang_vel, *dof_pos, *dof_vel;
+};
+
+struct PhysArgs {
+    he_sim_params p;
+    const he_model* model;   // device copy
+    const PhysTopo* topo;    // device copy
+    float* root_states;
+    float* dof_state;
+    float* dof_targets;
+    const float* actions;    // non-null: targets = offset + scale*clip(a) (frozen dofs 0) first
+    const float* pd_offset;  // [69]
+    const float* pd_scale;   // [69]
+    const int32_t* frozen;   // [69]
+    int clip_actions;
+    float* rb_state;
+    float* contact_forces;
+    float* dof_force;
+    int32_t* num_contacts;
+    const float* mass_scale;     // [N,24] or null
+    const float* friction;       // [N] or null
+    const int32_t* terrain_kind; // [N] or null
+    int num_envs;
+    int substeps;
+};
+
+hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream);
+hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream);
+hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);

@@ -1,0 +1,217 @@
+/*
+ * humanoid_engine.h -- C ABI of libhumanoid_engine.so, the MI355X (gfx950) batched SMPL-humanoid
+ * rollout engine that replaces Isaac Gym/PhysX + gymtorch under puffer-phc.
+ *
+ * Conventions
+ *   - every entry point returns 0 on success, non-zero on failure; he_last_error() gives the text
+ *     (the gymtorch C++ it replaces printf'ed and returned an empty tensor,
+ *      packages/gymtorch/gymtorch/gymtorch.cpp:40-51,114-117; the Python shim raises instead);
+ *   - all float/int pointers passed to compute entry points are DEVICE pointers on the handle's
+ *     device; `stream` is a hipStream_t (NULL = default stream); nothing here synchronises the host;
+ *   - quaternions are xyzw (puffer_phc/torch_utils.py:61), Z-up, gravity -9.81 z
+ *     (puffer_phc/envs/isaacgym_env.py:29-33).
+ *
+ * Each entry point cites the reference interface it replaces (paths under packages/puffer-phc/
+ * unless noted). Isaac Gym's own binary is not vendored; the cited lines are its call sites.
+ */
+#ifndef HUMANOID_ENGINE_H
+#define HUMANOID_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HE_NUM_BODIES 24
+#define HE_NUM_DOF 69
+#define HE_NUM_GEN 75          /* 6 root + 69 joint generalized velocities */
+#define HE_MAX_PAIRS 256
+#define HE_MAX_CONTACTS 32
+#define HE_OBS_SELF 358
+#define HE_OBS_TASK 576
+#define HE_OBS_DIM 934         /* humanoid_phc.py:458-467 */
+#define HE_REWARD_RAW 5        /* 4 imitation terms + power, humanoid_phc.py:562-569 */
+
+/* geometry kinds (one geom per body, assets/smpl_humanoid.xml:27-168) */
+#define HE_GEOM_SPHERE 0
+#define HE_GEOM_CAPSULE 1
+#define HE_GEOM_BOX 2
+
+/* Model blob: what gym.load_asset + get_asset_dof_properties + create_actor give the reference
+ * (humanoid_phc.py:211-230, 276-324, 370-381). Built on the host from the MJCF. */
+typedef struct he_model {
+    int32_t num_bodies, num_dof, num_pairs, reserved;
+    int32_t parents[HE_NUM_BODIES];
+    int32_t geom_type[HE_NUM_BODIES];
+    float local_pos[HE_NUM_BODIES][3];   /* joint offset in parent frame */
+    float mass[HE_NUM_BODIES];
+    float com[HE_NUM_BODIES][3];         /* body frame */
+    float inertia[HE_NUM_BODIES][6];     /* about COM, body frame: xx yy zz xy xz yz */
+    float geom_params[HE_NUM_BODIES][10];
+    float geom_radius[HE_NUM_BODIES];
+    float stiffness[HE_NUM_DOF], damping[HE_NUM_DOF], armature[HE_NUM_DOF], effort[HE_NUM_DOF];
+    int32_t pairs[HE_MAX_PAIRS][2];      /* self-collision candidate pairs */
+} he_model;
+
+/* Simulation parameters: isaacgym_env.py:6-35 + asset options humanoid_phc.py:211-214. */
+typedef struct he_sim_params {
+    float dt;                        /* 1/60 */
+    float gravity[3];                /* 0 0 -9.81 */
+    float contact_offset;            /* 0.02 */
+    float friction;                  /* 1.0 (plane static=dynamic=1, humanoid_phc.py:259-260) */
+    float baumgarte;                 /* penetration recovery fraction per substep */
+    float max_depenetration_velocity;/* 10 */
+    float angular_damping;           /* 0.01 */
+    float max_angular_velocity;      /* 100 */
+    int32_t solver_iterations;       /* PGS sweeps per substep */
+    int32_t self_collision;          /* 1 = has_self_collision (config.py:57) */
+    int32_t max_contacts;            /* <= HE_MAX_CONTACTS */
+    float kp_scale, kd_scale;        /* config.py:106-107 */
+    int32_t terrain;                 /* 0 plane everywhere, 1 per-env terrain kind (config 5) */
+    float terrain_slope;             /* radians, terrain kind 1 */
+    float step_height, step_length;  /* terrain kind 2 (box steps along +x) */
+} he_sim_params;
+
+/* Imitation (reward / reset / obs) parameters: config.py:37-50, 97-112; humanoid_phc.py:1230-1335. */
+typedef struct he_imitation_params {
+    float k_pos, k_rot, k_vel, k_ang_vel;
+    float w_pos, w_rot, w_vel, w_ang_vel;
+    float power_coef;                /* rew_power_coef 0.0005 */
+    int32_t use_power_reward;        /* 1 */
+    float control_dt;                /* isaac_base.dt = 2 * 1/60 */
+    int32_t enable_early_termination;/* 1 */
+    int32_t eval_mode;               /* flag_im_eval: mean-distance termination */
+    int32_t reset_body_mask;         /* bit b set = body b in _reset_bodies_id */
+    float term_dist[HE_NUM_BODIES];  /* _termination_distances */
+} he_imitation_params;
+
+/* Buffer kinds (humanoid_phc.py:497-554, the tensors gymtorch.wrap_tensor exposed). */
+typedef enum he_buf_kind {
+    HE_BUF_ROOT_STATE = 0,     /* f32 [N,13]  pos3 quat4 linvel3 angvel3  (acquire_actor_root_state_tensor) */
+    HE_BUF_DOF_STATE = 1,      /* f32 [N*69,2] (pos, vel)                 (acquire_dof_state_tensor) */
+    HE_BUF_RB_STATE = 2,       /* f32 [N*24,13]                           (acquire_rigid_body_state_tensor) */
+    HE_BUF_CONTACT_FORCE = 3,  /* f32 [N*24,3]                            (acquire_net_contact_force_tensor) */
+    HE_BUF_DOF_FORCE = 4,      /* f32 [N*69]                              (acquire_dof_force_tensor) */
+    HE_BUF_DOF_TARGET = 5,     /* f32 [N,69]  position targets            (set_dof_position_target_tensor) */
+    HE_BUF_NUM_CONTACTS = 6,   /* i32 [N]     contacts used last substep  (diagnostic) */
+    HE_BUF_COUNT = 7
+} he_buf_kind;
+
+#define HE_DTYPE_F32 1   /* GymTensor.h:23 eGymDataTypeFp32 */
+#define HE_DTYPE_I32 2   /* GymTensor.h:24 eGymDataTypeUint32 (torch int32) */
+
+typedef struct he_engine he_engine;
+
+const char* he_last_error(void);
+int he_version(void);
+int he_device_count(int* count);
+
+/* gymapi.acquire_gym + create_sim (isaacgym_env.py:48-50): bind a HIP device, copy params. */
+int he_create(const he_sim_params* params, int device, he_engine** out);
+/* gym.load_asset (humanoid_phc.py:216); the host parses the MJCF into the blob. */
+int he_set_model(he_engine* h, const he_model* model);
+/* create_env/create_actor x N + prepare_sim (humanoid_phc.py:264-326, :74): allocates the state
+ * tensors, places actors at (start_xy, 0.89) with identity rotation (humanoid_phc.py:340-347). */
+int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy);
+/* gym.destroy_sim (isaacgym_env.py:99) */
+int he_destroy(he_engine* h);
+
+/* acquire_*_tensor (humanoid_phc.py:499-504): device pointer + shape of an engine-owned buffer.
+ * The memory stays owned by the engine (non-owning wrap, gymtorch.cpp:90). */
+int he_get_buffer(he_engine* h, int kind, void** dptr, int64_t* shape, int* ndim, int* dtype);
+
+/* set_dof_position_target_tensor (humanoid_phc.py:127-128): device-to-device copy of [N,69]. */
+int he_set_dof_targets(he_engine* h, const float* src, void* stream);
+/* set_{actor_root_state,dof_state,dof_position_target}_tensor_indexed (humanoid_phc.py:750-767):
+ * rows `ids[0..k)` (int32 actor ids = env ids, one actor per env) are copied from the full-size
+ * source tensor into the engine state. */
+int he_set_root_state_indexed(he_engine* h, const float* src, const int32_t* ids, int k, void* stream);
+int he_set_dof_state_indexed(he_engine* h, const float* src, const int32_t* ids, int k, void* stream);
+int he_set_dof_targets_indexed(he_engine* h, const float* src, const int32_t* ids, int k, void* stream);
+
+/* Per-env domain randomisation (config 5; the reference removed it, humanoid_phc.py:349):
+ * body mass scale [N,24] and friction [N], terrain kind [N] (0 plane, 1 slope, 2 steps).
+ * NULL disables the corresponding array. Device pointers, owned by the caller. */
+int he_set_env_properties(he_engine* h, const float* mass_scale, const float* friction,
+                          const int32_t* terrain_kind);
+
+/* gym.simulate x substeps + fetch_results (humanoid_phc.py:131-134): articulated rigid-body step
+ * with implicit PD drives, ground + self contacts and a PGS contact solve; updates every state
+ * buffer (root, dof, rigid-body, contact force, dof force). One kernel launch. */
+int he_simulate(he_engine* h, int substeps, void* stream);
+/* action -> PD target (humanoid_phc.py:1218-1228, freeze hand/toe :116-125) fused into the step:
+ * target = offset + scale*clip(a,-1,1) (frozen dofs 0), then he_simulate. */
+int he_set_pd_params(he_engine* h, const float* host_offset, const float* host_scale,
+                     const int32_t* host_frozen_mask, int clip_actions);
+int he_step_actions(he_engine* h, const float* actions, int substeps, void* stream);
+/* refresh_*_tensor (humanoid_phc.py:782-789): buffers are the live engine state, nothing to copy;
+ * kept for API parity (no FK recompute: rigid-body rows written by the caller after a reset stay,
+ * as the reference relies on, humanoid_phc.py:922-931). */
+int he_refresh(he_engine* h, void* stream);
+
+/* ---------------- motion library + fused imitation kernel (A5-A9) ---------------------- */
+/* MotionLibBase.load_motions table upload (motion_lib.py:396-420). Host pointers; the engine
+ * re-lays the frames out as interleaved per-frame records in device memory.
+ * gts/gvs/gavs [F,24,3], grs/lrs [F,24,4], dvs [F,23,3]; per-motion arrays [M]. */
+int he_load_motions(he_engine* h, int64_t num_frames_total, int num_motions,
+                    const float* gts, const float* grs, const float* lrs, const float* gvs,
+                    const float* gavs, const float* dvs, const int64_t* length_starts,
+                    const int64_t* num_frames, const float* lengths, const float* dt);
+
+/* Per-env motion bookkeeping buffers (device, caller-owned, all [N] unless noted):
+ * motion_ids i64, start_times f32, start_offsets f32, global_offset f32 [N,3], progress i16. */
+typedef struct he_env_motion {
+    const int64_t* motion_ids;
+    float* start_times;
+    float* start_offsets;
+    float* global_offset;
+    int16_t* progress;
+} he_env_motion;
+
+/* Post-physics half of HumanoidPHC.step (humanoid_phc.py:138-149): progress += 1, then
+ * _compute_reward (:1230-1305), _compute_reset (:1313-1335) and _compute_observations
+ * (:937-961) for all envs, in one launch. Outputs: obs [N,934], rew [N], reward_raw [N,5],
+ * reset u8 [N], terminate u8 [N]. */
+int he_imitation_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em,
+                      float* obs, float* rew, float* reward_raw, uint8_t* reset, uint8_t* terminate,
+                      void* stream);
+
+/* MotionLibBase.get_motion_state (motion_lib.py:549-626) for K queries (device arrays):
+ * ids i64 [K], times f32 [K], offset f32 [K,3] or NULL. Outputs (device, nullable):
+ * rg_pos [K,24,3], rb_rot [K,24,4], body_vel [K,24,3], body_ang_vel [K,24,3],
+ * dof_pos [K,69], dof_vel [K,69]. */
+int he_motion_state(he_engine* h, int k, const int64_t* ids, const float* times, const float* offset,
+                    float* rg_pos, float* rb_rot, float* body_vel, float* body_ang_vel,
+                    float* dof_pos, float* dof_vel, void* stream);
+
+/* _reset_ref_state_init + _reset_env_tensors + _compute_observations(env_ids)
+ * (humanoid_phc.py:694-731, 747-780, 937-961): for env ids [k] (int32), motion time
+ * t = floor(phase*len/(1/30))*(1/30) (motion_lib.py:526-535) with `phases` f32 [k] uniform [0,1);
+ * writes root/dof/rigid-body state, dof targets := dof_pos, zero contact forces, progress = 0,
+ * start_times = t, start_offsets = 0, global_offset = 0, and the k obs rows. */
+int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motion* em,
+                  const int32_t* env_ids, int k, const float* phases, float* obs, uint8_t* reset,
+                  uint8_t* terminate, void* stream);
+
+/* Fully device-side env step used by the rollout path (no host sync): actions -> PD targets ->
+ * physics -> reward/reset/obs -> device reset of flagged envs (phases from a counter-based hash
+ * of (seed, step, env)) -> obs for reset envs. */
+int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em,
+                const float* actions, int substeps, uint64_t seed, uint64_t step_index,
+                float* obs, float* rew, float* reward_raw, uint8_t* reset, uint8_t* terminate,
+                void* stream);
+
+/* Second half of he_env_step on its own (after he_step_actions): reward/reset/obs with the device
+ * reset of flagged envs. he_env_step == he_step_actions + he_imitation_reset_step. */
+int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, uint64_t seed,
+                            uint64_t step_index, float* obs, float* rew, float* reward_raw, uint8_t* reset,
+                            uint8_t* terminate, void* stream);
+
+/* hash-based uniform used by he_env_step (exposed for parity tests): out[k] for env ids[k]. */
+float he_hash_uniform(uint64_t seed, uint64_t step_index, uint32_t env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HUMANOID_ENGINE_H */

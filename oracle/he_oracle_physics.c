@@ -1,0 +1,724 @@
+/*
+ * he_oracle_physics.c -- TEST INFRASTRUCTURE ONLY (see he_oracle.c header).
+ *
+ * Scalar fp64 reference of the engine's articulated-body step. It replaces
+ * gym.simulate (puffer_phc/envs/humanoid_phc.py:131-134) whose PhysX implementation is closed
+ * and absent: PHYSICS PARITY VS ISAAC GYM IS UNPINNED. Constants follow
+ * puffer_phc/envs/isaacgym_env.py:6-35 (dt 1/60, gravity, contact offset 0.02, max depenetration
+ * 10), asset options humanoid_phc.py:211-214 (angular damping 0.01, max angular velocity 100),
+ * PD drives humanoid_phc.py:276-280 and the self-collision filter humanoid_phc.py:370-381.
+ *
+ * Algorithm per substep (generalized velocity u = [w_root(3), v_root(3), joint(69)],
+ * joint velocity = relative angular velocity in the child frame, joint position = exp map):
+ *   FK -> spatial axes S about the root origin o -> RNEA bias (gravity + Coriolis)
+ *   -> CRBA mass matrix + armature -> implicit PD (effort-saturated dofs explicit)
+ *   -> branch-induced sparse LTDL factorisation -> free velocity
+ *   -> ground + self contacts (speculative within contact_offset) -> Delassus A = Z^T D^-1 Z
+ *      with Z = L^-T J^T -> projected Gauss-Seidel (pyramidal friction) -> velocity update
+ *   -> damping / clamps -> semi-implicit position update.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/humanoid_engine.h"
+
+typedef double R;
+#define NB HE_NUM_BODIES
+#define ND HE_NUM_DOF
+#define NG HE_NUM_GEN
+#define MAXC HE_MAX_CONTACTS
+#define MAXROW (3 * MAXC)
+
+typedef struct topo {
+    int dof_parent[NG];
+    int dof_body[NG];
+    int body_dof0[NB];
+    int is_anc[NB][NB]; /* is_anc[a][b]: a is ancestor-or-self of b */
+} topo;
+
+static void build_topo(const he_model* m, topo* t) {
+    for (int i = 0; i < 6; ++i) { t->dof_parent[i] = i - 1; t->dof_body[i] = 0; }
+    t->body_dof0[0] = 0;
+    for (int b = 1; b < NB; ++b) {
+        int d0 = 6 + 3 * (b - 1);
+        t->body_dof0[b] = d0;
+        int p = m->parents[b];
+        int plast = p == 0 ? 5 : 6 + 3 * (p - 1) + 2;
+        for (int c = 0; c < 3; ++c) {
+            t->dof_parent[d0 + c] = c == 0 ? plast : d0 + c - 1;
+            t->dof_body[d0 + c] = b;
+        }
+    }
+    memset(t->is_anc, 0, sizeof(t->is_anc));
+    for (int b = 0; b < NB; ++b)
+        for (int a = b; a >= 0; a = m->parents[a]) { t->is_anc[a][b] = 1; if (a == 0) break; }
+}
+
+/* ---------------------------------------------------------------- small math */
+static inline R dot3(const R* a, const R* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void cross3(const R* a, const R* b, R* o) {
+    R x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static void qmul(const R* a, const R* b, R* o) { /* Hamilton, xyzw */
+    R x = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    R y = a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0];
+    R z = a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3];
+    R w = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    o[0] = x; o[1] = y; o[2] = z; o[3] = w;
+}
+static void qnormalize(R* q) {
+    R n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    if (n < 1e-12) { q[0] = q[1] = q[2] = 0; q[3] = 1; return; }
+    for (int i = 0; i < 4; ++i) q[i] /= n;
+}
+static void qexp(const R* v, R* q) { /* rotation vector -> unit quaternion */
+    R th = sqrt(dot3(v, v));
+    if (th < 1e-8) { q[0] = 0.5 * v[0]; q[1] = 0.5 * v[1]; q[2] = 0.5 * v[2]; q[3] = 1; qnormalize(q); return; }
+    R s = sin(0.5 * th) / th;
+    q[0] = v[0] * s; q[1] = v[1] * s; q[2] = v[2] * s; q[3] = cos(0.5 * th);
+}
+static void qlog(const R* qin, R* v) { /* minimal rotation vector, |angle| <= pi */
+    R q[4] = {qin[0], qin[1], qin[2], qin[3]};
+    if (q[3] < 0) for (int i = 0; i < 4; ++i) q[i] = -q[i];
+    R s = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+    if (s < 1e-8) { v[0] = 2 * q[0]; v[1] = 2 * q[1]; v[2] = 2 * q[2]; return; }
+    R th = 2 * atan2(s, q[3]);
+    v[0] = q[0] / s * th; v[1] = q[1] / s * th; v[2] = q[2] / s * th;
+}
+static void qmat(const R* q, R m[3][3]) {
+    R x = q[0], y = q[1], z = q[2], w = q[3];
+    m[0][0] = 1 - 2 * (y * y + z * z); m[0][1] = 2 * (x * y - z * w); m[0][2] = 2 * (x * z + y * w);
+    m[1][0] = 2 * (x * y + z * w); m[1][1] = 1 - 2 * (x * x + z * z); m[1][2] = 2 * (y * z - x * w);
+    m[2][0] = 2 * (x * z - y * w); m[2][1] = 2 * (y * z + x * w); m[2][2] = 1 - 2 * (x * x + y * y);
+}
+static inline void matvec(R m[3][3], const R* v, R* o) {
+    R a = m[0][0] * v[0] + m[0][1] * v[1] + m[0][2] * v[2];
+    R b = m[1][0] * v[0] + m[1][1] * v[1] + m[1][2] * v[2];
+    R c = m[2][0] * v[0] + m[2][1] * v[1] + m[2][2] * v[2];
+    o[0] = a; o[1] = b; o[2] = c;
+}
+
+/* spatial inertia about o: (m, h = m*(c-o), I3 about o) ; f = I V with V = (w, v):
+ *   n = I3 w + h x v ;  f = m v - h x w */
+typedef struct sinertia { R m, h[3], I[3][3]; } sinertia;
+static void si_apply(const sinertia* I, const R* V, R* F) {
+    R hv[3], hw[3];
+    cross3(I->h, V + 3, hv);
+    cross3(I->h, V, hw);
+    for (int r = 0; r < 3; ++r) {
+        F[r] = I->I[r][0] * V[0] + I->I[r][1] * V[1] + I->I[r][2] * V[2] + hv[r];
+        F[3 + r] = I->m * V[3 + r] - hw[r];
+    }
+}
+static void si_add(sinertia* a, const sinertia* b) {
+    a->m += b->m;
+    for (int r = 0; r < 3; ++r) { a->h[r] += b->h[r]; for (int c = 0; c < 3; ++c) a->I[r][c] += b->I[r][c]; }
+}
+/* motion cross: V x W */
+static void crm(const R* V, const R* W, R* O) {
+    R a[3], b[3], c[3];
+    cross3(V, W, a);
+    cross3(V, W + 3, b);
+    cross3(V + 3, W, c);
+    for (int i = 0; i < 3; ++i) { O[i] = a[i]; O[3 + i] = b[i] + c[i]; }
+}
+/* force cross: V x* F */
+static void crf(const R* V, const R* F, R* O) {
+    R a[3], b[3], c[3];
+    cross3(V, F, a);
+    cross3(V + 3, F + 3, b);
+    cross3(V, F + 3, c);
+    for (int i = 0; i < 3; ++i) { O[i] = a[i] + b[i]; O[3 + i] = c[i]; }
+}
+
+/* ---------------------------------------------------------------- env state */
+typedef struct env_state {
+    R root_pos[3], root_q[4], root_v[3], root_w[3];
+    R q[ND], u[ND], target[ND];
+} env_state;
+
+typedef struct kin {
+    R qw[NB][4];     /* body world rotation */
+    R Rw[NB][3][3];
+    R pw[NB][3];     /* body origin */
+    R o[3];
+    R S[NG][6];
+    R V[NB][6];
+} kin;
+
+static void kinematics(const he_model* m, const topo* t, const env_state* s, kin* k) {
+    memcpy(k->qw[0], s->root_q, sizeof(R) * 4);
+    qnormalize(k->qw[0]);
+    memcpy(k->pw[0], s->root_pos, sizeof(R) * 3);
+    qmat(k->qw[0], k->Rw[0]);
+    for (int b = 1; b < NB; ++b) {
+        int p = m->parents[b];
+        R ql[4], lp[3] = {m->local_pos[b][0], m->local_pos[b][1], m->local_pos[b][2]}, off[3];
+        qexp(&s->q[3 * (b - 1)], ql);
+        qmul(k->qw[p], ql, k->qw[b]);
+        qmat(k->qw[b], k->Rw[b]);
+        matvec(k->Rw[p], lp, off);
+        for (int c = 0; c < 3; ++c) k->pw[b][c] = k->pw[p][c] + off[c];
+    }
+    memcpy(k->o, k->pw[0], sizeof(R) * 3);
+    memset(k->S, 0, sizeof(k->S));
+    for (int c = 0; c < 3; ++c) { k->S[c][c] = 1; k->S[3 + c][3 + c] = 1; }
+    for (int b = 1; b < NB; ++b) {
+        R r[3] = {k->pw[b][0] - k->o[0], k->pw[b][1] - k->o[1], k->pw[b][2] - k->o[2]};
+        for (int c = 0; c < 3; ++c) {
+            R a[3] = {k->Rw[b][0][c], k->Rw[b][1][c], k->Rw[b][2][c]}, l[3];
+            cross3(r, a, l);
+            R* S = k->S[t->body_dof0[b] + c];
+            S[0] = a[0]; S[1] = a[1]; S[2] = a[2]; S[3] = l[0]; S[4] = l[1]; S[5] = l[2];
+        }
+    }
+    /* body spatial velocities about o */
+    k->V[0][0] = s->root_w[0]; k->V[0][1] = s->root_w[1]; k->V[0][2] = s->root_w[2];
+    k->V[0][3] = s->root_v[0]; k->V[0][4] = s->root_v[1]; k->V[0][5] = s->root_v[2];
+    for (int b = 1; b < NB; ++b) {
+        int p = m->parents[b];
+        for (int i = 0; i < 6; ++i) k->V[b][i] = k->V[p][i];
+        for (int c = 0; c < 3; ++c) {
+            R uu = s->u[3 * (b - 1) + c];
+            for (int i = 0; i < 6; ++i) k->V[b][i] += k->S[t->body_dof0[b] + c][i] * uu;
+        }
+    }
+}
+
+static void body_inertia(const he_model* m, const kin* k, int b, R mass_scale, sinertia* I) {
+    R mass = m->mass[b] * mass_scale;
+    R com[3] = {m->com[b][0], m->com[b][1], m->com[b][2]}, cw[3];
+    matvec((R(*)[3])k->Rw[b], com, cw);
+    R s[3] = {k->pw[b][0] + cw[0] - k->o[0], k->pw[b][1] + cw[1] - k->o[1], k->pw[b][2] + cw[2] - k->o[2]};
+    const float* in = m->inertia[b];
+    R Ib[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
+    R tmp[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            R acc = 0;
+            for (int x = 0; x < 3; ++x) acc += k->Rw[b][r][x] * Ib[x][c];
+            tmp[r][c] = acc;
+        }
+    R ss = dot3(s, s);
+    I->m = mass;
+    for (int r = 0; r < 3; ++r) {
+        I->h[r] = mass * s[r];
+        for (int c = 0; c < 3; ++c) {
+            R acc = 0;
+            for (int x = 0; x < 3; ++x) acc += tmp[r][x] * k->Rw[b][c][x];
+            I->I[r][c] = acc * mass_scale + mass * ((r == c ? ss : 0) - s[r] * s[c]);
+        }
+    }
+}
+
+/* ---------------------------------------------------------------- contacts */
+typedef struct contact {
+    int b0, b1;       /* b1 = -1 for terrain */
+    R x[3], n[3], t1[3], t2[3];
+    R gap;
+    R mu;
+} contact;
+
+static R terrain_height(const he_sim_params* p, int kind, const R* x, R* n) {
+    /* returns signed distance of x to the terrain surface along its normal n */
+    if (kind == 1) {
+        R s = sin(p->terrain_slope), c = cos(p->terrain_slope);
+        n[0] = -s; n[1] = 0; n[2] = c;
+        return dot3(n, x);
+    }
+    n[0] = 0; n[1] = 0; n[2] = 1;
+    if (kind == 2) {
+        R h = 0;
+        if (x[0] > 0) h = p->step_height * floor(x[0] / p->step_length);
+        return x[2] - h;
+    }
+    return x[2];
+}
+
+static void friction_basis(const R* n, R* t1, R* t2) {
+    R a[3] = {1, 0, 0};
+    if (fabs(n[0]) > 0.9) { a[0] = 0; a[1] = 1; }
+    R d = dot3(a, n);
+    for (int i = 0; i < 3; ++i) t1[i] = a[i] - d * n[i];
+    R l = sqrt(dot3(t1, t1));
+    for (int i = 0; i < 3; ++i) t1[i] /= l;
+    cross3(n, t1, t2);
+}
+
+static void body_point(const kin* k, int b, const R* local, R* out) {
+    R w[3];
+    matvec((R(*)[3])k->Rw[b], local, w);
+    for (int i = 0; i < 3; ++i) out[i] = k->pw[b][i] + w[i];
+}
+
+/* body collision proxy: segment (a, b) and radius */
+static void body_segment(const he_model* m, const kin* k, int b, R* a, R* c, R* r) {
+    const float* g = m->geom_params[b];
+    if (m->geom_type[b] == HE_GEOM_SPHERE) {
+        R l[3] = {g[0], g[1], g[2]};
+        body_point(k, b, l, a);
+        memcpy(c, a, sizeof(R) * 3);
+        *r = g[3];
+    } else if (m->geom_type[b] == HE_GEOM_CAPSULE) {
+        R l0[3] = {g[0], g[1], g[2]}, l1[3] = {g[3], g[4], g[5]};
+        body_point(k, b, l0, a);
+        body_point(k, b, l1, c);
+        *r = g[6];
+    } else { /* box -> capsule proxy along its longest axis */
+        R e[3] = {g[3], g[4], g[5]};
+        int ax = 0;
+        if (e[1] > e[ax]) ax = 1;
+        if (e[2] > e[ax]) ax = 2;
+        R rp = m->geom_radius[b];
+        R half = e[ax] - rp;
+        if (half < 0) half = 0;
+        R bq[4] = {g[6], g[7], g[8], g[9]}, bm[3][3];
+        qmat(bq, bm);
+        R dir[3] = {bm[0][ax] * half, bm[1][ax] * half, bm[2][ax] * half};
+        R l0[3] = {g[0] - dir[0], g[1] - dir[1], g[2] - dir[2]}, l1[3] = {g[0] + dir[0], g[1] + dir[1], g[2] + dir[2]};
+        body_point(k, b, l0, a);
+        body_point(k, b, l1, c);
+        *r = rp;
+    }
+}
+
+/* closest points between segments p1q1 and p2q2 (Ericson, RTCD 5.1.9) */
+static void seg_seg(const R* p1, const R* q1, const R* p2, const R* q2, R* c1, R* c2) {
+    R d1[3], d2[3], r[3];
+    for (int i = 0; i < 3; ++i) { d1[i] = q1[i] - p1[i]; d2[i] = q2[i] - p2[i]; r[i] = p1[i] - p2[i]; }
+    R a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    R s, t;
+    const R eps = 1e-12;
+    if (a <= eps && e <= eps) { s = t = 0; }
+    else if (a <= eps) { s = 0; t = f / e; t = t < 0 ? 0 : (t > 1 ? 1 : t); }
+    else {
+        R c = dot3(d1, r);
+        if (e <= eps) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+        else {
+            R b = dot3(d1, d2), den = a * e - b * b;
+            s = den > eps ? (b * f - c * e) / den : 0;
+            s = s < 0 ? 0 : (s > 1 ? 1 : s);
+            t = (b * s + f) / e;
+            if (t < 0) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+            else if (t > 1) { t = 1; s = (b - c) / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+        }
+    }
+    for (int i = 0; i < 3; ++i) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
+}
+
+static int add_contact(contact* cs, int nc, int maxc, int b0, int b1, const R* x, const R* n, R gap, R mu) {
+    if (nc >= maxc) return nc;
+    contact* c = &cs[nc];
+    c->b0 = b0; c->b1 = b1;
+    memcpy(c->x, x, sizeof(R) * 3);
+    memcpy(c->n, n, sizeof(R) * 3);
+    c->gap = gap;
+    c->mu = mu;
+    friction_basis(n, c->t1, c->t2);
+    return nc + 1;
+}
+
+static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k, int terrain_kind, R mu, contact* cs) {
+    int maxc = p->max_contacts < MAXC ? p->max_contacts : MAXC;
+    int nc = 0;
+    R off = p->contact_offset;
+    for (int b = 0; b < NB; ++b) {
+        const float* g = m->geom_params[b];
+        R n[3], x[3];
+        if (m->geom_type[b] == HE_GEOM_SPHERE) {
+            R l[3] = {g[0], g[1], g[2]}, c[3];
+            body_point(k, b, l, c);
+            R d = terrain_height(p, terrain_kind, c, n) - g[3];
+            if (d < off) {
+                for (int i = 0; i < 3; ++i) x[i] = c[i] - g[3] * n[i];
+                nc = add_contact(cs, nc, maxc, b, -1, x, n, d, mu);
+            }
+        } else if (m->geom_type[b] == HE_GEOM_CAPSULE) {
+            for (int e = 0; e < 2; ++e) {
+                R l[3] = {g[3 * e], g[3 * e + 1], g[3 * e + 2]}, c[3];
+                body_point(k, b, l, c);
+                R d = terrain_height(p, terrain_kind, c, n) - g[6];
+                if (d < off) {
+                    for (int i = 0; i < 3; ++i) x[i] = c[i] - g[6] * n[i];
+                    nc = add_contact(cs, nc, maxc, b, -1, x, n, d, mu);
+                }
+            }
+        } else {
+            /* box corners, keep the 4 deepest (ties by corner index) */
+            R bq[4] = {g[6], g[7], g[8], g[9]}, bm[3][3];
+            qmat(bq, bm);
+            R cx[8][3], cd[8], cn[8][3];
+            int cand[8], ncand = 0;
+            for (int ci = 0; ci < 8; ++ci) {
+                R sgn[3] = {(ci & 1) ? 1.0 : -1.0, (ci & 2) ? 1.0 : -1.0, (ci & 4) ? 1.0 : -1.0};
+                R lb[3] = {sgn[0] * g[3], sgn[1] * g[4], sgn[2] * g[5]}, lr[3];
+                matvec(bm, lb, lr);
+                R l[3] = {g[0] + lr[0], g[1] + lr[1], g[2] + lr[2]};
+                body_point(k, b, l, cx[ci]);
+                cd[ci] = terrain_height(p, terrain_kind, cx[ci], cn[ci]);
+                if (cd[ci] < off) cand[ncand++] = ci;
+            }
+            /* selection of up to 4 deepest */
+            for (int sel = 0; sel < 4 && ncand > 0; ++sel) {
+                int best = 0;
+                for (int j = 1; j < ncand; ++j)
+                    if (cd[cand[j]] < cd[cand[best]]) best = j;
+                int ci = cand[best];
+                nc = add_contact(cs, nc, maxc, b, -1, cx[ci], cn[ci], cd[ci], mu);
+                for (int j = best; j < ncand - 1; ++j) cand[j] = cand[j + 1];
+                --ncand;
+            }
+        }
+    }
+    if (p->self_collision) {
+        for (int pi = 0; pi < m->num_pairs; ++pi) {
+            int i = m->pairs[pi][0], j = m->pairs[pi][1];
+            R a0[3], a1[3], b0[3], b1[3], ri, rj, ci[3], cj[3];
+            body_segment(m, k, i, a0, a1, &ri);
+            body_segment(m, k, j, b0, b1, &rj);
+            seg_seg(a0, a1, b0, b1, ci, cj);
+            R d[3] = {ci[0] - cj[0], ci[1] - cj[1], ci[2] - cj[2]};
+            R len = sqrt(dot3(d, d));
+            R gap = len - ri - rj;
+            if (gap < off) {
+                R n[3];
+                if (len > 1e-9) { n[0] = d[0] / len; n[1] = d[1] / len; n[2] = d[2] / len; }
+                else { n[0] = 0; n[1] = 0; n[2] = 1; }
+                R x[3];
+                for (int c = 0; c < 3; ++c) x[c] = cj[c] + n[c] * (rj + 0.5 * gap);
+                nc = add_contact(cs, nc, maxc, i, j, x, n, gap, mu);
+            }
+        }
+    }
+    return nc;
+}
+
+/* ---------------------------------------------------------------- sparse LTDL (dense storage) */
+static void ltdl_factor(R H[NG][NG], const int* lam) {
+    for (int k = NG - 1; k >= 0; --k) {
+        for (int i = lam[k]; i != -1; i = lam[i]) {
+            R a = H[k][i] / H[k][k];
+            for (int j = i; j != -1; j = lam[j]) H[i][j] -= a * H[k][j];
+            H[k][i] = a;
+        }
+    }
+}
+static void ltdl_solve_LT(R H[NG][NG], const int* lam, R* y) { /* y <- L^-T y */
+    for (int k = NG - 1; k >= 0; --k)
+        for (int i = lam[k]; i != -1; i = lam[i]) y[i] -= H[k][i] * y[k];
+}
+static void ltdl_solve_L(R H[NG][NG], const int* lam, R* y) { /* y <- L^-1 y */
+    for (int k = 0; k < NG; ++k)
+        for (int i = lam[k]; i != -1; i = lam[i]) y[k] -= H[k][i] * y[i];
+}
+
+typedef struct step_out {
+    R contact_force[NB][3];
+    R dof_force[ND];
+    int num_contacts;
+} step_out;
+
+/* one substep; updates s in place */
+static void substep(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
+                    R mu, int terrain_kind, step_out* out) {
+    static __thread kin k;
+    static __thread R H[NG][NG];
+    static __thread R Z[MAXROW][NG];
+    static __thread R A[MAXROW][MAXROW];
+    static __thread contact cs[MAXC];
+    const R dt = p->dt;
+    kinematics(m, t, s, &k);
+    sinertia I[NB], Ic[NB];
+    for (int b = 0; b < NB; ++b) body_inertia(m, &k, b, mass_scale ? mass_scale[b] : 1.0, &I[b]);
+    /* RNEA bias with u_dot = 0 and gravity (a_0 = -g) */
+    R Aacc[NB][6], F[NB][6];
+    Aacc[0][0] = Aacc[0][1] = Aacc[0][2] = 0;
+    {
+        R vxw[3];
+        cross3(s->root_v, s->root_w, vxw);
+        for (int c = 0; c < 3; ++c) Aacc[0][3 + c] = vxw[c] - p->gravity[c];
+    }
+    for (int b = 1; b < NB; ++b) {
+        int pb = m->parents[b];
+        for (int i = 0; i < 6; ++i) Aacc[b][i] = Aacc[pb][i];
+        for (int c = 0; c < 3; ++c) {
+            R cr[6];
+            crm(k.V[b], k.S[t->body_dof0[b] + c], cr);
+            R uu = s->u[3 * (b - 1) + c];
+            for (int i = 0; i < 6; ++i) Aacc[b][i] += cr[i] * uu;
+        }
+    }
+    for (int b = 0; b < NB; ++b) {
+        R IA[6], IV[6], x[6];
+        si_apply(&I[b], Aacc[b], IA);
+        si_apply(&I[b], k.V[b], IV);
+        crf(k.V[b], IV, x);
+        for (int i = 0; i < 6; ++i) F[b][i] = IA[i] + x[i];
+        Ic[b] = I[b];
+    }
+    for (int b = NB - 1; b > 0; --b) {
+        int pb = m->parents[b];
+        for (int i = 0; i < 6; ++i) F[pb][i] += F[b][i];
+        si_add(&Ic[pb], &Ic[b]);
+    }
+    R bias[NG];
+    for (int i = 0; i < NG; ++i) {
+        const R* S = k.S[i];
+        const R* f = F[t->dof_body[i]];
+        bias[i] = S[0] * f[0] + S[1] * f[1] + S[2] * f[2] + S[3] * f[3] + S[4] * f[4] + S[5] * f[5];
+    }
+    /* CRBA: H_ij = S_j . (Ic_{body(i)} S_i) for j ancestor-or-self of i */
+    memset(H, 0, sizeof(H));
+    for (int i = 0; i < NG; ++i) {
+        R IS[6];
+        si_apply(&Ic[t->dof_body[i]], k.S[i], IS);
+        for (int j = i; j != -1; j = t->dof_parent[j]) {
+            const R* S = k.S[j];
+            R v = S[0] * IS[0] + S[1] * IS[1] + S[2] * IS[2] + S[3] * IS[3] + S[4] * IS[4] + S[5] * IS[5];
+            H[i][j] = v;
+            H[j][i] = v;
+        }
+    }
+    /* armature + implicit PD drives */
+    R rhs[NG], coef[NG];
+    for (int i = 0; i < NG; ++i) { rhs[i] = -bias[i]; coef[i] = 0; }
+    for (int d = 0; d < ND; ++d) {
+        int g = 6 + d;
+        H[g][g] += m->armature[d];
+        R kp = m->stiffness[d] * p->kp_scale, kd = m->damping[d] * p->kd_scale;
+        R err = s->target[d] - s->q[d];
+        R u = s->u[d];
+        R tau = kp * (err - dt * u) - kd * u;
+        R lim = m->effort[d];
+        if (fabs(tau) <= lim) {
+            H[g][g] += dt * (kd + dt * kp);
+            out->dof_force[d] = tau; /* updated after the solve */
+        } else {
+            tau = tau > 0 ? lim : -lim;
+            out->dof_force[d] = tau;
+            kp = kd = 0;
+        }
+        rhs[g] += tau;
+        coef[g] = dt * kp + kd; /* d tau / d u+ for the post-solve drive force */
+    }
+    ltdl_factor(H, t->dof_parent);
+    R du[NG];
+    for (int i = 0; i < NG; ++i) du[i] = dt * rhs[i];
+    ltdl_solve_LT(H, t->dof_parent, du);
+    for (int i = 0; i < NG; ++i) du[i] /= H[i][i];
+    ltdl_solve_L(H, t->dof_parent, du);
+    R u0[NG], uf[NG];
+    for (int c = 0; c < 3; ++c) { u0[c] = s->root_w[c]; u0[3 + c] = s->root_v[c]; }
+    for (int d = 0; d < ND; ++d) u0[6 + d] = s->u[d];
+    for (int i = 0; i < NG; ++i) uf[i] = u0[i] + du[i];
+    /* contacts */
+    int nc = gen_contacts(m, p, &k, terrain_kind, mu, cs);
+    out->num_contacts = nc;
+    memset(out->contact_force, 0, sizeof(out->contact_force));
+    R unew[NG];
+    memcpy(unew, uf, sizeof(unew));
+    if (nc > 0) {
+        int nr = 3 * nc;
+        R brow[MAXROW];
+        for (int r = 0; r < nr; ++r) {
+            const contact* c = &cs[r / 3];
+            const R* dir = (r % 3 == 0) ? c->n : (r % 3 == 1 ? c->t1 : c->t2);
+            R rho[3], xo[3] = {c->x[0] - k.o[0], c->x[1] - k.o[1], c->x[2] - k.o[2]};
+            cross3(xo, dir, rho);
+            R* z = Z[r];
+            for (int i = 0; i < NG; ++i) {
+                int bi = t->dof_body[i];
+                R sgn = 0;
+                if (t->is_anc[bi][c->b0]) sgn += 1;
+                if (c->b1 >= 0 && t->is_anc[bi][c->b1]) sgn -= 1;
+                const R* S = k.S[i];
+                z[i] = sgn == 0 ? 0 : sgn * (S[0] * rho[0] + S[1] * rho[1] + S[2] * rho[2] + S[3] * dir[0] + S[4] * dir[1] + S[5] * dir[2]);
+            }
+            R ju = 0;
+            for (int i = 0; i < NG; ++i) ju += z[i] * uf[i];
+            R bb = 0;
+            if (r % 3 == 0) bb = c->gap >= 0 ? c->gap / dt : fmax(p->baumgarte * c->gap / dt, -p->max_depenetration_velocity);
+            brow[r] = ju + bb;
+            ltdl_solve_LT(H, t->dof_parent, z);
+        }
+        for (int r = 0; r < nr; ++r)
+            for (int c2 = 0; c2 <= r; ++c2) {
+                R acc = 0;
+                for (int i = 0; i < NG; ++i) acc += Z[r][i] * Z[c2][i] / H[i][i];
+                A[r][c2] = acc;
+                A[c2][r] = acc;
+            }
+        R lam[MAXROW];
+        memset(lam, 0, sizeof(lam));
+        for (int it = 0; it < p->solver_iterations; ++it) {
+            for (int ci = 0; ci < nc; ++ci) {
+                int r0 = 3 * ci;
+                R w = brow[r0];
+                for (int j = 0; j < nr; ++j) w += A[r0][j] * lam[j];
+                R ln = lam[r0] - w / (A[r0][r0] + 1e-12);
+                lam[r0] = ln > 0 ? ln : 0;
+                R bound = cs[ci].mu * lam[r0];
+                for (int tdir = 1; tdir <= 2; ++tdir) {
+                    int r = r0 + tdir;
+                    R wt = brow[r];
+                    for (int j = 0; j < nr; ++j) wt += A[r][j] * lam[j];
+                    R lt = lam[r] - wt / (A[r][r] + 1e-12);
+                    lam[r] = lt > bound ? bound : (lt < -bound ? -bound : lt);
+                }
+            }
+        }
+        R y[NG];
+        memset(y, 0, sizeof(y));
+        for (int r = 0; r < nr; ++r)
+            if (lam[r] != 0) for (int i = 0; i < NG; ++i) y[i] += Z[r][i] * lam[r];
+        for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
+        ltdl_solve_L(H, t->dof_parent, y);
+        for (int i = 0; i < NG; ++i) unew[i] += y[i];
+        for (int ci = 0; ci < nc; ++ci) {
+            const contact* c = &cs[ci];
+            for (int x = 0; x < 3; ++x) {
+                R f = (lam[3 * ci] * c->n[x] + lam[3 * ci + 1] * c->t1[x] + lam[3 * ci + 2] * c->t2[x]) / dt;
+                out->contact_force[c->b0][x] += f;
+                if (c->b1 >= 0) out->contact_force[c->b1][x] -= f;
+            }
+        }
+    }
+    /* drive force actually applied: tau(u+) = tau_exp - (dt kp + kd)(u+ - u) */
+    for (int d = 0; d < ND; ++d) out->dof_force[d] -= coef[6 + d] * (unew[6 + d] - u0[6 + d]);
+    /* angular damping and max angular velocity (asset options, humanoid_phc.py:212-213) */
+    R damp = 1.0 / (1.0 + dt * p->angular_damping);
+    for (int c = 0; c < 3; ++c) unew[c] *= damp;
+    for (int d = 0; d < ND; ++d) unew[6 + d] *= damp;
+    R wmax = p->max_angular_velocity;
+    for (int b = 0; b < NB; ++b) {
+        R* w = b == 0 ? &unew[0] : &unew[6 + 3 * (b - 1)];
+        R nrm = sqrt(dot3(w, w));
+        if (nrm > wmax) { R sc = wmax / nrm; w[0] *= sc; w[1] *= sc; w[2] *= sc; }
+    }
+    /* write velocities + semi-implicit position update */
+    for (int c = 0; c < 3; ++c) { s->root_w[c] = unew[c]; s->root_v[c] = unew[3 + c]; }
+    for (int d = 0; d < ND; ++d) s->u[d] = unew[6 + d];
+    for (int c = 0; c < 3; ++c) s->root_pos[c] += dt * s->root_v[c];
+    {
+        R dw[3] = {dt * s->root_w[0], dt * s->root_w[1], dt * s->root_w[2]}, dq[4], nq[4];
+        qexp(dw, dq);
+        qmul(dq, s->root_q, nq);
+        qnormalize(nq);
+        memcpy(s->root_q, nq, sizeof(nq));
+    }
+    for (int b = 1; b < NB; ++b) {
+        R* qv = &s->q[3 * (b - 1)];
+        R ql[4], dq[4], nq[4], dw[3] = {dt * s->u[3 * (b - 1)], dt * s->u[3 * (b - 1) + 1], dt * s->u[3 * (b - 1) + 2]};
+        qexp(qv, ql);
+        qexp(dw, dq);
+        qmul(ql, dq, nq);
+        qnormalize(nq);
+        qlog(nq, qv);
+    }
+}
+
+static void write_rb(const he_model* m, const topo* t, const env_state* s, float* rb) {
+    kin k;
+    kinematics(m, t, s, &k);
+    for (int b = 0; b < NB; ++b) {
+        R r[3] = {k.pw[b][0] - k.o[0], k.pw[b][1] - k.o[1], k.pw[b][2] - k.o[2]}, wxr[3];
+        cross3(k.V[b], r, wxr);
+        for (int c = 0; c < 3; ++c) {
+            rb[b * 13 + c] = (float)k.pw[b][c];
+            rb[b * 13 + 7 + c] = (float)(k.V[b][3 + c] + wxr[c]);
+            rb[b * 13 + 10 + c] = (float)k.V[b][c];
+        }
+        for (int c = 0; c < 4; ++c) rb[b * 13 + 3 + c] = (float)k.qw[b][c];
+    }
+}
+
+/* gym.simulate x substeps for n envs. root_states [N,13], dof_state [N,69,2] (in/out),
+ * targets [N,69]; outputs rb_state [N,24,13], contact_forces [N,24,3], dof_force [N,69],
+ * num_contacts [N] (nullable). mass_scale [N,24], friction [N], terrain_kind [N] nullable. */
+void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* root_states, float* dof_state,
+                     const float* targets, int substeps, float* rb_state, float* contact_forces, float* dof_force,
+                     int32_t* num_contacts, const float* mass_scale, const float* friction, const int32_t* terrain_kind) {
+    topo t;
+    build_topo(m, &t);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int e = 0; e < n; ++e) {
+        env_state s;
+        float* rs = root_states + (size_t)e * 13;
+        for (int c = 0; c < 3; ++c) { s.root_pos[c] = rs[c]; s.root_v[c] = rs[7 + c]; s.root_w[c] = rs[10 + c]; }
+        for (int c = 0; c < 4; ++c) s.root_q[c] = rs[3 + c];
+        for (int d = 0; d < ND; ++d) {
+            s.q[d] = dof_state[((size_t)e * ND + d) * 2];
+            s.u[d] = dof_state[((size_t)e * ND + d) * 2 + 1];
+            s.target[d] = targets[(size_t)e * ND + d];
+        }
+        R ms[NB];
+        if (mass_scale) for (int b = 0; b < NB; ++b) ms[b] = mass_scale[(size_t)e * NB + b];
+        R mu = friction ? friction[e] : p->friction;
+        int tk = (p->terrain && terrain_kind) ? terrain_kind[e] : 0;
+        step_out out;
+        memset(&out, 0, sizeof(out));
+        for (int it = 0; it < substeps; ++it) substep(m, &t, p, &s, mass_scale ? ms : NULL, mu, tk, &out);
+        for (int c = 0; c < 3; ++c) { rs[c] = (float)s.root_pos[c]; rs[7 + c] = (float)s.root_v[c]; rs[10 + c] = (float)s.root_w[c]; }
+        for (int c = 0; c < 4; ++c) rs[3 + c] = (float)s.root_q[c];
+        for (int d = 0; d < ND; ++d) {
+            dof_state[((size_t)e * ND + d) * 2] = (float)s.q[d];
+            dof_state[((size_t)e * ND + d) * 2 + 1] = (float)s.u[d];
+            dof_force[(size_t)e * ND + d] = (float)out.dof_force[d];
+        }
+        write_rb(m, &t, &s, rb_state + (size_t)e * NB * 13);
+        for (int b = 0; b < NB; ++b)
+            for (int c = 0; c < 3; ++c) contact_forces[((size_t)e * NB + b) * 3 + c] = (float)out.contact_force[b][c];
+        if (num_contacts) num_contacts[e] = out.num_contacts;
+    }
+}
+
+/* kinematics only: rigid-body state of given generalized states (used by tests) */
+void ho_forward_kinematics(const he_model* m, int n, const float* root_states, const float* dof_state, float* rb_state) {
+    topo t;
+    build_topo(m, &t);
+    for (int e = 0; e < n; ++e) {
+        env_state s;
+        const float* rs = root_states + (size_t)e * 13;
+        for (int c = 0; c < 3; ++c) { s.root_pos[c] = rs[c]; s.root_v[c] = rs[7 + c]; s.root_w[c] = rs[10 + c]; }
+        for (int c = 0; c < 4; ++c) s.root_q[c] = rs[3 + c];
+        for (int d = 0; d < ND; ++d) { s.q[d] = dof_state[((size_t)e * ND + d) * 2]; s.u[d] = dof_state[((size_t)e * ND + d) * 2 + 1]; }
+        write_rb(m, &t, &s, rb_state + (size_t)e * NB * 13);
+    }
+}
+
+/* total mechanical quantities for invariant tests: linear momentum [3], angular momentum about
+ * the world origin [3], kinetic energy, potential energy (gravity). */
+void ho_momentum_energy(const he_model* m, const he_sim_params* p, int n, const float* root_states,
+                        const float* dof_state, double* out /* [N,8] */) {
+    topo t;
+    build_topo(m, &t);
+    for (int e = 0; e < n; ++e) {
+        env_state s;
+        const float* rs = root_states + (size_t)e * 13;
+        for (int c = 0; c < 3; ++c) { s.root_pos[c] = rs[c]; s.root_v[c] = rs[7 + c]; s.root_w[c] = rs[10 + c]; }
+        for (int c = 0; c < 4; ++c) s.root_q[c] = rs[3 + c];
+        for (int d = 0; d < ND; ++d) { s.q[d] = dof_state[((size_t)e * ND + d) * 2]; s.u[d] = dof_state[((size_t)e * ND + d) * 2 + 1]; }
+        kin k;
+        kinematics(m, &t, &s, &k);
+        R P[6] = {0}, ke = 0, pe = 0;
+        for (int b = 0; b < NB; ++b) {
+            sinertia I;
+            body_inertia(m, &k, b, 1.0, &I);
+            R h[6];
+            si_apply(&I, k.V[b], h); /* momentum about o: (L_o, p) */
+            for (int i = 0; i < 6; ++i) P[i] += h[i];
+            ke += 0.5 * (h[0] * k.V[b][0] + h[1] * k.V[b][1] + h[2] * k.V[b][2] + h[3] * k.V[b][3] + h[4] * k.V[b][4] + h[5] * k.V[b][5]);
+            R com_z = k.o[2] + I.h[2] / I.m;
+            pe += -I.m * p->gravity[2] * com_z;
+        }
+        /* angular momentum about world origin: L_0 = L_o + o x p */
+        R oxp[3];
+        cross3(k.o, P + 3, oxp);
+        double* o = out + (size_t)e * 8;
+        o[0] = P[3]; o[1] = P[4]; o[2] = P[5];
+        o[3] = P[0] + oxp[0]; o[4] = P[1] + oxp[1]; o[5] = P[2] + oxp[2];
+        o[6] = ke; o[7] = pe;
+    }
+}

@@ -1,0 +1,169 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of the CPU oracle ``oracle/libhe_oracle.so``.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import this
+module; the product path (``humanoid_amd``) never does. See ``he_oracle.c`` for what each
+function restates (reference file:line) and which parts are pinned by golden vectors.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from humanoid_amd import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhe_oracle.so")
+_lib = None
+
+
+def build(force=False):
+    """Incremental make (no-op when up to date); falls back to a prebuilt .so without a compiler."""
+    try:
+        subprocess.run(["make", "-C", HERE] + (["-B"] if force else []), check=True, capture_output=True)
+    except (OSError, subprocess.CalledProcessError):
+        if not os.path.exists(LIB_PATH):
+            raise
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.ho_hash_uniform.restype = C.c_float
+        _lib.ho_hash_uniform.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+        _lib.ho_sample_time_interval.restype = C.c_float
+        _lib.ho_sample_time_interval.argtypes = [C.c_float, C.c_float]
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def f32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+class HoMotion(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("gts", "grs", "lrs", "gvs", "gavs", "dvs", "length_starts",
+                                            "num_frames", "lengths", "dt")]
+
+
+class MotionTables:
+    """Keeps the numpy arrays alive behind the HoMotion struct."""
+
+    def __init__(self, gts, grs, lrs, gvs, gavs, dvs, length_starts, num_frames, lengths, dt):
+        self.arrays = dict(gts=f32(gts), grs=f32(grs), lrs=f32(lrs), gvs=f32(gvs), gavs=f32(gavs), dvs=f32(dvs),
+                           length_starts=np.ascontiguousarray(length_starts, np.int64),
+                           num_frames=np.ascontiguousarray(num_frames, np.int64), lengths=f32(lengths), dt=f32(dt))
+        self.struct = HoMotion(**{k: _p(v) for k, v in self.arrays.items()})
+
+    @classmethod
+    def from_tables(cls, t):
+        return cls(t.gts, t.grs, t.lrs, t.gvs, t.gavs, t.dvs, t.length_starts, t.num_frames, t.lengths, t.dt)
+
+
+def quat_prims(q, r, v, e, t):
+    n = q.shape[0]
+    outs = dict(mul=(n, 4), rot=(n, 3), tan_norm=(n, 6), angle=(n,), axis=(n, 3), expmap=(n, 3), exp2q=(n, 4),
+                slerp=(n, 4), heading=(n,), hq=(n, 4), hqi=(n, 4))
+    res = {k: np.zeros(s, np.float32) for k, s in outs.items()}
+    ins = [f32(q), f32(r), f32(v), f32(e), f32(t).reshape(-1)]
+    lib().ho_quat_prims(C.c_int(n), *[_p(a) for a in ins], *[_p(res[k]) for k in outs])
+    return res
+
+
+def motion_state(mt: MotionTables, ids, times, offset=None):
+    k = len(ids)
+    ids = np.ascontiguousarray(ids, np.int64)
+    times = f32(times)
+    off = None if offset is None else f32(offset)
+    out = dict(rg_pos=np.zeros((k, 24, 3), np.float32), rb_rot=np.zeros((k, 24, 4), np.float32),
+               body_vel=np.zeros((k, 24, 3), np.float32), body_ang_vel=np.zeros((k, 24, 3), np.float32),
+               dof_pos=np.zeros((k, 69), np.float32), dof_vel=np.zeros((k, 69), np.float32))
+    lib().ho_motion_state(C.byref(mt.struct), C.c_int(k), _p(ids), _p(times), _p(off),
+                          *[_p(out[n]) for n in ("rg_pos", "rb_rot", "body_vel", "body_ang_vel", "dof_pos", "dof_vel")])
+    return out
+
+
+def sample_time_interval(phase, length):
+    return lib().ho_sample_time_interval(float(phase), float(length))
+
+
+def hash_uniform(seed, step, env):
+    return lib().ho_hash_uniform(seed, step, env)
+
+
+def imitation_step(params, mt: MotionTables, rb_state, dof_vel, dof_force, progress, motion_ids, start_times,
+                   start_offsets, global_offset):
+    n = rb_state.shape[0]
+    progress = np.ascontiguousarray(progress, np.int16).copy()
+    out = dict(obs=np.zeros((n, 934), np.float32), rew=np.zeros(n, np.float32),
+               reward_raw=np.zeros((n, 5), np.float32), reset=np.zeros(n, np.uint8), terminate=np.zeros(n, np.uint8))
+    ins = [f32(rb_state), f32(dof_vel), f32(dof_force)]
+    lib().ho_imitation_step(C.byref(params), C.byref(mt.struct), C.c_int(n), *[_p(a) for a in ins], _p(progress),
+                            _p(np.ascontiguousarray(motion_ids, np.int64)), _p(f32(start_times)), _p(f32(start_offsets)),
+                            _p(f32(global_offset)), _p(out["obs"]), _p(out["rew"]), _p(out["reward_raw"]),
+                            _p(out["reset"]), _p(out["terminate"]))
+    out["progress"] = progress
+    return out
+
+
+def reset_envs(params, mt: MotionTables, env_ids, phases, motion_ids, state):
+    """state: dict of numpy arrays (modified in place): start_times, start_offsets, global_offset, progress,
+    root_states [N,13], dof_state [N,69,2], dof_targets [N,69], rb_state [N,24,13], contact_forces [N,24,3],
+    obs [N,934], reset [N] u8, terminate [N] u8."""
+    ids = np.ascontiguousarray(env_ids, np.int32)
+    names = ("start_times", "start_offsets", "global_offset", "progress", "root_states", "dof_state", "dof_targets",
+             "rb_state", "contact_forces", "obs", "reset", "terminate")
+    for n in names:
+        assert state[n].flags.c_contiguous
+    lib().ho_reset_envs(C.byref(params), C.byref(mt.struct), C.c_int(len(ids)), _p(ids), _p(f32(phases)),
+                        _p(np.ascontiguousarray(motion_ids, np.int64)), *[_p(state[n]) for n in names])
+    return state
+
+
+def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, dof_state, targets, substeps=2,
+                 mass_scale=None, friction=None, terrain_kind=None):
+    """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays). Returns outputs."""
+    n = root_states.shape[0]
+    assert root_states.dtype == np.float32 and root_states.flags.c_contiguous
+    assert dof_state.dtype == np.float32 and dof_state.flags.c_contiguous
+    out = dict(rb_state=np.zeros((n, 24, 13), np.float32), contact_forces=np.zeros((n, 24, 3), np.float32),
+               dof_force=np.zeros((n, 69), np.float32), num_contacts=np.zeros(n, np.int32))
+    ms = None if mass_scale is None else f32(mass_scale)
+    fr = None if friction is None else f32(friction)
+    tk = None if terrain_kind is None else np.ascontiguousarray(terrain_kind, np.int32)
+    lib().ho_physics_step(C.byref(model), C.byref(sim), C.c_int(n), _p(root_states), _p(dof_state), _p(f32(targets)),
+                          C.c_int(substeps), _p(out["rb_state"]), _p(out["contact_forces"]), _p(out["dof_force"]),
+                          _p(out["num_contacts"]), _p(ms), _p(fr), _p(tk))
+    return out
+
+
+def forward_kinematics(model, root_states, dof_state):
+    n = root_states.shape[0]
+    rb = np.zeros((n, 24, 13), np.float32)
+    lib().ho_forward_kinematics(C.byref(model), C.c_int(n), _p(f32(root_states)), _p(f32(dof_state)), _p(rb))
+    return rb
+
+
+def momentum_energy(model, sim, root_states, dof_state):
+    n = root_states.shape[0]
+    out = np.zeros((n, 8), np.float64)
+    lib().ho_momentum_energy(C.byref(model), C.byref(sim), C.c_int(n), _p(f32(root_states)), _p(f32(dof_state)), _p(out))
+    return out
+
+
+def imitation_from_ref(params, pos, rot, vel, ang, rpos, rrot, rvel, rang, progress, pass_time):
+    n = pos.shape[0]
+    out = dict(rew=np.zeros(n, np.float32), reward_raw=np.zeros((n, 4), np.float32), reset=np.zeros(n, np.uint8),
+               terminate=np.zeros(n, np.uint8), self_obs=np.zeros((n, 358), np.float32),
+               task_obs=np.zeros((n, 576), np.float32))
+    ins = [f32(a) for a in (pos, rot, vel, ang, rpos, rrot, rvel, rang)]
+    lib().ho_imitation_from_ref(C.byref(params), C.c_int(n), *[_p(a) for a in ins],
+                                _p(np.ascontiguousarray(progress, np.int16)), _p(np.ascontiguousarray(pass_time, np.uint8)),
+                                *[_p(out[k]) for k in ("rew", "reward_raw", "reset", "terminate", "self_obs", "task_obs")])
+    return out

@@ -1,0 +1,80 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads and exports every symbol the
+header declares; ctypes struct layouts match the header's sizes; host-side model/topology logic."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "humanoid_engine.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(he_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from humanoid_amd import engine
+    lib_path = engine.LIB_PATH
+    if not os.path.exists(lib_path):
+        from humanoid_amd import build
+        build.build()
+    lib = C.CDLL(lib_path)  # loads without a GPU
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(engine.HE_SYMBOLS)
+    lib.he_version.restype = C.c_int
+    assert lib.he_version() == 1
+    lib.he_hash_uniform.restype = C.c_float
+    lib.he_hash_uniform.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+    from oracle import oracle as O
+    for s, st, e in [(0, 0, 0), (1, 7, 4095), (123456789, 1 << 40, 17)]:
+        assert lib.he_hash_uniform(s, st, e) == O.hash_uniform(s, st, e)
+
+
+def test_errors_are_reported_without_gpu():
+    from humanoid_amd import _abi, engine
+    lib = engine.load_library()
+    h = C.c_void_p()
+    p = _abi.default_sim_params()
+    rc = lib.he_create(C.byref(p), 0, C.byref(h))
+    assert rc != 0
+    assert lib.he_last_error().decode()
+
+
+def test_struct_sizes_match_header(tmp_path):
+    from humanoid_amd import _abi
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "humanoid_engine.h"\nint main(){printf("%zu %zu %zu %zu\\n",'
+                   "sizeof(he_model),sizeof(he_sim_params),sizeof(he_imitation_params),sizeof(he_env_motion));}\n")
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(x) for x in out] == [C.sizeof(_abi.HeModel), C.sizeof(_abi.HeSimParams),
+                                     C.sizeof(_abi.HeImitationParams), C.sizeof(_abi.HeEnvMotion)]
+
+
+def test_model_blob(model):
+    from humanoid_amd import _abi
+    hm = _abi.make_model(model)
+    assert hm.num_pairs == 245
+    assert abs(sum(hm.mass) - 73.995) < 1e-2
+    assert list(hm.parents)[:5] == [-1, 0, 1, 2, 3]
+
+
+def test_mjcf_roundtrip_matches_baked_json(model):
+    xml = "/root/reference/packages/puffer-phc/puffer_phc/assets/smpl_humanoid.xml"
+    if not os.path.exists(xml):
+        pytest.skip("reference asset not present (GPU box)")
+    from humanoid_amd.model import parse_mjcf
+    m = parse_mjcf(xml)
+    np.testing.assert_allclose(m.local_pos, model.local_pos)
+    np.testing.assert_allclose(m.mass, model.mass)
+    np.testing.assert_allclose(m.inertia, model.inertia)

@@ -1,0 +1,307 @@
+"""GPU parity: the HIP engine (through its C ABI) against the golden fixtures and the CPU oracle.
+
+Tolerances (float32 kernels vs the reference's float32 torch / the fp64 oracle):
+* imitation outputs: 5e-5 abs (+1e-5 rel) on obs/reward, exact on reset/terminate/progress;
+  quaternions up to sign within 5e-6 (the slerp is evaluated in torch's float32 order on both);
+* physics after one policy step (2 substeps): positions 1e-4 m, joint angles 1e-4 rad (BASELINE's
+  1e-4 rad/m), velocities 2e-3 (PGS in fp32 vs fp64) -- envs whose contact sets differ between
+  fp32 and fp64 (a point within rounding of the 0.02 m contact offset) are counted and must be rare.
+"""
+import numpy as np
+import pytest
+
+from humanoid_amd import _abi
+from humanoid_amd.body_sets import EVAL_BODIES, body_ids
+from oracle import oracle as O
+
+import cases
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+
+
+def quat_close(a, b, atol):
+    a = np.asarray(a).reshape(-1, 4)
+    b = np.asarray(b).reshape(-1, 4)
+    d = np.minimum(np.abs(a - b).max(-1), np.abs(a + b).max(-1))
+    assert d.max() <= atol, f"max quaternion diff {d.max()}"
+
+
+def make_engine(he_model, n, **sim):
+    from humanoid_amd.engine import Engine
+    _require_gpu()
+    return Engine(he_model, n, device=0, sim_params=_abi.default_sim_params(**sim))
+
+
+def tables_from_golden(g):
+    from humanoid_amd.motion_lib import MotionTables
+    return MotionTables(gts=g["gts"], grs=g["grs"], lrs=g["lrs"], gvs=g["gvs"], gavs=g["gavs"], dvs=g["dvs"],
+                        num_frames=g["num_frames"], length_starts=g["length_starts"], lengths=g["motion_lengths"],
+                        dt=g["motion_dt"], fps=1.0 / g["motion_dt"])
+
+
+def cu(x, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(x), device="cuda:0")
+    return t if dtype is None else t.to(dtype)
+
+
+def test_zero_copy_buffers(he_model):
+    eng = make_engine(he_model, 8)
+    root = eng.root_states
+    assert root.shape == (8, 13) and root.is_cuda
+    assert eng.dof_state.shape == (8 * 69, 2)
+    assert eng.rb_state.shape == (8 * 24, 13)
+    assert eng.contact_forces.shape == (8 * 24, 3)
+    assert eng.dof_force.shape == (8 * 69,)
+    torch.cuda.synchronize()
+    r = root.cpu().numpy()
+    np.testing.assert_allclose(r[:, 2], 0.89)
+    np.testing.assert_allclose(r[:, 6], 1.0)
+    # indexed writes from a separate full-size source
+    src = torch.zeros(8, 13, device="cuda:0")
+    src[:, 2] = 2.5
+    ids = torch.tensor([1, 5], dtype=torch.int32, device="cuda:0")
+    eng.set_root_state_indexed(src, ids)
+    torch.cuda.synchronize()
+    z = eng.root_states[:, 2].cpu().numpy()
+    assert z[1] == 2.5 and z[5] == 2.5 and z[0] == np.float32(0.89)
+    with pytest.raises(Exception):
+        eng.set_root_state_indexed(src[:, :12], ids)
+
+
+def test_motion_state_matches_golden(he_model, golden):
+    g = golden("motion_lib")
+    eng = make_engine(he_model, 4)
+    eng.load_motions(tables_from_golden(g))
+    r = eng.motion_state(cu(g["q_ids"], torch.int64), cu(g["q_times"]), cu(g["q_offset"]))
+    torch.cuda.synchronize()
+    r = {k: v.cpu().numpy() for k, v in r.items()}
+    np.testing.assert_allclose(r["rg_pos"], g["ms_rg_pos"], atol=2e-6)
+    np.testing.assert_allclose(r["body_vel"], g["ms_body_vel"], atol=1e-5)
+    np.testing.assert_allclose(r["body_ang_vel"], g["ms_body_ang_vel"], atol=1e-5)
+    np.testing.assert_allclose(r["dof_vel"], g["ms_dof_vel"], atol=1e-5)
+    quat_close(r["rb_rot"], g["ms_rb_rot"], 5e-6)
+    np.testing.assert_allclose(r["dof_pos"], g["ms_dof_pos"], atol=2e-4)
+
+
+def _load_env_state(eng, g):
+    n = g["rb_state"].shape[0]
+    eng.rb_state.copy_(cu(g["rb_state"].reshape(n * 24, 13)))
+    ds = eng.dof_state.view(n, 69, 2)
+    ds[..., 1] = cu(g["dof_vel"])
+    eng.dof_force.copy_(cu(g["dof_force"].reshape(-1)))
+
+
+def test_imitation_step_matches_golden_and_oracle(he_model, golden):
+    g = golden("env_step")
+    n = g["rb_state"].shape[0]
+    eng = make_engine(he_model, n)
+    eng.load_motions(tables_from_golden(g))
+    _load_env_state(eng, g)
+    mids = cu(g["motion_ids"], torch.int64)
+    st, so = cu(g["start_times"]), cu(g["start_offsets"])
+    go, prog = cu(g["global_offset"]), cu(g["progress_in"], torch.int16)
+    em = eng.env_motion(mids, st, so, go, prog)
+    obs = torch.zeros(n, 934, device="cuda:0")
+    rew = torch.zeros(n, device="cuda:0")
+    raw = torch.zeros(n, 5, device="cuda:0")
+    reset = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    term = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    eng.imitation_step(_abi.imitation_params(), em, obs, rew, raw, reset, term)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(prog.cpu().numpy(), g["progress_out"])
+    np.testing.assert_allclose(rew.cpu().numpy(), g["rew"], atol=5e-5, rtol=1e-5)
+    np.testing.assert_allclose(raw.cpu().numpy(), g["reward_raw"], atol=5e-5, rtol=1e-5)
+    np.testing.assert_array_equal(reset.cpu().numpy(), g["reset"])
+    np.testing.assert_array_equal(term.cpu().numpy(), g["terminate"])
+    np.testing.assert_allclose(obs.cpu().numpy(), g["obs"], atol=5e-5, rtol=1e-5)
+    # eval-mode termination
+    prog.copy_(cu(g["progress_in"], torch.int16))
+    pe = _abi.imitation_params(eval_mode=True, termination_distance=0.5, reset_body_ids=body_ids(EVAL_BODIES))
+    eng.imitation_step(pe, em, obs, rew, raw, reset, term)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(reset.cpu().numpy(), g["reset_eval"])
+    np.testing.assert_array_equal(term.cpu().numpy(), g["terminate_eval"])
+
+
+def test_reset_envs_matches_golden(he_model, golden):
+    g = golden("env_reset")
+    s = golden("env_step")
+    n = g["root_states"].shape[0]
+    eng = make_engine(he_model, n)
+    eng.load_motions(tables_from_golden(s))
+    eng.rb_state.copy_(cu(g["rb_state_in"].reshape(n * 24, 13)))
+    mids = torch.arange(n, device="cuda:0", dtype=torch.int64)
+    st = torch.zeros(n, device="cuda:0")
+    so = torch.zeros(n, device="cuda:0")
+    go = cu(g["global_offset_in"])
+    prog = torch.full((n,), 7, dtype=torch.int16, device="cuda:0")
+    em = eng.env_motion(mids, st, so, go, prog)
+    obs = torch.zeros(n, 934, device="cuda:0")
+    reset = torch.ones(n, dtype=torch.uint8, device="cuda:0")
+    term = torch.ones(n, dtype=torch.uint8, device="cuda:0")
+    ids = cu(g["env_ids"], torch.int32)
+    eng.reset_envs(_abi.imitation_params(), em, ids, cu(g["phases"]), obs, reset, term)
+    torch.cuda.synchronize()
+    I = g["env_ids"]
+    np.testing.assert_array_equal(st.cpu().numpy()[I], g["start_times"][I])
+    np.testing.assert_array_equal(go.cpu().numpy(), g["global_offset"])
+    rs = eng.root_states.cpu().numpy()[I]
+    gr = g["root_states"][I]
+    np.testing.assert_allclose(rs[:, :3], gr[:, :3], atol=2e-6)
+    quat_close(rs[:, 3:7], gr[:, 3:7], 5e-6)
+    np.testing.assert_allclose(rs[:, 7:], gr[:, 7:], atol=1e-5)
+    ds = eng.dof_state.view(n, 69, 2).cpu().numpy()[I]
+    np.testing.assert_allclose(ds[..., 0], g["dof_pos"][I], atol=2e-4)
+    np.testing.assert_allclose(ds[..., 1], g["dof_vel"][I], atol=1e-5)
+    np.testing.assert_allclose(eng.dof_targets.cpu().numpy()[I], g["dof_pos"][I], atol=2e-4)
+    rb = eng.rb_state.view(n, 24, 13).cpu().numpy()[I]
+    grb = g["rb_state"][I]
+    np.testing.assert_allclose(rb[..., :3], grb[..., :3], atol=2e-6)
+    quat_close(rb[..., 3:7], grb[..., 3:7], 5e-6)
+    np.testing.assert_allclose(rb[..., 7:], grb[..., 7:], atol=1e-5)
+    np.testing.assert_allclose(obs.cpu().numpy()[I], g["obs"][I], atol=5e-5, rtol=1e-5)
+    p = prog.cpu().numpy()
+    assert (p[I] == 0).all() and (p[np.setdiff1d(np.arange(n), I)] == 7).all()
+    assert (reset.cpu().numpy()[I] == 0).all()
+
+
+def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=1e-4, vel_tol=2e-3, max_skip=0.1,
+                     **sim):
+    n = root.shape[0]
+    eng = make_engine(he_model, n, **sim)
+    eng.root_states.copy_(cu(root))
+    eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
+    eng.dof_targets.copy_(cu(targets))
+    r_o, d_o = root.copy(), dof.copy()
+    sp = _abi.default_sim_params(**sim)
+    mismatch = np.zeros(n, bool)
+    for _ in range(steps):
+        eng.simulate(substeps)
+        out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, substeps)
+        torch.cuda.synchronize()
+        mismatch |= eng.num_contacts.cpu().numpy() != out["num_contacts"]
+    ok = ~mismatch
+    assert mismatch.mean() <= max_skip, f"contact-set mismatch in {mismatch.sum()}/{n} envs"
+    rg = eng.root_states.cpu().numpy()
+    dg = eng.dof_state.view(n, 69, 2).cpu().numpy()
+    rbg = eng.rb_state.view(n, 24, 13).cpu().numpy()
+    np.testing.assert_allclose(rg[ok, :3], r_o[ok, :3], atol=pos_tol)
+    quat_close(rg[ok, 3:7], r_o[ok, 3:7], pos_tol)
+    np.testing.assert_allclose(dg[ok, :, 0], d_o[ok, :, 0], atol=pos_tol)
+    np.testing.assert_allclose(rg[ok, 7:], r_o[ok, 7:], atol=vel_tol, rtol=1e-3)
+    np.testing.assert_allclose(dg[ok, :, 1], d_o[ok, :, 1], atol=vel_tol, rtol=1e-3)
+    np.testing.assert_allclose(rbg[ok, :, :3], out["rb_state"][ok, :, :3], atol=pos_tol)
+    np.testing.assert_allclose(eng.dof_force.view(n, 69).cpu().numpy()[ok], out["dof_force"][ok], atol=0.5, rtol=1e-3)
+    return eng, out
+
+
+def test_physics_airborne_matches_oracle(he_model):
+    rng = np.random.default_rng(1)
+    root, dof = cases.random_state(64, rng, height=(3.0, 4.0))
+    targets = rng.uniform(-0.5, 0.5, (64, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, self_collision=0, max_skip=0.0)
+
+
+def test_physics_standing_matches_oracle(he_model, model):
+    rng = np.random.default_rng(2)
+    root, dof = cases.standing_state(model, 64, rng, xy_jitter=1.0)
+    targets = np.zeros((64, 69), np.float32)
+    _physics_compare(he_model, root, dof, targets, steps=5)
+
+
+def test_physics_contact_rich_matches_oracle(he_model):
+    rng = np.random.default_rng(3)
+    root, dof = cases.random_state(96, rng, height=(0.85, 1.0), ang=0.8, vel=0.5)
+    r2, d2 = cases.lying_state(32, rng)
+    root = np.concatenate([root, r2])
+    dof = np.concatenate([dof, d2])
+    targets = rng.uniform(-0.5, 0.5, (128, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets)
+
+
+def test_physics_domain_randomised_terrain(he_model, model):
+    """Config 5 extension: per-env mass scale, friction and terrain kind vs the oracle."""
+    n = 48
+    rng = np.random.default_rng(4)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    root[:, 2] += 0.1
+    ms = rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32)
+    fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
+    tk = (np.arange(n) % 3).astype(np.int32)
+    eng = make_engine(he_model, n, terrain=1)
+    eng.set_env_properties(cu(ms), cu(fr), cu(tk))
+    eng.root_states.copy_(cu(root))
+    eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
+    sp = _abi.default_sim_params(terrain=1)
+    r_o, d_o = root.copy(), dof.copy()
+    for _ in range(3):
+        eng.simulate(2)
+        out = O.physics_step(eng.he_model, sp, r_o, d_o, np.zeros((n, 69), np.float32), 2, mass_scale=ms, friction=fr,
+                             terrain_kind=tk)
+    torch.cuda.synchronize()
+    ok = eng.num_contacts.cpu().numpy() == out["num_contacts"]
+    assert ok.mean() >= 0.9
+    np.testing.assert_allclose(eng.root_states.cpu().numpy()[ok, :3], r_o[ok, :3], atol=1e-4)
+    np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[ok, :, 0], d_o[ok, :, 0], atol=1e-4)
+
+
+def test_env_step_fused_matches_oracle(he_model, model, golden):
+    """he_env_step = actions->PD targets->physics->reward/reset/obs->device reset (hash phases)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    from humanoid_amd.body_sets import frozen_dof_mask
+    g = golden("env_step")
+    n = 24
+    tables = tables_from_golden(g)
+    eng = make_engine(he_model, n)
+    eng.load_motions(tables)
+    off, sc = pd_action_offset_scale(model)
+    frozen = np.array(frozen_dof_mask(), np.int32)
+    eng.set_pd_params(off, sc, frozen)
+    rng = np.random.default_rng(5)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    eng.root_states.copy_(cu(root))
+    eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
+    st = cu(g["start_times"]); so = torch.zeros(n, device="cuda:0"); go = torch.zeros(n, 3, device="cuda:0")
+    prog = torch.zeros(n, dtype=torch.int16, device="cuda:0")
+    mids = torch.arange(n, device="cuda:0", dtype=torch.int64)
+    em = eng.env_motion(mids, st, so, go, prog)
+    p = _abi.imitation_params()
+    obs = torch.zeros(n, 934, device="cuda:0"); rew = torch.zeros(n, device="cuda:0")
+    raw = torch.zeros(n, 5, device="cuda:0")
+    reset = torch.zeros(n, dtype=torch.uint8, device="cuda:0"); term = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    actions = rng.uniform(-1.5, 1.5, (n, 69)).astype(np.float32)
+    seed = 1234
+    # oracle mirror
+    mt = O.MotionTables.from_tables(tables)
+    sp = _abi.default_sim_params()
+    r_o, d_o = root.copy(), dof.copy()
+    st_o = g["start_times"].astype(np.float32).copy(); so_o = np.zeros(n, np.float32); go_o = np.zeros((n, 3), np.float32)
+    prog_o = np.zeros(n, np.int16)
+    tgt = off + sc * np.clip(actions, -1, 1)
+    tgt[:, frozen.astype(bool)] = 0
+    for step in range(3):
+        eng.env_step(p, em, cu(actions), obs, rew, raw, reset, term, seed=seed, step_index=step)
+        out = O.physics_step(eng.he_model, sp, r_o, d_o, tgt.astype(np.float32), 2)
+        im = O.imitation_step(p, mt, out["rb_state"], d_o[..., 1], out["dof_force"], prog_o, np.arange(n), st_o, so_o, go_o)
+        prog_o = im["progress"]
+        ids = np.nonzero(im["reset"])[0]
+        state = dict(start_times=st_o, start_offsets=so_o, global_offset=go_o, progress=prog_o, root_states=r_o,
+                     dof_state=d_o, dof_targets=np.zeros((n, 69), np.float32), rb_state=out["rb_state"],
+                     contact_forces=out["contact_forces"], obs=im["obs"], reset=np.zeros(n, np.uint8),
+                     terminate=np.zeros(n, np.uint8))
+        if len(ids):
+            ph = np.array([O.hash_uniform(seed, step, int(e)) for e in ids], np.float32)
+            O.reset_envs(p, mt, ids, ph, np.arange(n), state)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(reset.cpu().numpy(), im["reset"])
+        np.testing.assert_allclose(rew.cpu().numpy(), im["rew"], atol=2e-3, rtol=1e-3)
+        np.testing.assert_allclose(obs.cpu().numpy(), state["obs"], atol=2e-3, rtol=1e-3)
+        np.testing.assert_array_equal(prog.cpu().numpy(), prog_o)
+        np.testing.assert_allclose(st.cpu().numpy(), st_o, atol=0)
