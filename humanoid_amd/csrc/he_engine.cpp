@@ -62,6 +62,7 @@ struct he_engine {
     int64_t *m_starts = nullptr, *m_nframes = nullptr;
     int64_t m_frames = 0;
     int m_motions = 0;
+    unsigned long long* stamps = nullptr;
 };
 
 extern "C" {
@@ -271,6 +272,7 @@ PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
     a.terrain_kind = h->terrain_kind;
     a.num_envs = h->num_envs;
     a.substeps = substeps;
+    a.stamps = h->stamps;
     return a;
 }
 }  // namespace
@@ -348,7 +350,7 @@ int he_load_motions(he_engine* h, int64_t F, int M, const float* gts, const floa
 
 namespace {
 MotionDev motion_dev(he_engine* h) {
-    return MotionDev{h->m_hot, h->m_cold, h->m_starts, h->m_nframes, h->m_lengths, h->m_dt};
+    return MotionDev{h->m_hot, h->m_cold, h->m_starts, h->m_nframes, h->m_lengths, h->m_dt, h->m_motions};
 }
 
 int imit_common(he_engine* h, const he_imitation_params* p, const he_env_motion* em, ImitArgs& a, const char* what) {
@@ -439,6 +441,12 @@ int he_motion_state(he_engine* h, int k, const int64_t* ids, const float* times,
     a.rg_pos = rg_pos; a.rb_rot = rb_rot; a.body_vel = body_vel; a.body_ang_vel = body_ang_vel;
     a.dof_pos = dof_pos; a.dof_vel = dof_vel;
     HE_CHECK(launch_motion_state(a, (hipStream_t)stream));
+    return 0;
+}
+
+int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer) {
+    if (!h) return fail("he_set_debug_stamps: null handle");
+    h->stamps = reinterpret_cast<unsigned long long*>(device_buffer);
     return 0;
 }
 

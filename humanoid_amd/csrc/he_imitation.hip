@@ -40,7 +40,12 @@ struct FrameSel {
 };
 
 // motion_lib.py:655-665 in float32
+HE_DEV int64_t clamp_mid(const MotionDev& m, int64_t mid) {
+    return mid < 0 ? 0 : (mid >= m.num_motions ? (int64_t)m.num_motions - 1 : mid);
+}
+
 HE_DEV FrameSel frame_select(const MotionDev& m, int64_t mid, float time) {
+    mid = clamp_mid(m, mid);
     float len = m.lengths[mid];
     int64_t nf = m.num_frames[mid];
     float dt = m.dt[mid];
@@ -177,7 +182,7 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
     const bool act = lane < NB;
     const int b = act ? lane : 0;
     const he_imitation_params& p = a.p;
-    const int64_t mid = a.motion_ids[e];
+    const int64_t mid = clamp_mid(a.m, a.motion_ids[e]);
     f3 off = f3{a.global_offset[3 * e], a.global_offset[3 * e + 1], a.global_offset[3 * e + 2]};
     float start = a.start_times[e], soff = a.start_offsets[e];
     int prog = a.progress[e];
@@ -288,7 +293,7 @@ __global__ void __launch_bounds__(256) motion_state_kernel(MotionStateArgs a) {
     if (q >= a.k || lane >= NB) return;
     const int b = lane;
     f3 off = a.offset ? f3{a.offset[3 * q], a.offset[3 * q + 1], a.offset[3 * q + 2]} : f3{0.f, 0.f, 0.f};
-    FrameSel fs = frame_select(a.m, a.ids[q], a.times[q]);
+    FrameSel fs = frame_select(a.m, a.ids[q], a.times[q]);  // clamps the id
     BodyRef r = body_ref(a.m, fs, b, off);
     size_t o3 = ((size_t)q * NB + b) * 3, o4 = ((size_t)q * NB + b) * 4;
     if (a.rg_pos) { a.rg_pos[o3] = r.pos.x; a.rg_pos[o3 + 1] = r.pos.y; a.rg_pos[o3 + 2] = r.pos.z; }

@@ -17,6 +17,7 @@ struct MotionDev {
     const int64_t* num_frames;    // [M]
     const float* lengths;         // [M]
     const float* dt;              // [M]
+    int num_motions;              // M (ids are clamped into range: a bad id must never fault)
 };
 
 struct ImitArgs {
@@ -75,6 +76,7 @@ struct PhysArgs {
     const int32_t* terrain_kind; // [N] or null
     int num_envs;
     int substeps;
+    unsigned long long* stamps;  // diagnostics: [N][16] phase cycles or null
 };
 
 hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream);

@@ -41,11 +41,24 @@ struct Lds {
     float brow[3 * MAXC];
     float cf[NB][3];
     float dforce[ND];
+    float Dinv[NG];
     float root_pos[3], root_q[4];
     int nc;
+    PhysTopo T;  // static tables copied from global memory once per launch
 };
 
 HE_DEV void sync() { __syncthreads(); }
+
+// optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
+// s_memtime deltas per phase into stamps[block * 16 + phase]
+#define STAMP(id)                                                             \
+    do {                                                                      \
+        if (stamps && lane == 0) {                                            \
+            unsigned long long _t = __builtin_readcyclecounter();             \
+            stamps[id] += _t - t_prev;                                        \
+            t_prev = _t;                                                      \
+        }                                                                     \
+    } while (0)
 
 // spatial inertia (m, h, I6) applied to V=(w, v): n = I w + h x v ; f = m v - h x w
 HE_DEV void si_apply(const float* I, const float* V, float* F) {
@@ -235,10 +248,12 @@ HE_DEV void kinematics(Lds& L, const he_model& m, const PhysTopo& T, int lane) {
 
 // ---------------------------------------------------------------------------------- one substep
 HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, const he_model& m, const PhysTopo& T,
-                    int lane, const float* mass_scale, float mu, int tkind) {
+                    int lane, const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
+                    unsigned long long& t_prev) {
     const he_sim_params& p = a.p;
     const float dt = p.dt;
     kinematics(L, m, T, lane);
+    STAMP(0);
     const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
     // ---- body spatial inertias about o
     if (lane < NB) {
@@ -290,6 +305,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         for (int x = 0; x < 6; ++x) L.Acc[b][x] = IA[x] + X[x];  // body force f_b
     }
     sync();
+    STAMP(1);
     // ---- subtree sums: F_b (forces) and composite inertias
     if (lane < NB) {
         uint32_t sm = T.sub_mask[lane];
@@ -303,6 +319,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         for (int x = 0; x < 10; ++x) L.Ic[lane][x] = Ics[x];
     }
     sync();
+    STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
     for (int i = lane; i < NG; i += W) {
         int b = T.dof_body[i];
@@ -325,53 +342,55 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         L.coef[i] = cf;
     }
     sync();
+    STAMP(3);
     // ---- CRBA entries H(i, j) = S_j . IS_i for j in chain(i); + armature + implicit drive terms
     for (int e = lane; e < T.nnz; e += W) {
-        // find row i: rows are contiguous, search via row_start (75 rows)
-        int lo = 0, hi = NG - 1;
-        while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if (T.row_start[mid] <= e) lo = mid; else hi = mid - 1;
-        }
-        int i = lo, pos = e - T.row_start[i];
+        int i = T.ent_row[e], pos = e - T.row_start[i];
         int j = T.dof_chain[i][pos];
         float h = dot6(L.S[j], L.IS[i]);
-        if (j == i && i >= 6) {
-            int d = i - 6;
-            h += m.armature[d] + dt * L.coef[i];
-        }
+        if (j == i && i >= 6) h += m.armature[i - 6] + dt * L.coef[i];
         L.H[e] = h;
     }
     sync();
-    // ---- sparse LTDL, k = NG-1 .. 0 (Featherstone RBDA 6.5): H(i,j) -= H(k,i) H(k,j) / H(k,k)
-    for (int k = NG - 1; k > 0; --k) {
-        int d = T.dof_nanc[k] - 1;  // ancestors of k occupy chain positions 0..d-1
-        if (d <= 0) continue;
-        int rk = T.row_start[k];
-        float inv = 1.0f / L.H[rk + d];
-        int npairs = d * (d + 1) / 2;
-        for (int t = lane; t < npairs; t += W) {
-            int ix = T.tri_i[t], jx = T.tri_j[t];
+    STAMP(4);
+    // ---- sparse LTDL (RBDA 6.5) by dof level: all dofs with the same chain length are eliminated
+    // together (their updates only touch shared ancestors -> LDS float atomics); rows are scaled
+    // by their pivots in one pass at the end.
+    for (int len = T.num_levels; len >= 2; --len) {
+        const int d = len - 1, npairs = d * (d + 1) / 2;
+        const int k0 = T.level_start[len - 1], total = (T.level_start[len] - k0) * npairs;
+        for (int t = lane; t < total; t += W) {
+            int kk = t / npairs, pr = t - kk * npairs;
+            int k = T.level_dofs[k0 + kk];
+            int rk = T.row_start[k];
+            int ix = T.tri_i[pr], jx = T.tri_j[pr];
             int i = T.dof_chain[k][ix];
-            L.H[T.row_start[i] + jx] -= L.H[rk + ix] * inv * L.H[rk + jx];
+            atomicAdd(&L.H[T.row_start[i] + jx], -L.H[rk + ix] * L.H[rk + jx] / L.H[rk + d]);
         }
         sync();
-        if (lane < d) L.H[rk + lane] *= inv;
-        sync();
     }
-    // ---- free velocity: du = L^-1 D^-1 L^-T rhs
+    for (int i = lane; i < NG; i += W) L.Dinv[i] = 1.0f / L.H[T.row_start[i] + T.dof_nanc[i] - 1];
+    sync();
+    for (int e = lane; e < T.nnz; e += W) {
+        int i = T.ent_row[e];
+        if (e - T.row_start[i] < T.dof_nanc[i] - 1) L.H[e] *= L.Dinv[i];
+    }
     for (int i = lane; i < NG; i += W) L.y[i] = L.rhs[i];
     sync();
-    for (int k = NG - 1; k > 0; --k) {  // L^-T
-        int d = T.dof_nanc[k] - 1;
-        int rk = T.row_start[k];
-        float yk = L.y[k];
-        if (lane < d) L.y[T.dof_chain[k][lane]] -= L.H[rk + lane] * yk;
+    STAMP(5);
+    // ---- free velocity: du = L^-1 D^-1 L^-T rhs (both sweeps level-parallel)
+    for (int len = T.num_levels; len >= 2; --len) {  // L^-T: push to ancestors, deepest level first
+        const int d = len - 1, k0 = T.level_start[len - 1], total = (T.level_start[len] - k0) * d;
+        for (int t = lane; t < total; t += W) {
+            int kk = t / d, x = t - kk * d;
+            int k = T.level_dofs[k0 + kk];
+            atomicAdd(&L.y[T.dof_chain[k][x]], -L.H[T.row_start[k] + x] * L.y[k]);
+        }
         sync();
     }
-    for (int i = lane; i < NG; i += W) L.y[i] /= L.H[T.row_start[i] + T.dof_nanc[i] - 1];
+    for (int i = lane; i < NG; i += W) L.y[i] *= L.Dinv[i];
     sync();
-    for (int lv = 1; lv < T.num_levels; ++lv) {  // L^-1 by chain-length levels
+    for (int lv = 1; lv < T.num_levels; ++lv) {  // L^-1: pull from ancestors, shallowest first
         for (int t = T.level_start[lv] + lane; t < T.level_start[lv + 1]; t += W) {
             int k = T.level_dofs[t];
             int rk = T.row_start[k];
@@ -380,6 +399,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
             L.y[k] = acc;
         }
         sync();
+        STAMP(6);
     }
     for (int i = lane; i < NG; i += W) L.uf[i] = L.u0[i] + L.y[i];
     // ---- contacts: terrain (bodies in order, box corners deepest-first), then self pairs
@@ -387,58 +407,66 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
     const float off = p.contact_offset;
     int nc = 0;
     {
-        int myn = 0;
-        f3 px[4];
-        f3 pn[4];
-        float pg[4];
+        // per body: sphere 1, capsule 2 (end spheres), box up to 4 deepest corners (ranked by depth,
+        // ties by corner index -- the oracle's selection order); fully unrolled, no scratch arrays
+        int b = lane < NB ? lane : 0;
+        const float* g = m.geom_params[b];
+        int gt = m.geom_type[b];
+        float cd[8];
+        f3 cxs[8], cns[8];
+        bool cand[8];
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) { cand[ci] = false; cd[ci] = 0.f; }
         if (lane < NB) {
-            int b = lane;
-            const float* g = m.geom_params[b];
-            int gt = m.geom_type[b];
-            f3 n;
             if (gt == HE_GEOM_SPHERE) {
                 f3 c = body_point(L, b, f3{g[0], g[1], g[2]});
-                float dd = terrain_dist(p, tkind, c, n) - g[3];
-                if (dd < off) { px[0] = c - n * g[3]; pn[0] = n; pg[0] = dd; myn = 1; }
+                cd[0] = terrain_dist(p, tkind, c, cns[0]) - g[3];
+                cxs[0] = c - cns[0] * g[3];
+                cand[0] = cd[0] < off;
             } else if (gt == HE_GEOM_CAPSULE) {
+#pragma unroll
                 for (int e2 = 0; e2 < 2; ++e2) {
                     f3 c = body_point(L, b, f3{g[3 * e2], g[3 * e2 + 1], g[3 * e2 + 2]});
-                    float dd = terrain_dist(p, tkind, c, n) - g[6];
-                    if (dd < off) { px[myn] = c - n * g[6]; pn[myn] = n; pg[myn] = dd; ++myn; }
+                    cd[e2] = terrain_dist(p, tkind, c, cns[e2]) - g[6];
+                    cxs[e2] = c - cns[e2] * g[6];
+                    cand[e2] = cd[e2] < off;
                 }
             } else {
                 f4 bq = f4{g[6], g[7], g[8], g[9]};
-                f3 cx[8], cnv[8];
-                float cd[8];
-                int cand[8], ncand = 0;
+#pragma unroll
                 for (int ci = 0; ci < 8; ++ci) {
                     f3 lb = f3{(ci & 1) ? g[3] : -g[3], (ci & 2) ? g[4] : -g[4], (ci & 4) ? g[5] : -g[5]};
-                    f3 l = f3{g[0], g[1], g[2]} + qapply(bq, lb);
-                    cx[ci] = body_point(L, b, l);
-                    cd[ci] = terrain_dist(p, tkind, cx[ci], cnv[ci]);
-                    if (cd[ci] < off) cand[ncand++] = ci;
-                }
-                for (int sel = 0; sel < 4 && ncand > 0; ++sel) {
-                    int best = 0;
-                    for (int j = 1; j < ncand; ++j)
-                        if (cd[cand[j]] < cd[cand[best]]) best = j;
-                    int ci = cand[best];
-                    px[myn] = cx[ci]; pn[myn] = cnv[ci]; pg[myn] = cd[ci]; ++myn;
-                    for (int j = best; j < ncand - 1; ++j) cand[j] = cand[j + 1];
-                    --ncand;
+                    cxs[ci] = body_point(L, b, f3{g[0], g[1], g[2]} + qapply(bq, lb));
+                    cd[ci] = terrain_dist(p, tkind, cxs[ci], cns[ci]);
+                    cand[ci] = cd[ci] < off;
                 }
             }
         }
-        // exclusive scan of per-lane counts (<= 4) across the wave
+        int rank[8];
+        int myn = 0;
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) {
+            int rk = 0;
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj) {
+                // box corners by depth; sphere / capsule end points in geometric order
+                bool before = gt == HE_GEOM_BOX ? (cd[cj] < cd[ci] || (cd[cj] == cd[ci] && cj < ci)) : cj < ci;
+                if (cand[cj] && before) ++rk;
+            }
+            rank[ci] = rk;
+            if (cand[ci] && rk < 4) ++myn;
+        }
         int incl = myn;
-        for (int s = 1; s < W; s <<= 1) {
-            int v = __shfl_up(incl, s, W);
-            if (lane >= s) incl += v;
+        for (int s2 = 1; s2 < W; s2 <<= 1) {
+            int v = __shfl_up(incl, s2, W);
+            if (lane >= s2) incl += v;
         }
         int total = __shfl(incl, W - 1, W);
         int base = incl - myn;
-        for (int k = 0; k < myn; ++k)
-            if (base + k < maxc) store_contact(L, base + k, lane, -1, px[k], pn[k], pg[k], mu);
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci)
+            if (cand[ci] && rank[ci] < 4 && base + rank[ci] < maxc)
+                store_contact(L, base + rank[ci], b, -1, cxs[ci], cns[ci], cd[ci], mu);
         nc = total < maxc ? total : maxc;
     }
     if (p.self_collision && nc < maxc) {
@@ -474,6 +502,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
     if (lane == 0) L.nc = nc;
     if (lane < NB) { L.cf[lane][0] = 0.f; L.cf[lane][1] = 0.f; L.cf[lane][2] = 0.f; }
     sync();
+    STAMP(7);
     if (nc > 0) {
         const int nr = 3 * nc;
         // ---- contact rows: Z[i][r] = J_r^T (dense over the 75 dofs), brow = J_r uf + bias
@@ -505,29 +534,52 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
                 bb = g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             L.brow[r] = ju + bb;
-            // Z <- L^-T Z, row r owned by this lane
-            for (int k = NG - 1; k > 0; --k) {
-                float zk = Z[k * mpad + r];
-                if (zk == 0.f) continue;
-                int d = T.dof_nanc[k] - 1;
-                int rk = T.row_start[k];
-                for (int x = 0; x < d; ++x) Z[T.dof_chain[k][x] * mpad + r] -= L.H[rk + x] * zk;
+            // Z <- L^-T Z for row r (owned by this lane); a terrain row is supported on one chain
+            if (L.cb1[ci] < 0) {
+                const int8_t* ch = T.dof_chain[T.body_last_dof[L.cb0[ci]]];
+                int len = T.dof_nanc[T.body_last_dof[L.cb0[ci]]];
+                for (int x = len - 1; x > 0; --x) {
+                    int k = ch[x];
+                    float zk = Z[k * mpad + r];
+                    int rk = T.row_start[k];
+                    for (int y = 0; y < x; ++y) Z[ch[y] * mpad + r] -= L.H[rk + y] * zk;
+                }
+            } else {
+                for (int k = NG - 1; k > 0; --k) {
+                    float zk = Z[k * mpad + r];
+                    if (zk == 0.f) continue;
+                    int d = T.dof_nanc[k] - 1;
+                    int rk = T.row_start[k];
+                    for (int x = 0; x < d; ++x) Z[T.dof_chain[k][x] * mpad + r] -= L.H[rk + x] * zk;
+                }
             }
         }
         sync();
-        // ---- Delassus A = Z^T D^-1 Z (full symmetric, row r contiguous)
+        STAMP(8);
+        // ---- Delassus A = Z^T D^-1 Z (full symmetric, row r contiguous), summed over the
+        // support chain of whichever row is a terrain row
         for (int t = lane; t < nr * nr; t += W) {
             int r = t / nr, c = t - r * nr;
             if (c > r) continue;
+            int cr = r / 3, cc = c / 3;
             float acc = 0.f;
-            for (int i = 0; i < NG; ++i) {
-                float zr = Z[i * mpad + r];
-                if (zr != 0.f) acc += zr * Z[i * mpad + c] / L.H[T.row_start[i] + T.dof_nanc[i] - 1];
+            int b = L.cb1[cr] < 0 ? L.cb0[cr] : (L.cb1[cc] < 0 ? L.cb0[cc] : -1);
+            if (b >= 0) {
+                int ld = T.body_last_dof[b];
+                const int8_t* ch = T.dof_chain[ld];
+                int len = T.dof_nanc[ld];
+                for (int x = 0; x < len; ++x) {
+                    int i = ch[x];
+                    acc += Z[i * mpad + r] * Z[i * mpad + c] * L.Dinv[i];
+                }
+            } else {
+                for (int i = 0; i < NG; ++i) acc += Z[i * mpad + r] * Z[i * mpad + c] * L.Dinv[i];
             }
             A[r * mpad + c] = acc;
             A[c * mpad + r] = acc;
         }
         sync();
+        STAMP(9);
         // ---- projected Gauss-Seidel; lane l keeps residual w and impulse for rows l and l+64
         float w0 = lane < nr ? L.brow[lane] : 0.f, w1 = lane + W < nr ? L.brow[lane + W] : 0.f;
         float l0 = 0.f, l1 = 0.f;
@@ -555,10 +607,11 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         if (lane < nr) L.brow[lane] = l0;
         if (lane + W < nr) L.brow[lane + W] = l1;
         sync();
+        STAMP(10);
         for (int i = lane; i < NG; i += W) {
             float acc = 0.f;
             for (int r = 0; r < nr; ++r) acc += Z[i * mpad + r] * L.brow[r];
-            L.y[i] = acc / L.H[T.row_start[i] + T.dof_nanc[i] - 1];
+            L.y[i] = acc * L.Dinv[i];
         }
         sync();
         for (int lv = 1; lv < T.num_levels; ++lv) {
@@ -585,6 +638,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
             L.cf[lane][0] = fx / dt; L.cf[lane][1] = fy / dt; L.cf[lane][2] = fz / dt;
         }
         sync();
+        STAMP(11);
     }
     // ---- drive force actually applied, damping, clamps, write velocities
     const float damp = 1.0f / (1.0f + dt * p.angular_damping);
@@ -620,6 +674,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         }
     }
     sync();
+    STAMP(12);
 }
 
 __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a, int mpad) {
@@ -630,7 +685,12 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a, int mpad) {
     const int e = blockIdx.x;
     const int lane = threadIdx.x;
     const he_model& m = *a.model;
-    const PhysTopo& T = *a.topo;
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.topo);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&L.T);
+        for (int i = lane; i < (int)(sizeof(PhysTopo) / 4); i += W) dst[i] = src[i];
+    }
+    const PhysTopo& T = L.T;
     // ---- load state
     const float* rs = a.root_states + (size_t)e * 13;
     if (lane < 3) { L.root_pos[lane] = rs[lane]; L.u0[3 + lane] = rs[7 + lane]; L.u0[lane] = rs[10 + lane]; }
@@ -653,9 +713,12 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a, int mpad) {
     const float* ms = a.mass_scale ? a.mass_scale + (size_t)e * NB : nullptr;
     float mu = a.friction ? a.friction[e] : a.p.friction;
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;
-    for (int s = 0; s < a.substeps; ++s) substep(L, Z, A, mpad, a, m, T, lane, ms, mu, tk);
+    unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * 16 : nullptr;
+    unsigned long long t_prev = __builtin_readcyclecounter();
+    for (int s = 0; s < a.substeps; ++s) substep(L, Z, A, mpad, a, m, T, lane, ms, mu, tk, stamps, t_prev);
     // ---- outputs: generalized state, FK rigid-body state, forces
     kinematics(L, m, T, lane);
+    STAMP(13);
     float* rso = a.root_states + (size_t)e * 13;
     if (lane < 3) { rso[lane] = L.root_pos[lane]; rso[7 + lane] = L.u0[3 + lane]; rso[10 + lane] = L.u0[lane]; }
     if (lane < 4) rso[3 + lane] = L.root_q[lane];

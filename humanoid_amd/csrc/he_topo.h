@@ -25,6 +25,8 @@ struct PhysTopo {
     int16_t level_start[HE_MAX_CHAIN + 1];
     int8_t level_dofs[HE_NUM_GEN];        // dofs grouped by chain length
     uint8_t tri_i[HE_MAX_TRI], tri_j[HE_MAX_TRI];
+    uint8_t ent_row[HE_NNZ_MAX];          // packed entry -> row of the sparse mass matrix
+    int8_t body_last_dof[HE_NUM_BODIES];  // chain(body_last_dof[b]) = all dofs on b's chain
 };
 
 #ifdef __cplusplus
@@ -75,8 +77,13 @@ static inline void he_build_topo(const he_model& m, PhysTopo& t) {
     }
     t.level_start[HE_MAX_CHAIN] = (int16_t)cnt;
     t.num_levels = lvl;
+    for (int i = 0; i < HE_NUM_GEN; ++i)
+        for (int k = 0; k < t.dof_nanc[i]; ++k) t.ent_row[t.row_start[i] + k] = (uint8_t)i;
+    for (int b = 0; b < HE_NUM_BODIES; ++b) t.body_last_dof[b] = (int8_t)(b == 0 ? 5 : 6 + 3 * (b - 1) + 2);
     int p = 0;
     for (int i = 0; i < 29 && p < HE_MAX_TRI; ++i)
         for (int j = 0; j <= i && p < HE_MAX_TRI; ++j) { t.tri_i[p] = (uint8_t)i; t.tri_j[p] = (uint8_t)j; ++p; }
 }
 #endif
+
+static_assert(sizeof(PhysTopo) % 4 == 0, "PhysTopo is copied to LDS in 4-byte words");

@@ -30,7 +30,7 @@ HE_SYMBOLS = (
     "he_get_buffer", "he_set_dof_targets", "he_set_root_state_indexed", "he_set_dof_state_indexed",
     "he_set_dof_targets_indexed", "he_set_env_properties", "he_simulate", "he_set_pd_params", "he_step_actions",
     "he_refresh", "he_load_motions", "he_imitation_step", "he_motion_state", "he_reset_envs", "he_env_step",
-    "he_imitation_reset_step", "he_hash_uniform",
+    "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform",
 )
 
 
@@ -61,6 +61,7 @@ def load_library(path: Optional[str] = None):
         "he_env_step": [V, V, V, V, I, C.c_uint64, C.c_uint64, V, V, V, V, V, V],
         "he_imitation_reset_step": [V, V, V, C.c_uint64, C.c_uint64, V, V, V, V, V, V],
         "he_device_count": [V],
+        "he_set_debug_stamps": [V, V],
     }
     for name, args in sigs.items():
         fn = getattr(lib, name)
@@ -274,10 +275,21 @@ class Engine:
                                         vp(out.get("dof_vel")), self.stream))
         return out
 
-    @staticmethod
-    def env_motion(motion_ids, start_times, start_offsets, global_offset, progress) -> _abi.HeEnvMotion:
-        return _abi.HeEnvMotion(motion_ids.data_ptr(), start_times.data_ptr(), start_offsets.data_ptr(),
-                                global_offset.data_ptr(), progress.data_ptr())
+    def env_motion(self, motion_ids, start_times, start_offsets, global_offset, progress) -> _abi.HeEnvMotion:
+        """Per-env motion bookkeeping block; the returned struct keeps the tensors alive."""
+        import torch
+        n = self.num_envs
+        checks = ((motion_ids, torch.int64, (n,)), (start_times, torch.float32, (n,)),
+                  (start_offsets, torch.float32, (n,)), (global_offset, torch.float32, (n, 3)),
+                  (progress, torch.int16, (n,)))
+        for t, dt, shape in checks:
+            self._contig(t, dt)
+            if tuple(t.shape) != shape:
+                raise EngineError(f"env motion buffer has shape {tuple(t.shape)}, expected {shape}")
+        em = _abi.HeEnvMotion(motion_ids.data_ptr(), start_times.data_ptr(), start_offsets.data_ptr(),
+                              global_offset.data_ptr(), progress.data_ptr())
+        em.keep_alive = (motion_ids, start_times, start_offsets, global_offset, progress)
+        return em
 
     def imitation_step(self, params: _abi.HeImitationParams, em: _abi.HeEnvMotion, obs, rew, reward_raw, reset,
                        terminate):
@@ -308,6 +320,14 @@ class Engine:
                                                 C.c_void_p(rew.data_ptr()), C.c_void_p(reward_raw.data_ptr()),
                                                 C.c_void_p(reset.data_ptr()), C.c_void_p(terminate.data_ptr()),
                                                 self.stream))
+
+    def set_debug_stamps(self, buf=None):
+        """Diagnostics: int64 [num_envs, 16] device tensor receiving per-phase cycles, or None."""
+        import torch
+        if buf is not None:
+            self._contig(buf, torch.int64)
+        self._stamps = buf
+        _check(self.lib.he_set_debug_stamps(self.h, None if buf is None else C.c_void_p(buf.data_ptr())))
 
     def hash_uniform(self, seed, step, env):
         return self.lib.he_hash_uniform(seed, step, env)

@@ -208,6 +208,10 @@ int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he
                             uint64_t step_index, float* obs, float* rew, float* reward_raw, uint8_t* reset,
                             uint8_t* terminate, void* stream);
 
+/* Diagnostics: when non-NULL, the physics kernel accumulates per-phase shader cycles into
+ * device_buffer [N][16] (u64; phases listed in DESIGN.md §4). NULL disables (default). */
+int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer);
+
 /* hash-based uniform used by he_env_step (exposed for parity tests): out[k] for env ids[k]. */
 float he_hash_uniform(uint64_t seed, uint64_t step_index, uint32_t env);
 

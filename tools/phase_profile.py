@@ -1,0 +1,55 @@
+"""Per-phase cycle breakdown of the physics kernel (diagnostic build path: he_set_debug_stamps).
+
+Runs the bench workload (default configs[1], 4096 envs) for a few steps with stamps enabled and
+prints mean shader cycles per env per policy step for each phase.
+Usage: python tools/phase_profile.py [--config standstill|imitation|dr] [--steps 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba", "ltdl factor", "free solve",
+          "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="standstill")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--max-contacts", type=int, default=24)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    from humanoid_amd.model import load_default_model
+    bargs = argparse.Namespace(config=args.config, num_envs=args.num_envs, clips=128, seed=0,
+                               max_contacts=args.max_contacts)
+    model = load_default_model()
+    ro = bench.Rollout(bargs, model, 0, 0)
+    for _ in range(args.warmup):
+        ro.step()
+    buf = torch.zeros(args.num_envs, 16, dtype=torch.int64, device=ro.eng.device)
+    ro.eng.set_debug_stamps(buf)
+    nc = []
+    for _ in range(args.steps):
+        ro.step()
+        nc.append(ro.eng.num_contacts.float().mean().item())
+    torch.cuda.synchronize()
+    ro.eng.set_debug_stamps(None)
+    cyc = buf.cpu().numpy().astype(np.float64) / args.steps
+    mean = cyc.mean(0)
+    total = mean[:len(PHASES)].sum()
+    rows = {PHASES[i]: {"cycles": round(float(mean[i])), "share": round(float(mean[i] / total), 4)}
+            for i in range(len(PHASES))}
+    print(json.dumps({"config": args.config, "num_envs": args.num_envs, "mean_contacts": float(np.mean(nc)),
+                      "cycles_per_env_step": round(float(total)), "phases": rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
