@@ -41,9 +41,9 @@ def parse():
     ap.add_argument("--clips", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=256)
-    ap.add_argument("--cpu-steps", type=int, default=10)
-    ap.add_argument("--max-contacts", type=int, default=24)
+    ap.add_argument("--cpu-envs", type=int, default=2048)
+    ap.add_argument("--cpu-steps", type=int, default=300)
+    ap.add_argument("--max-contacts", type=int, default=20)
     return ap.parse_args()
 
 

@@ -10,7 +10,7 @@ import numpy as np
 from .model import HumanoidModel
 
 NB, ND, NG = 24, 69, 75
-MAX_PAIRS, MAX_CONTACTS = 256, 32
+MAX_PAIRS, MAX_CONTACTS = 256, 21
 OBS_SELF, OBS_TASK, OBS_DIM = 358, 576, 934
 
 BUF_ROOT_STATE, BUF_DOF_STATE, BUF_RB_STATE, BUF_CONTACT_FORCE, BUF_DOF_FORCE, BUF_DOF_TARGET, BUF_NUM_CONTACTS = range(7)
@@ -97,7 +97,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.max_angular_velocity = 100.0
     p.solver_iterations = 8
     p.self_collision = 1
-    p.max_contacts = MAX_CONTACTS
+    p.max_contacts = 20
     p.kp_scale = 1.0
     p.kd_scale = 1.0
     p.terrain = 0

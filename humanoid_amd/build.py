@@ -17,7 +17,7 @@ SOURCES = [
     ("he_physics.hip", []),
     ("he_engine.cpp", ["-x", "hip"]),
 ]
-HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h")]
+HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", "he_regla.h", "he_smpl_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h")]
 
 
 def _hipcc():

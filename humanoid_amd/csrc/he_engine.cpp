@@ -14,7 +14,7 @@
 #include "he_kernels.h"
 #include "he_topo.h"
 
-size_t physics_lds_bytes(int max_contacts, int* mpad_out);
+size_t physics_lds_bytes();
 
 namespace {
 thread_local std::string g_err;

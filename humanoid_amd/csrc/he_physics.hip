@@ -1,23 +1,29 @@
 // he_physics.hip -- articulated SMPL-humanoid step for gfx950 (replaces
 // gym.simulate x control_freq_inv, puffer_phc/envs/humanoid_phc.py:131-134).
 //
-// Mapping: one environment per 64-lane workgroup (one wave), all substeps of a policy step in
-// one launch. Generalized state lives in LDS for the whole launch; HBM sees one coalesced read of
-// the env's root/dof/target rows and one write of root/dof/rigid-body/contact/dof-force rows.
-// Lanes parallelise over bodies (24), dofs (75), sparse mass-matrix entries (1221), contact
-// rows (3 x contacts) and elimination pairs; the tree-ordered sweeps are expressed through static
-// root-first chain tables (he_topo.h) so each lane walks its own chain without waiting on levels.
+// Mapping: one environment per 64-lane workgroup (= one wave), all substeps of a policy step in
+// one launch; HBM sees one coalesced read of the env's root/dof/target rows and one write of the
+// root/dof/rigid-body/contact/dof-force rows.
+//   * tree kinematics / RNEA / CRBA inputs: lane = body or dof, spatial quantities in LDS;
+//   * joint-space algebra (75x75 mass matrix, sparse LTDL, triangular solves): register-resident,
+//     lane j owns column j, fully unrolled over the static SMPL dof tree (he_regla.h);
+//   * contact rows: lane = row, each lane back-substitutes its own J^T row in registers against a
+//     packed copy of L read by LDS broadcast; Delassus rows by lane = column;
+//   * PGS: residuals and impulses in registers, one conflict-free LDS column read per row update.
+// A workgroup is a single wave, so LDS hand-offs between phases need program order only (LDS
+// executes a wave's instructions in order); no s_barrier is issued.
 //
-// Algorithm (DESIGN.md §3, fp64 reference oracle/he_oracle_physics.c):
+// Algorithm (fp64 reference oracle/he_oracle_physics.c):
 //   FK -> spatial axes S about the root origin -> RNEA bias -> CRBA (+armature) -> implicit PD
 //   -> sparse LTDL -> free velocity -> ground/self contacts -> Z = L^-T J^T, A = Z^T D^-1 Z
-//   -> PGS (residuals kept in registers, one LDS column read per row update) -> velocity update
-//   -> damping / clamps -> semi-implicit integration.
+//   -> PGS -> velocity update -> damping / clamps -> semi-implicit integration.
 #include <hip/hip_runtime.h>
 
 #include "../../include/humanoid_engine.h"
 #include "he_kernels.h"
 #include "he_math.h"
+#include "he_regla.h"
+#include "he_smpl_topo.h"
 #include "he_topo.h"
 
 namespace {
@@ -26,28 +32,45 @@ constexpr int NB = HE_NUM_BODIES;
 constexpr int ND = HE_NUM_DOF;
 constexpr int NG = HE_NUM_GEN;
 constexpr int MAXC = HE_MAX_CONTACTS;
+constexpr int MAXR = 3 * MAXC;  // <= 63: one contact row per lane
 constexpr int W = 64;
+static_assert(MAXR <= W - 1, "contact rows must fit one per lane");
+static_assert(smpl::kNG == NG && smpl::kNB == NB, "generated topology mismatch");
+
+struct BodyTopo {
+    int8_t depth[NB];
+    int8_t chain[NB][9];
+    int8_t dof0[NB];
+    uint32_t anc_mask[NB];
+    uint32_t sub_mask[NB];
+};
 
 struct Lds {
     float q[ND], tgt[ND];
-    float u0[NG], uf[NG], y[NG], coef[NG], rhs[NG];
+    float u0[NG], uf[NG], rhs[NG], coef[NG], Dinv[NG], sDinv[NG];
     float ql[NB][4], qw[NB][4], pw[NB][3];
     float S[NG][6], IS[NG][6];
     float V[NB][6], Acc[NB][6], F[NB][6];
     float Ib[NB][10], Ic[NB][10];  // m, h(3), I(xx yy zz xy xz yz)
-    float H[HE_NNZ_MAX];
+    alignas(16) float Lp[smpl::kNpack];  // packed unit-lower factor L (row K: ancestors in chain order)
     float cx[MAXC][3], cn[MAXC][3], ct1[MAXC][3], ct2[MAXC][3], cgap[MAXC], cmu[MAXC];
     int cb0[MAXC], cb1[MAXC];
-    float brow[3 * MAXC];
+    float lam[W];
     float cf[NB][3];
     float dforce[ND];
-    float Dinv[NG];
     float root_pos[3], root_q[4];
     int nc;
-    PhysTopo T;  // static tables copied from global memory once per launch
+    BodyTopo T;
 };
 
-HE_DEV void sync() { __syncthreads(); }
+// wave-level ordering point: one wave per workgroup, LDS executes its instructions in order, so
+// only the compiler must not move memory operations across phase boundaries
+HE_DEV void sync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
 
 // optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
 // s_memtime deltas per phase into stamps[block * 16 + phase]
@@ -120,13 +143,14 @@ HE_DEV void body_segment(const he_model& m, const Lds& L, int b, f3& a, f3& c, f
         a = body_point(L, b, f3{g[0], g[1], g[2]});
         c = body_point(L, b, f3{g[3], g[4], g[5]});
         r = g[6];
-    } else {
-        float e[3] = {g[3], g[4], g[5]};
+    } else {  // box -> capsule proxy along its longest axis
+        float e0 = g[3], e1 = g[4], e2 = g[5];
         int ax = 0;
-        if (e[1] > e[ax]) ax = 1;
-        if (e[2] > e[ax]) ax = 2;
+        float emax = e0;
+        if (e1 > emax) { ax = 1; emax = e1; }
+        if (e2 > emax) { ax = 2; emax = e2; }
         float rp = m.geom_radius[b];
-        float half = fmaxf(e[ax] - rp, 0.f);
+        float half = fmaxf(emax - rp, 0.f);
         f4 bq = f4{g[6], g[7], g[8], g[9]};
         f3 unit = ax == 0 ? f3{1.f, 0.f, 0.f} : (ax == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
         f3 dir = qapply(bq, unit) * half;
@@ -189,8 +213,95 @@ HE_DEV void store_contact(Lds& L, int slot, int b0, int b1, f3 x, f3 n, float ga
     L.cmu[slot] = mu;
 }
 
+// ordered multiply / multiply-add (volatile asm keeps program order against the surrounding LDS
+// reads, so the unrolled sweeps do not hoist every load ahead of the arithmetic)
+template <class T>
+HE_DEV const T* opaque(const T* p) {  // same address through an opaque offset: pins dependent loads
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(p) + off);
+}
+HE_DEV void fmul_ordered(float& z, float a) { asm volatile("v_mul_f32 %0, %0, %1" : "+v"(z) : "v"(a)); }
+HE_DEV void ffma_ordered(float& acc, float a, float b) { asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "v"(a), "v"(b)); }
+
+// Delassus column entries A[RR][lane] for RR < nr, one row per step (constant register indices);
+// dof groups without a nonzero entry in any row are skipped
+constexpr int NGRP = (NG + 3) / 4;
+template <int RR>
+HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uint32_t live) {
+    if constexpr (RR < MAXR) {
+        if (RR >= nr) return;
+        float acc = 0.f;
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) {
+            if ((live >> g) & 1u) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int i = 4 * g + k < NG ? 4 * g + k : 0;
+                    if (4 * g + k < NG) acc = fmaf(regla::rdlane(z[i], RR), z[i], acc);
+                }
+            }
+        }
+        acol[RR] = acc;
+        delassus_rows<RR + 1>(z, acol, nr, live);
+    }
+}
+
+// one Gauss-Seidel sweep over the contacts: normal row clamped at 0, friction rows to the pyramid
+// |lambda_t| <= mu lambda_n; lane r holds w_r, lambda_r, A[r][r]; lane c holds column A[.][c]
+template <int CI>
+HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float diag, int nc, const float* cmu,
+                      int lane) {
+    if constexpr (CI < MAXC) {
+        if (CI >= nc) return;
+        const float mu_c = cmu[CI];
+        float lamn = 0.f;
+#pragma unroll
+        for (int kind = 0; kind < 3; ++kind) {
+            constexpr int R0 = 3 * CI;
+            const int r = R0 + kind;
+            const float wr = regla::rdlane(w, r), lr = regla::rdlane(lamv, r), arr = regla::rdlane(diag, r);
+            float nl = lr - wr / arr;
+            if (kind == 0) {
+                nl = fmaxf(nl, 0.f);
+                lamn = nl;
+            } else {
+                const float bnd = mu_c * lamn;
+                nl = fminf(fmaxf(nl, -bnd), bnd);
+            }
+            w = fmaf(acol[R0 + kind], nl - lr, w);
+            lamv = lane == r ? nl : lamv;
+        }
+        pgs_sweep<CI + 1>(w, lamv, acol, diag, nc, cmu, lane);
+    }
+}
+
+// y <- L^-1 D^-1 L^-T y for a distributed right-hand side (lane i: y[i], lanes < 11: y[64+i])
+template <class LdsT>
+HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
+    using namespace regla;
+    const int dj = smpl::kDofNanc[lane] - 1, dj2 = lane < NH ? smpl::kDofNanc[64 + lane] - 1 : 0;
+    solve_LT_cols<NG - 1>(L.Lp, dj, dj2, yl, y2, lane);
+    yl *= L.Dinv[lane];
+    if (lane < NH) y2 *= L.Dinv[64 + lane];
+    float r1[kRowRegs], r2[kRowRegs];
+    const float4* p1 = reinterpret_cast<const float4*>(L.Lp + smpl::kPackStart[lane]);
+    const float4* p2 = reinterpret_cast<const float4*>(L.Lp + smpl::kPackStart[lane < NH ? 64 + lane : 0]);
+#pragma unroll
+    for (int q = 0; q < kRowRegs / 4; ++q) {
+        const float4 v1 = p1[q], v2 = p2[q];
+        r1[4 * q] = v1.x; r1[4 * q + 1] = v1.y; r1[4 * q + 2] = v1.z; r1[4 * q + 3] = v1.w;
+        r2[4 * q] = v2.x; r2[4 * q + 1] = v2.y; r2[4 * q + 2] = v2.z; r2[4 * q + 3] = v2.w;
+    }
+    const uint64_t a1lo = smpl::kAncLo[lane];
+    const uint64_t a2lo = lane < NH ? smpl::kAncLo[64 + lane] : 0ull;
+    const uint32_t a2hi = lane < NH ? smpl::kAncHi[64 + lane] : 0u;
+    solve_L_rows<0>(r1, r2, a1lo, a2lo, a2hi, yl, y2, lane);
+}
+
 // ---------------------------------------------------------------------------------- kinematics
-HE_DEV void kinematics(Lds& L, const he_model& m, const PhysTopo& T, int lane) {
+HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
+    const BodyTopo& T = L.T;
     if (lane < NB) {
         if (lane == 0) {
             L.ql[0][0] = L.root_q[0]; L.ql[0][1] = L.root_q[1]; L.ql[0][2] = L.root_q[2]; L.ql[0][3] = L.root_q[3];
@@ -201,13 +312,12 @@ HE_DEV void kinematics(Lds& L, const he_model& m, const PhysTopo& T, int lane) {
         }
     }
     sync();
-    if (lane < NB) {
-        // walk this body's chain from the root
+    if (lane < NB) {  // walk this body's chain from the root
         f4 q = qnormalize(f4{L.ql[0][0], L.ql[0][1], L.ql[0][2], L.ql[0][3]});
         f3 p = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
-        int depth = T.body_depth[lane];
+        int depth = T.depth[lane];
         for (int k = 1; k <= depth; ++k) {
-            int a = T.body_chain[lane][k];
+            int a = T.chain[lane][k];
             p = p + qapply(q, f3{m.local_pos[a][0], m.local_pos[a][1], m.local_pos[a][2]});
             q = qmul(q, f4{L.ql[a][0], L.ql[a][1], L.ql[a][2], L.ql[a][3]});
         }
@@ -221,7 +331,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, const PhysTopo& T, int lane) {
         if (i < 6) {
             for (int c = 0; c < 6; ++c) S[c] = (c == i) ? 1.f : 0.f;
         } else {
-            int b = T.dof_body[i], c = (i - 6) % 3;
+            int b = dof_body(i), c = (i - 6) % 3;
             f4 q = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
             f3 e = c == 0 ? f3{1.f, 0.f, 0.f} : (c == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
             f3 a = qapply(q, e);
@@ -232,10 +342,10 @@ HE_DEV void kinematics(Lds& L, const he_model& m, const PhysTopo& T, int lane) {
     sync();
     if (lane < NB) {
         float V[6] = {L.u0[0], L.u0[1], L.u0[2], L.u0[3], L.u0[4], L.u0[5]};
-        int depth = T.body_depth[lane];
+        int depth = T.depth[lane];
         for (int k = 1; k <= depth; ++k) {
-            int a = T.body_chain[lane][k];
-            int d0 = T.body_dof0[a];
+            int a = T.chain[lane][k];
+            int d0 = T.dof0[a];
             for (int c = 0; c < 3; ++c) {
                 float uu = L.u0[d0 + c];
                 for (int x = 0; x < 6; ++x) V[x] += L.S[d0 + c][x] * uu;
@@ -247,15 +357,29 @@ HE_DEV void kinematics(Lds& L, const he_model& m, const PhysTopo& T, int lane) {
 }
 
 // ---------------------------------------------------------------------------------- one substep
-HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, const he_model& m, const PhysTopo& T,
-                    int lane, const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
+HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
+                    const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
                     unsigned long long& t_prev) {
+    using namespace regla;
+    // opaque per substep: keeps the compiler from hoisting ~1k uniform model loads out of the
+    // substep loop into SGPRs (which then spill into VGPR lanes)
+    asm volatile("" : "+s"(mp));
+    const he_model& m = *mp;
+    // likewise an opaque VGPR base for LDS: addresses become base + immediate offset instead of
+    // hundreds of hoisted uniform address constants
+    int lds_off = 0;
+    asm volatile("" : "+v"(lds_off));
+    Lds& L = *reinterpret_cast<Lds*>(reinterpret_cast<char*>(&L0) + lds_off);
+    // and the lane id: the many per-lane predicates of the unrolled algebra are then rebuilt
+    // next to their use instead of being hoisted as loop invariants
+    asm volatile("" : "+v"(lane));
+    const BodyTopo& T = L.T;
     const he_sim_params& p = a.p;
     const float dt = p.dt;
-    kinematics(L, m, T, lane);
+    kinematics(L, m, lane);
     STAMP(0);
     const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
-    // ---- body spatial inertias about o
+    // ---- body spatial inertias about o + RNEA body forces (gravity as base acceleration)
     if (lane < NB) {
         int b = lane;
         float ms = mass_scale ? mass_scale[b] : 1.f;
@@ -266,7 +390,6 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         f3 cw = qapply(q, f3{m.com[b][0], m.com[b][1], m.com[b][2]});
         f3 s = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} + cw - o;
         const float* in = m.inertia[b];
-        // R Ib R^T: columns of R are c0 c1 c2 ; Ib symmetric
         float Ib[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
         float R[3][3] = {{c0.x, c1.x, c2.x}, {c0.y, c1.y, c2.y}, {c0.z, c1.z, c2.z}};
         float T1[3][3];
@@ -282,15 +405,14 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
         float* o10 = L.Ib[b];
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
-        // ---- RNEA bias acceleration along the chain
         float Acc[6];
         f3 vxw = cross3(f3{L.u0[3], L.u0[4], L.u0[5]}, f3{L.u0[0], L.u0[1], L.u0[2]});
         Acc[0] = 0.f; Acc[1] = 0.f; Acc[2] = 0.f;
         Acc[3] = vxw.x - p.gravity[0]; Acc[4] = vxw.y - p.gravity[1]; Acc[5] = vxw.z - p.gravity[2];
-        int depth = T.body_depth[b];
+        int depth = T.depth[b];
         for (int k = 1; k <= depth; ++k) {
-            int ab = T.body_chain[b][k];
-            int d0 = T.body_dof0[ab];
+            int ab = T.chain[b][k];
+            int d0 = T.dof0[ab];
             for (int c = 0; c < 3; ++c) {
                 float cr[6];
                 crm(L.V[ab], L.S[d0 + c], cr);
@@ -322,7 +444,7 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
     STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
     for (int i = lane; i < NG; i += W) {
-        int b = T.dof_body[i];
+        int b = dof_body(i);
         float bias = dot6(L.S[i], L.F[b]);
         si_apply(L.Ic[b], L.S[i], L.IS[i]);
         float rhs = -bias, cf = 0.f;
@@ -343,65 +465,49 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
     }
     sync();
     STAMP(3);
-    // ---- CRBA entries H(i, j) = S_j . IS_i for j in chain(i); + armature + implicit drive terms
-    for (int e = lane; e < T.nnz; e += W) {
-        int i = T.ent_row[e], pos = e - T.row_start[i];
-        int j = T.dof_chain[i][pos];
-        float h = dot6(L.S[j], L.IS[i]);
-        if (j == i && i >= 6) h += m.armature[i - 6] + dt * L.coef[i];
-        L.H[e] = h;
-    }
-    sync();
-    STAMP(4);
-    // ---- sparse LTDL (RBDA 6.5) by dof level: all dofs with the same chain length are eliminated
-    // together (their updates only touch shared ancestors -> LDS float atomics); rows are scaled
-    // by their pivots in one pass at the end.
-    for (int len = T.num_levels; len >= 2; --len) {
-        const int d = len - 1, npairs = d * (d + 1) / 2;
-        const int k0 = T.level_start[len - 1], total = (T.level_start[len] - k0) * npairs;
-        for (int t = lane; t < total; t += W) {
-            int kk = t / npairs, pr = t - kk * npairs;
-            int k = T.level_dofs[k0 + kk];
-            int rk = T.row_start[k];
-            int ix = T.tri_i[pr], jx = T.tri_j[pr];
-            int i = T.dof_chain[k][ix];
-            atomicAdd(&L.H[T.row_start[i] + jx], -L.H[rk + ix] * L.H[rk + jx] / L.H[rk + d]);
+    // ---- CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i
+    RegMat M;
+    {
+        float Sj[6], Sj2[6];
+        for (int x = 0; x < 6; ++x) { Sj[x] = L.S[lane][x]; Sj2[x] = lane < NH ? L.S[64 + lane][x] : 0.f; }
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+            float IS[6];
+            for (int x = 0; x < 6; ++x) IS[x] = L.IS[i][x];
+            const bool in = (smpl::kAncLo[i] >> lane) & 1ull;
+            float h = in ? dot6(Sj, IS) : 0.f;
+            if (i >= 6 && lane == i) h += m.armature[i >= 6 ? i - 6 : 0] + dt * L.coef[i];
+            M.c[i] = h;
+            if (i >= 64) {
+                const bool in2 = lane < NH && ((smpl::kAncHi[i] >> lane) & 1u);
+                float h2 = in2 ? dot6(Sj2, IS) : 0.f;
+                if (lane == i - 64) h2 += m.armature[i - 6] + dt * L.coef[i];
+                M.c2[i >= 64 ? i - 64 : 0] = h2;
+            }
         }
-        sync();
     }
-    for (int i = lane; i < NG; i += W) L.Dinv[i] = 1.0f / L.H[T.row_start[i] + T.dof_nanc[i] - 1];
-    sync();
-    for (int e = lane; e < T.nnz; e += W) {
-        int i = T.ent_row[e];
-        if (e - T.row_start[i] < T.dof_nanc[i] - 1) L.H[e] *= L.Dinv[i];
+    STAMP(4);
+    // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
+    {
+        float Dl = 1.f, D2 = 1.f;
+        factor<NG - 1>(M, Dl, D2, lane);
+        L.Dinv[lane] = 1.0f / Dl;
+        L.sDinv[lane] = 1.0f / sqrtf(Dl);
+        if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
+        store_packed<NG - 1>(M, L.Lp, lane, smpl::kDofNanc[lane] - 1,
+                             lane < NH ? smpl::kDofNanc[64 + lane] - 1 : 0);
     }
-    for (int i = lane; i < NG; i += W) L.y[i] = L.rhs[i];
     sync();
     STAMP(5);
-    // ---- free velocity: du = L^-1 D^-1 L^-T rhs (both sweeps level-parallel)
-    for (int len = T.num_levels; len >= 2; --len) {  // L^-T: push to ancestors, deepest level first
-        const int d = len - 1, k0 = T.level_start[len - 1], total = (T.level_start[len] - k0) * d;
-        for (int t = lane; t < total; t += W) {
-            int kk = t / d, x = t - kk * d;
-            int k = T.level_dofs[k0 + kk];
-            atomicAdd(&L.y[T.dof_chain[k][x]], -L.H[T.row_start[k] + x] * L.y[k]);
-        }
-        sync();
+    // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs)
+    {
+        float yl = L.rhs[lane], y2 = lane < NH ? L.rhs[64 + lane] : 0.f;
+        joint_space_solve(L, yl, y2, lane);
+        L.uf[lane] = L.u0[lane] + yl;
+        if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
     }
-    for (int i = lane; i < NG; i += W) L.y[i] *= L.Dinv[i];
     sync();
-    for (int lv = 1; lv < T.num_levels; ++lv) {  // L^-1: pull from ancestors, shallowest first
-        for (int t = T.level_start[lv] + lane; t < T.level_start[lv + 1]; t += W) {
-            int k = T.level_dofs[t];
-            int rk = T.row_start[k];
-            float acc = L.y[k];
-            for (int x = 0; x < lv; ++x) acc -= L.H[rk + x] * L.y[T.dof_chain[k][x]];
-            L.y[k] = acc;
-        }
-        sync();
-        STAMP(6);
-    }
-    for (int i = lane; i < NG; i += W) L.uf[i] = L.u0[i] + L.y[i];
+    STAMP(6);
     // ---- contacts: terrain (bodies in order, box corners deepest-first), then self pairs
     const int maxc = p.max_contacts < MAXC ? p.max_contacts : MAXC;
     const float off = p.contact_offset;
@@ -504,147 +610,105 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
     sync();
     STAMP(7);
     if (nc > 0) {
+        // ---- contact rows, one per lane: z = J_r^T, brow = J_r uf + bias, then z <- D^-1/2 L^-T z
+        // (dofs outside every row's support stay zero and are skipped wave-uniformly), so that the
+        // Delassus operator A = Zh Zh^T is a plain Gram matrix of the lanes' registers
         const int nr = 3 * nc;
-        // ---- contact rows: Z[i][r] = J_r^T (dense over the 75 dofs), brow = J_r uf + bias
-        for (int t = lane; t < NG * nr; t += W) {
-            int i = t / nr, r = t - i * nr;
-            int ci = r / 3, kind = r - 3 * ci;
+        float brow = 0.f, diag = 0.f, lamv = 0.f;
+        float acol[MAXR];  // lane c: A[r][c]
+        {
+            float z[NG];
+            const int r = lane < nr ? lane : 0;
+            const int ci = r / 3, kind = r - 3 * ci;
             const float* dir = kind == 0 ? L.cn[ci] : (kind == 1 ? L.ct1[ci] : L.ct2[ci]);
-            int bi = T.dof_body[i];
-            float sgn = (T.anc_mask[L.cb0[ci]] >> bi & 1u) ? 1.f : 0.f;
-            if (L.cb1[ci] >= 0 && (T.anc_mask[L.cb1[ci]] >> bi & 1u)) sgn -= 1.f;
-            float z = 0.f;
-            if (sgn != 0.f) {
-                f3 xo = f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o;
-                f3 dd = f3{dir[0], dir[1], dir[2]};
-                f3 rho = cross3(xo, dd);
-                const float* S = L.S[i];
-                z = sgn * (S[0] * rho.x + S[1] * rho.y + S[2] * rho.z + S[3] * dd.x + S[4] * dd.y + S[5] * dd.z);
+            const uint32_t anc0 = lane < nr ? T.anc_mask[L.cb0[ci]] : 0u;
+            const uint32_t anc1 = (lane < nr && L.cb1[ci] >= 0) ? T.anc_mask[L.cb1[ci]] : 0u;
+            const f3 dd = f3{dir[0], dir[1], dir[2]};
+            const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o, dd);
+#pragma unroll
+            for (int i = 0; i < NG; ++i) {
+                const Lds& Lg = *opaque(&L);  // the LDS reads of dof i stay at this point
+                const int bi = smpl::kDofBody[i];
+                const float sgn = (float)((anc0 >> bi) & 1u) - (float)((anc1 >> bi) & 1u);
+                const float* S = Lg.S[i];
+                z[i] = sgn * (S[0] * rho.x + S[1] * rho.y + S[2] * rho.z + S[3] * dd.x + S[4] * dd.y + S[5] * dd.z);
+                ffma_ordered(brow, z[i], Lg.uf[i]);
             }
-            Z[i * mpad + r] = z;
-        }
-        sync();
-        for (int r = lane; r < nr; r += W) {
-            float ju = 0.f;
-            for (int i = 0; i < NG; ++i) ju += Z[i * mpad + r] * L.uf[i];
-            int ci = r / 3;
-            float bb = 0.f;
-            if (r - 3 * ci == 0) {
-                float g = L.cgap[ci];
-                bb = g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
+            if (lane < nr && kind == 0) {
+                const float g = L.cgap[ci];
+                brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
-            L.brow[r] = ju + bb;
-            // Z <- L^-T Z for row r (owned by this lane); a terrain row is supported on one chain
-            if (L.cb1[ci] < 0) {
-                const int8_t* ch = T.dof_chain[T.body_last_dof[L.cb0[ci]]];
-                int len = T.dof_nanc[T.body_last_dof[L.cb0[ci]]];
-                for (int x = len - 1; x > 0; --x) {
-                    int k = ch[x];
-                    float zk = Z[k * mpad + r];
-                    int rk = T.row_start[k];
-                    for (int y = 0; y < x; ++y) Z[ch[y] * mpad + r] -= L.H[rk + y] * zk;
-                }
-            } else {
-                for (int k = NG - 1; k > 0; --k) {
-                    float zk = Z[k * mpad + r];
-                    if (zk == 0.f) continue;
-                    int d = T.dof_nanc[k] - 1;
-                    int rk = T.row_start[k];
-                    for (int x = 0; x < d; ++x) Z[T.dof_chain[k][x] * mpad + r] -= L.H[rk + x] * zk;
-                }
-            }
-        }
-        sync();
-        STAMP(8);
-        // ---- Delassus A = Z^T D^-1 Z (full symmetric, row r contiguous), summed over the
-        // support chain of whichever row is a terrain row
-        for (int t = lane; t < nr * nr; t += W) {
-            int r = t / nr, c = t - r * nr;
-            if (c > r) continue;
-            int cr = r / 3, cc = c / 3;
-            float acc = 0.f;
-            int b = L.cb1[cr] < 0 ? L.cb0[cr] : (L.cb1[cc] < 0 ? L.cb0[cc] : -1);
-            if (b >= 0) {
-                int ld = T.body_last_dof[b];
-                const int8_t* ch = T.dof_chain[ld];
-                int len = T.dof_nanc[ld];
-                for (int x = 0; x < len; ++x) {
-                    int i = ch[x];
-                    acc += Z[i * mpad + r] * Z[i * mpad + c] * L.Dinv[i];
-                }
-            } else {
-                for (int i = 0; i < NG; ++i) acc += Z[i * mpad + r] * Z[i * mpad + c] * L.Dinv[i];
-            }
-            A[r * mpad + c] = acc;
-            A[c * mpad + r] = acc;
-        }
-        sync();
-        STAMP(9);
-        // ---- projected Gauss-Seidel; lane l keeps residual w and impulse for rows l and l+64
-        float w0 = lane < nr ? L.brow[lane] : 0.f, w1 = lane + W < nr ? L.brow[lane + W] : 0.f;
-        float l0 = 0.f, l1 = 0.f;
-        for (int it = 0; it < p.solver_iterations; ++it) {
-            for (int ci = 0; ci < nc; ++ci) {
-                float lamn = 0.f;
-                for (int kind = 0; kind < 3; ++kind) {
-                    int r = 3 * ci + kind;
-                    float wr = r < W ? __shfl(w0, r, W) : __shfl(w1, r - W, W);
-                    float lr = r < W ? __shfl(l0, r, W) : __shfl(l1, r - W, W);
-                    float arr = A[r * mpad + r] + 1e-12f;
-                    float nl = lr - wr / arr;
-                    if (kind == 0) { nl = fmaxf(nl, 0.f); lamn = nl; }
-                    else { float bnd = L.cmu[ci] * lamn; nl = fminf(fmaxf(nl, -bnd), bnd); }
-                    float del = nl - lr;
-                    if (del != 0.f) {
-                        if (lane < nr) w0 += A[r * mpad + lane] * del;
-                        if (lane + W < nr) w1 += A[r * mpad + lane + W] * del;
-                        if (r < W) { if (lane == r) l0 = nl; } else { if (lane == r - W) l1 = nl; }
+            zbs<NG - 1>(L.Lp, z);
+            uint32_t live = 0u;  // groups of 4 dofs with a nonzero entry in some row
+#pragma unroll
+            for (int g = 0; g < NGRP; ++g) {
+                const Lds& Lg = *opaque(&L);
+                bool nz = false;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * g + k < NG) {
+                        fmul_ordered(z[4 * g + k < NG ? 4 * g + k : 0], Lg.sDinv[4 * g + k < NG ? 4 * g + k : 0]);
+                        nz |= z[4 * g + k < NG ? 4 * g + k : 0] != 0.f;
                     }
-                }
+                if (__ballot(nz)) live |= 1u << g;
             }
+#pragma unroll
+            for (int i = 0; i < NG; ++i) ffma_ordered(diag, z[i], z[i]);
+            STAMP(8);
+            // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
+            delassus_rows<0>(z, acol, nr, live);
         }
-        // ---- du = L^-1 D^-1 (Z lambda)
-        if (lane < nr) L.brow[lane] = l0;
-        if (lane + W < nr) L.brow[lane + W] = l1;
+        STAMP(9);
+        // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
+        {
+            float w = lane < nr ? brow : 0.f;
+            diag = lane < nr ? diag + 1e-12f : 1.f;
+            for (int it = 0; it < p.solver_iterations; ++it) pgs_sweep<0>(w, lamv, acol, diag, nc, L.cmu, lane);
+        }
+        L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();
         STAMP(10);
-        for (int i = lane; i < NG; i += W) {
-            float acc = 0.f;
-            for (int r = 0; r < nr; ++r) acc += Z[i * mpad + r] * L.brow[r];
-            L.y[i] = acc * L.Dinv[i];
-        }
-        sync();
-        for (int lv = 1; lv < T.num_levels; ++lv) {
-            for (int t = T.level_start[lv] + lane; t < T.level_start[lv + 1]; t += W) {
-                int k = T.level_dofs[t];
-                int rk = T.row_start[k];
-                float acc = L.y[k];
-                for (int x = 0; x < lv; ++x) acc -= L.H[rk + x] * L.y[T.dof_chain[k][x]];
-                L.y[k] = acc;
-            }
-            sync();
-        }
-        for (int i = lane; i < NG; i += W) L.uf[i] += L.y[i];
+        // ---- contact impulses -> body spatial impulses (about o) and reported contact forces
         if (lane < NB) {
-            float fx = 0.f, fy = 0.f, fz = 0.f;
-            for (int ci = 0; ci < nc; ++ci) {
-                float s = L.cb0[ci] == lane ? 1.f : (L.cb1[ci] == lane ? -1.f : 0.f);
+            float F6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < nc; ++c) {
+                const float s = L.cb0[c] == lane ? 1.f : (L.cb1[c] == lane ? -1.f : 0.f);
                 if (s == 0.f) continue;
-                float ln = L.brow[3 * ci], la = L.brow[3 * ci + 1], lb = L.brow[3 * ci + 2];
-                fx += s * (ln * L.cn[ci][0] + la * L.ct1[ci][0] + lb * L.ct2[ci][0]);
-                fy += s * (ln * L.cn[ci][1] + la * L.ct1[ci][1] + lb * L.ct2[ci][1]);
-                fz += s * (ln * L.cn[ci][2] + la * L.ct1[ci][2] + lb * L.ct2[ci][2]);
+                const float ln = L.lam[3 * c], la = L.lam[3 * c + 1], lb = L.lam[3 * c + 2];
+                const f3 f = f3{ln * L.cn[c][0] + la * L.ct1[c][0] + lb * L.ct2[c][0],
+                                ln * L.cn[c][1] + la * L.ct1[c][1] + lb * L.ct2[c][1],
+                                ln * L.cn[c][2] + la * L.ct1[c][2] + lb * L.ct2[c][2]} * s;
+                const f3 n = cross3(f3{L.cx[c][0], L.cx[c][1], L.cx[c][2]} - o, f);
+                F6[0] += n.x; F6[1] += n.y; F6[2] += n.z; F6[3] += f.x; F6[4] += f.y; F6[5] += f.z;
             }
-            L.cf[lane][0] = fx / dt; L.cf[lane][1] = fy / dt; L.cf[lane][2] = fz / dt;
+            for (int x = 0; x < 6; ++x) L.Acc[lane][x] = F6[x];
+            L.cf[lane][0] = F6[3] / dt; L.cf[lane][1] = F6[4] / dt; L.cf[lane][2] = F6[5] / dt;
         }
         sync();
-        STAMP(11);
+        if (lane < NB) {
+            const uint32_t sm = T.sub_mask[lane];
+            float Fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (int d = 0; d < NB; ++d)
+                if (sm >> d & 1u)
+                    for (int x = 0; x < 6; ++x) Fs[x] += L.Acc[d][x];
+            for (int x = 0; x < 6; ++x) L.F[lane][x] = Fs[x];
+        }
+        sync();
+        // ---- du = L^-1 D^-1 L^-T (J^T lambda), generalized impulse tau_i = S_i . F_subtree(body(i))
+        {
+            float yl = dot6(L.S[lane], L.F[dof_body(lane)]);
+            float y2 = lane < NH ? dot6(L.S[64 + lane], L.F[dof_body(64 + lane)]) : 0.f;
+            joint_space_solve(L, yl, y2, lane);
+            L.uf[lane] += yl;
+            if (lane < NH) L.uf[64 + lane] += y2;
+        }
+        sync();
     }
+    STAMP(11);
     // ---- drive force actually applied, damping, clamps, write velocities
     const float damp = 1.0f / (1.0f + dt * p.angular_damping);
-    for (int i = lane; i < NG; i += W) {
+    for (int i = lane; i < NG; i += W)
         if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
-    }
     sync();
     if (lane < NB) {
         int d0 = lane == 0 ? 0 : 6 + 3 * (lane - 1);
@@ -677,20 +741,21 @@ HE_DEV void substep(Lds& L, float* Z, float* A, int mpad, const PhysArgs& a, con
     STAMP(12);
 }
 
-__global__ void __launch_bounds__(64) physics_kernel(PhysArgs a, int mpad) {
+__global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
-    float* Z = smem + (sizeof(Lds) + 3) / 4;
-    float* A = Z + NG * mpad;
     const int e = blockIdx.x;
     const int lane = threadIdx.x;
     const he_model& m = *a.model;
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.topo);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&L.T);
-        for (int i = lane; i < (int)(sizeof(PhysTopo) / 4); i += W) dst[i] = src[i];
+    // ---- body-level tree tables into LDS
+    if (lane < NB) {
+        const PhysTopo& T = *a.topo;
+        L.T.depth[lane] = T.body_depth[lane];
+        for (int k = 0; k < 9; ++k) L.T.chain[lane][k] = T.body_chain[lane][k];
+        L.T.dof0[lane] = T.body_dof0[lane];
+        L.T.anc_mask[lane] = T.anc_mask[lane];
+        L.T.sub_mask[lane] = T.sub_mask[lane];
     }
-    const PhysTopo& T = L.T;
     // ---- load state
     const float* rs = a.root_states + (size_t)e * 13;
     if (lane < 3) { L.root_pos[lane] = rs[lane]; L.u0[3 + lane] = rs[7 + lane]; L.u0[lane] = rs[10 + lane]; }
@@ -715,9 +780,9 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a, int mpad) {
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;
     unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * 16 : nullptr;
     unsigned long long t_prev = __builtin_readcyclecounter();
-    for (int s = 0; s < a.substeps; ++s) substep(L, Z, A, mpad, a, m, T, lane, ms, mu, tk, stamps, t_prev);
+    for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev);
     // ---- outputs: generalized state, FK rigid-body state, forces
-    kinematics(L, m, T, lane);
+    kinematics(L, m, lane);
     STAMP(13);
     float* rso = a.root_states + (size_t)e * 13;
     if (lane < 3) { rso[lane] = L.root_pos[lane]; rso[7 + lane] = L.u0[3 + lane]; rso[10 + lane] = L.u0[lane]; }
@@ -746,20 +811,11 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a, int mpad) {
 
 }  // namespace
 
-size_t physics_lds_bytes(int max_contacts, int* mpad_out) {
-    int m = 3 * (max_contacts < 1 ? 1 : (max_contacts > MAXC ? MAXC : max_contacts));
-    int mpad = m;
-    if (mpad_out) *mpad_out = mpad;
-    return ((sizeof(Lds) + 3) / 4) * 4 + (size_t)(NG * mpad + mpad * mpad) * sizeof(float);
-}
+size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16; }
 
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream) {
     if (a.num_envs <= 0) return hipSuccess;
-    int mpad = 0;
-    size_t lds = physics_lds_bytes(a.p.max_contacts, &mpad);
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(physics_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (err != hipSuccess) return err;
-    physics_kernel<<<a.num_envs, W, lds, stream>>>(a, mpad);
+    const size_t lds = physics_lds_bytes();
+    physics_kernel<<<a.num_envs, W, lds, stream>>>(a);
     return hipGetLastError();
 }

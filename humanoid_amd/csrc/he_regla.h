@@ -1,0 +1,210 @@
+// he_regla.h -- wave-resident dense linear algebra on the static SMPL dof tree (gfx950).
+//
+// The 75x75 joint-space inertia H lives in VGPRs, one column per lane: lane j holds c[i] =
+// H[i][j] for every row i (entries with i >= j are the lower triangle; i < j slots are scratch),
+// and lanes 0..10 additionally hold c2[i-64] = H[i][64+j] for the 11 dofs >= 64. Every loop over
+// the tree is unrolled at compile time by template recursion over the constexpr tables in
+// he_smpl_topo.h, so all register indices are immediates and the uniform factors travel through
+// v_readlane -> SGPR. Branch-induced sparsity (RBDA 6.5) means no fill-in: entries outside a
+// row's ancestor chain stay exactly zero.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "he_smpl_topo.h"
+
+namespace regla {
+
+using namespace smpl;
+constexpr int W = 64;
+constexpr int NG = kNG;
+constexpr int NH = NG - 64;  // columns held in the second register set
+
+struct RegMat {
+    float c[NG];
+    float c2[NH];
+};
+
+__device__ __forceinline__ float rdlane(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// v_writelane: `v` on lane `l` only
+template <int LANE>
+__device__ __forceinline__ float wrlane(float v, float old) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(v), "i"(LANE));
+    return old;
+}
+
+// H[ROW][COL] (ROW >= COL) from the owning lane, as a wave-uniform value
+template <int ROW, int COL>
+__device__ __forceinline__ float get(const RegMat& M) {
+    static_assert(ROW >= COL, "lower triangle only");
+    if constexpr (COL < 64) return rdlane(M.c[ROW], COL);
+    else return rdlane(M.c2[ROW - 64], COL - 64);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+    return v;
+}
+
+// ---------------------------------------------------------------- LTDL factorisation
+__device__ __forceinline__ float uniform(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// H[I][j] -= H[K][I] * L[K][j] for every column j (c[K] already scaled to row K of L)
+template <int K, int X, int D>
+__device__ __forceinline__ void fac_anc(RegMat& M, const float (&hk)[kMaxChain]) {
+    if constexpr (X < D) {
+        constexpr int I = kChain[K][X];
+        M.c[I] -= hk[X] * M.c[K];
+        if constexpr (I >= 64) M.c2[I - 64] -= hk[X] * M.c2[K - 64];
+        fac_anc<K, X + 1, D>(M, hk);
+    }
+}
+template <int K, int X, int D>
+__device__ __forceinline__ void read_row(const RegMat& M, float (&hk)[kMaxChain]) {
+    if constexpr (X < D) {
+        hk[X] = get<K, kChain[K][X]>(M);
+        read_row<K, X + 1, D>(M, hk);
+    }
+}
+
+// eliminate dof K (deepest first); the pivot D_K is kept on its owning lane (Dl / D2). The pivot
+// reciprocal and the row entries H[K][I] are wave-uniform (SGPRs), so each update is one FMA.
+template <int K>
+__device__ __forceinline__ void factor(RegMat& M, float& Dl, float& D2, int lane) {
+    if constexpr (K >= 0) {
+        constexpr int D = kDofNanc[K] - 1;
+        const float dk = get<K, K>(M);
+        const float inv = uniform(1.0f / dk);
+        float hk[kMaxChain];
+        read_row<K, 0, D>(M, hk);
+        M.c[K] *= inv;  // row K -> L[K][.] on lanes j < K
+        if constexpr (K >= 64) M.c2[K - 64] *= inv;
+        fac_anc<K, 0, D>(M, hk);
+        if constexpr (K < 64) Dl = wrlane<K>(dk, Dl);
+        else D2 = wrlane<K - 64>(dk, D2);
+        __builtin_amdgcn_sched_barrier(0);  // one elimination step at a time: bounded SGPR/VGPR live ranges
+        factor<K - 1>(M, Dl, D2, lane);
+    }
+}
+
+// ---------------------------------------------------------------- y <- L^-T y (y distributed: lane i holds y[i], y2 = y[64+i])
+template <int K>
+__device__ __forceinline__ void solve_LT(const RegMat& M, float& yl, float& y2, int lane) {
+    if constexpr (K >= 1) {
+        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
+        if (lane < K) yl -= M.c[K] * yk;
+        if constexpr (K > 64) {
+            if (lane < K - 64) y2 -= M.c2[K - 64] * yk;
+        }
+        solve_LT<K - 1>(M, yl, y2, lane);
+    }
+}
+
+// ---------------------------------------------------------------- y <- L^-1 y
+template <int K>
+__device__ __forceinline__ void solve_L(const RegMat& M, float& yl, float& y2, int lane) {
+    if constexpr (K < NG) {
+        float p = lane < K ? M.c[K] * yl : 0.0f;
+        if constexpr (K > 64) p += lane < K - 64 ? M.c2[K - 64] * y2 : 0.0f;
+        const float s = wave_sum(p);
+        if constexpr (K < 64) {
+            if (lane == K) yl -= s;
+        } else {
+            if (lane == K - 64) y2 -= s;
+        }
+        solve_L<K + 1>(M, yl, y2, lane);
+    }
+}
+
+// ---------------------------------------------------------------- packed copy of L for broadcast reads
+// Lp[kPackStart[K] + x] = L[K][kChain[K][x]] for x < depth(K) (rows padded to 4 floats): lane j
+// writes the entries of its column j; pad slots are loaded but never used
+template <int K>
+__device__ __forceinline__ void store_packed(const RegMat& M, float* Lp, int lane, int lane_depth,
+                                             int lane_depth2) {
+    if constexpr (K >= 1) {
+        if (lane < K && ((kAncLo[K] >> lane) & 1ull)) Lp[kPackStart[K] + lane_depth] = M.c[K];
+        if constexpr (K > 64) {
+            if (lane < K - 64 && ((kAncHi[K] >> lane) & 1u)) Lp[kPackStart[K] + lane_depth2] = M.c2[K - 64];
+        }
+        store_packed<K - 1>(M, Lp, lane, lane_depth, lane_depth2);
+    }
+}
+
+// z -= a * b as an ordered instruction: the DAG linearisation would otherwise sink the whole
+// unrolled sweep's FMAs below its LDS reads and spill the loaded rows
+__device__ __forceinline__ void fnma(float& z, float a, float b) {
+    asm volatile("v_fma_f32 %0, -%1, %2, %0" : "+v"(z) : "v"(a), "v"(b));
+}
+
+// ---------------------------------------------------------------- per-lane z <- L^-T z (each lane its own rhs)
+template <int K, int X, int D>
+__device__ __forceinline__ void zbs_anc(const float* row, float (&z)[NG], float zk) {
+    if constexpr (X < D) {
+        const float4 v = *reinterpret_cast<const float4*>(row + X);
+        fnma(z[kChain[K][X]], v.x, zk);
+        if constexpr (X + 1 < D) fnma(z[kChain[K][X + 1]], v.y, zk);
+        if constexpr (X + 2 < D) fnma(z[kChain[K][X + 2]], v.z, zk);
+        if constexpr (X + 3 < D) fnma(z[kChain[K][X + 3]], v.w, zk);
+        zbs_anc<K, X + 4, D>(row, z, zk);
+    }
+}
+template <int K>
+__device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG]) {
+    if constexpr (K >= 1) {
+        // the row offset passes through an opaque VGPR at this point of the program, so the LDS
+        // reads of row K cannot be hoisted ahead of the sweep (which would need ~1k VGPRs)
+        const float zk = z[K];
+        if (__ballot(zk != 0.f)) {  // dof outside every row's (ancestor-closed) support: no-op
+            int off = kPackStart[K];
+            asm volatile("" : "+v"(off));
+            zbs_anc<K, 0, kDofNanc[K] - 1>(Lp + off, z, zk);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        zbs<K - 1>(Lp, z);
+    }
+}
+
+// ---------------------------------------------------------------- y <- L^-1 y, row-distributed
+// lane i holds row i of L as r1[x] = L[i][kChain[i][x]] (and r2 for dof 64+i); the position of an
+// ancestor K in any chain through it is its depth, a compile-time constant, so each step is one
+// v_readlane of y_K plus a masked FMA -- no cross-lane reduction.
+constexpr int kRowRegs = 32;
+template <int K>
+__device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs],
+                                             uint64_t a1lo, uint64_t a2lo, uint32_t a2hi, float& yl,
+                                             float& y2, int lane) {
+    if constexpr (K < NG) {
+        constexpr int d = kDofNanc[K] - 1 < kRowRegs ? kDofNanc[K] - 1 : 0;
+        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
+        if constexpr (K < 64) {
+            if (((a1lo >> K) & 1ull) && lane != K) yl -= r1[d] * yk;
+            if ((a2lo >> K) & 1ull) y2 -= r2[d] * yk;
+        } else {
+            if (((a2hi >> (K - 64)) & 1u) && lane != K - 64) y2 -= r2[d] * yk;
+        }
+        solve_L_rows<K + 1>(r1, r2, a1lo, a2lo, a2hi, yl, y2, lane);
+    }
+}
+
+// ---------------------------------------------------------------- y <- L^-T y, column-distributed
+// lane j gathers L[K][j] = Lp[kPackStart[K] + depth(j)] for every descendant K (masked by the
+// compile-time ancestor sets) and updates its own y_j; y_K travels by v_readlane
+template <int K>
+__device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, float& yl, float& y2, int lane) {
+    if constexpr (K >= 1) {
+        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
+        if (lane < K && ((kAncLo[K] >> lane) & 1ull)) yl -= Lp[kPackStart[K] + dj] * yk;
+        if constexpr (K > 64) {
+            if (lane < K - 64 && ((kAncHi[K] >> lane) & 1u)) y2 -= Lp[kPackStart[K] + dj2] * yk;
+        }
+        solve_LT_cols<K - 1>(Lp, dj, dj2, yl, y2, lane);
+    }
+}
+
+}  // namespace regla

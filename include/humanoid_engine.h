@@ -27,7 +27,7 @@ extern "C" {
 #define HE_NUM_DOF 69
 #define HE_NUM_GEN 75          /* 6 root + 69 joint generalized velocities */
 #define HE_MAX_PAIRS 256
-#define HE_MAX_CONTACTS 32
+#define HE_MAX_CONTACTS 21       /* 3 rows each: all contact rows of an env fit one 64-lane wave */
 #define HE_OBS_SELF 358
 #define HE_OBS_TASK 576
 #define HE_OBS_DIM 934         /* humanoid_phc.py:458-467 */

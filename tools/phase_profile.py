@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--num-envs", type=int, default=4096)
-    ap.add_argument("--max-contacts", type=int, default=24)
+    ap.add_argument("--max-contacts", type=int, default=20)
     args = ap.parse_args()
     import numpy as np
     import torch
