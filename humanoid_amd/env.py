@@ -1,0 +1,428 @@
+"""Host-side mirror of the reference's environment classes on the HIP engine.
+
+``HumanoidPHC`` follows ``puffer_phc/envs/humanoid_phc.py`` (reset / step / motion resampling /
+eval toggles, same buffers and ``extras`` keys). ``PHCPufferEnv`` follows
+``puffer_phc/clean_pufferl/env.py:40-210`` (terminals / truncations / masks, episode statistics,
+info every ``log_interval`` ticks).
+
+Differences, all on the performance side:
+* ``HumanoidPHC.step`` is two launches (physics with the action->PD-target map fused in, then the
+  fused reward/reset/observation kernel) instead of ~200 eager torch ops;
+* ``PHCPufferEnv.step`` resets the flagged envs on the device inside the same launch
+  (``he_imitation_reset_step``) and keeps episode statistics on the device, so a step performs no
+  host synchronisation except the one-off ``info`` read every ``log_interval`` ticks. Reset
+  phases come from a counter-based hash of (seed, tick, env) rather than ``torch.rand``.
+There is no CPU path: constructing either class without the engine library or a GPU raises.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _abi
+from .body_sets import BODY_NAMES, DOF_NAMES, EVAL_BODIES, body_ids, frozen_dof_mask
+from .model import load_default_model, pd_action_offset_scale
+
+NUM_OBS = 934
+NUM_ACTIONS = 69
+
+
+# ------------------------------------------------------------------------------ config (config.py)
+@dataclass
+class RewardConfig:  # config.py:37-50
+    k_pos: float = 100.0
+    k_rot: float = 10.0
+    k_vel: float = 0.1
+    k_ang_vel: float = 0.1
+    w_pos: float = 0.5
+    w_rot: float = 0.3
+    w_vel: float = 0.1
+    w_ang_vel: float = 0.1
+    imitation_reward_dim: int = 4
+    full_body_reward: bool = True
+    use_power_reward: bool = True
+
+
+@dataclass
+class RobotConfig:  # config.py:53-86 (the fields the hot path reads)
+    humanoid_type: str = "smpl"
+    has_self_collision: bool = True
+    has_mesh: bool = False
+    reduce_action: bool = False
+    freeze_hand: bool = True
+    freeze_toe: bool = True
+    bias_offset: bool = False
+
+
+@dataclass
+class EnvConfig:  # config.py:89-157
+    device_type: str = "cuda"
+    device_id: int = 0
+    motion_file: object = "data/motion/amass_train_take6_upright.pkl"  # path, directory or clip dict
+    num_envs: int = 4096
+    headless: bool = True
+    clip_actions: bool = True
+    use_amp_obs: bool = False
+    enable_early_termination: bool = True
+    termination_distance: float = 0.25
+    max_episode_length: int = 300
+    auto_pmcp: bool = False
+    auto_pmcp_soft: bool = True
+    kp_scale: float = 1.0
+    kd_scale: float = 1.0
+    log_interval: int = 32
+    rew_power_coef: float = 0.0005
+    state_init: str = "Random"
+    min_motion_len: int = 5
+    max_motion_len: int = 600
+    robot: RobotConfig = field(default_factory=RobotConfig)
+    reward: RewardConfig = field(default_factory=RewardConfig)
+    # engine extensions (not in the reference config)
+    seed: int = 0
+    max_contacts: int = 20
+    solver_iterations: int = 8
+
+    @property
+    def device(self) -> str:
+        return "cpu" if self.device_type == "cpu" else f"cuda:{self.device_id}"
+
+    @property
+    def num_agents(self) -> int:
+        return self.num_envs
+
+
+class Box:
+    """Minimal ``gym.spaces.Box`` stand-in (gym/gymnasium are not dependencies of the engine)."""
+
+    def __init__(self, low, high, shape, dtype=np.float32):
+        self.low = np.full(shape, low, dtype)
+        self.high = np.full(shape, high, dtype)
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+
+    def sample(self, rng: Optional[np.random.Generator] = None):
+        rng = rng or np.random.default_rng()
+        lo = np.where(np.isfinite(self.low), self.low, -1.0)
+        hi = np.where(np.isfinite(self.high), self.high, 1.0)
+        return rng.uniform(lo, hi).astype(self.dtype)
+
+
+# ------------------------------------------------------------------------------ HumanoidPHC
+class HumanoidPHC:
+    """``humanoid_phc.py:HumanoidPHC`` on the engine. Buffers have the reference's names, shapes
+    and dtypes: obs_buf [N,934] f32, rew_buf [N] f32, reset_buf [N] bool, progress_buf [N] i16,
+    reward_raw [N,5] f32, extras {"terminate", "reward_raw"}."""
+
+    def __init__(self, cfg: EnvConfig, motion_data=None):
+        import torch
+        from .engine import Engine
+        from .motion_lib import MotionLibSMPL
+        if cfg.device_type != "cuda":
+            raise ValueError("the engine runs on the GPU only (device_type='cuda')")
+        if cfg.use_amp_obs:
+            raise NotImplementedError("AMP observations are out of scope (SURVEY §8f item 4)")
+        if cfg.robot.reduce_action:
+            raise NotImplementedError("reduce_action is off in the reference defaults and not supported")
+        self.cfg = cfg
+        self.device = torch.device(cfg.device)
+        n = cfg.num_envs
+        self.model = load_default_model()
+        self.num_bodies, self.num_dof = len(BODY_NAMES), 3 * len(DOF_NAMES)
+        self.num_obs, self.num_actions = NUM_OBS, NUM_ACTIONS
+        sim = _abi.default_sim_params(self_collision=int(cfg.robot.has_self_collision), kp_scale=cfg.kp_scale,
+                                      kd_scale=cfg.kd_scale, max_contacts=cfg.max_contacts,
+                                      solver_iterations=cfg.solver_iterations)
+        # start pose z=0.89 + U(-1,1) xy jitter (humanoid_phc.py:340-347)
+        rng = np.random.default_rng(cfg.seed)
+        self.engine = Engine(self.model, n, device=self.device.index or 0, sim_params=sim,
+                             start_xy=rng.uniform(-1.0, 1.0, (n, 2)).astype(np.float32))
+        off, sc = pd_action_offset_scale(self.model, bias_offset=cfg.robot.bias_offset)
+        frozen = np.zeros(self.num_dof, np.int32)
+        if cfg.robot.freeze_hand or cfg.robot.freeze_toe:
+            frozen = np.array(frozen_dof_mask(freeze_hand=cfg.robot.freeze_hand, freeze_toe=cfg.robot.freeze_toe),
+                              np.int32)
+        self.engine.set_pd_params(off, sc, frozen, clip_actions=False)  # clipping is the caller's (env.py:110)
+        self.single_observation_space = Box(-np.inf, np.inf, (NUM_OBS,))
+        self.single_action_space = Box(-1.0, 1.0, (NUM_ACTIONS,))
+        self.amp_observation_space = None
+        dev = self.device
+        self.obs_buf = torch.zeros(n, NUM_OBS, device=dev)
+        self.rew_buf = torch.zeros(n, device=dev)
+        self.reward_raw = torch.zeros(n, 5, device=dev)
+        self.progress_buf = torch.zeros(n, dtype=torch.int16, device=dev)
+        self._reset_u8 = torch.ones(n, dtype=torch.uint8, device=dev)
+        self._term_u8 = torch.ones(n, dtype=torch.uint8, device=dev)
+        self.reset_buf = self._reset_u8.view(torch.bool)
+        self._terminate_buf = self._term_u8.view(torch.bool)
+        self.extras = {}
+        self._global_offset = torch.zeros(n, 3, device=dev)
+        self._motion_start_times = torch.zeros(n, device=dev)
+        self._motion_start_times_offset = torch.zeros(n, device=dev)
+        self._sampled_motion_ids = torch.arange(n, device=dev)
+        self._motion_sample_start_idx = 0
+        self.all_env_ids = torch.arange(n, device=dev)
+        self.flag_test = False
+        self.flag_im_eval = False
+        self._gen = torch.Generator(device=dev).manual_seed(cfg.seed)
+        self._term_dist = float(cfg.termination_distance)
+        self._reset_bodies = list(range(self.num_bodies))
+        self._reset_bodies_backup = list(self._reset_bodies)
+        self._update_params()
+        self._em = self.engine.env_motion(self._sampled_motion_ids, self._motion_start_times,
+                                          self._motion_start_times_offset, self._global_offset, self.progress_buf)
+        # motion libraries (humanoid_phc.py:620-663)
+        data = cfg.motion_file if motion_data is None else motion_data
+        self._motion_train_lib = MotionLibSMPL(data, self.model, device=dev, min_length=cfg.min_motion_len,
+                                               seed=cfg.seed)
+        self._motion_eval_lib = MotionLibSMPL(data, self.model, device=dev, min_length=cfg.min_motion_len,
+                                              im_eval=True, seed=cfg.seed)
+        self._motion_lib = self._motion_train_lib
+        interval = self.num_unique_motions / (n + 50)  # even sampling on the first load (:645-648)
+        idx = np.floor(np.arange(0, self.num_unique_motions, interval)).astype(int)[:n]
+        self._load(sample_idxes=torch.from_numpy(idx))
+
+    # -- parameters ----------------------------------------------------------------------
+    def _update_params(self):
+        r = dataclasses.asdict(self.cfg.reward)
+        self._params = _abi.imitation_params(reward=r, use_power_reward=self.cfg.reward.use_power_reward,
+                                             power_coef=self.cfg.rew_power_coef,
+                                             enable_early_termination=self.cfg.enable_early_termination,
+                                             eval_mode=self.flag_im_eval, termination_distance=self._term_dist,
+                                             reset_body_ids=self._reset_bodies)
+
+    def set_termination_distances(self, termination_distances):  # :1338-1339
+        self._term_dist = termination_distances
+        self._update_params()
+
+    def _load(self, **kw):
+        n = self.cfg.num_envs
+        tables = self._motion_lib.load_motions(n, **kw)
+        self.engine.load_motions(tables)
+
+    # -- reset / step (:90-172) ----------------------------------------------------------
+    def _reset_envs(self, env_ids):
+        import torch
+        if len(env_ids) == 0:
+            return
+        phases = torch.rand(len(env_ids), device=self.device, generator=self._gen)
+        self.engine.reset_envs(self._params, self._em, env_ids.to(torch.int32), phases, self.obs_buf,
+                               self._reset_u8, self._term_u8)
+
+    def reset(self, env_ids=None):
+        safe_reset = env_ids is None or len(env_ids) == self.cfg.num_envs
+        if env_ids is None:
+            env_ids = self.all_env_ids
+        self._reset_envs(env_ids)
+        if safe_reset:  # one substep, then reset again (:97-101)
+            self.engine.simulate(1)
+            self._reset_envs(env_ids)
+        return self.obs_buf
+
+    def step(self, actions):
+        self.engine.step_actions(actions, 2)
+        self.engine.imitation_step(self._params, self._em, self.obs_buf, self.rew_buf, self.reward_raw,
+                                   self._reset_u8, self._term_u8)
+        self.extras["terminate"] = self._terminate_buf.clone()
+        self.extras["reward_raw"] = self.reward_raw.detach()
+        return self.obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    # -- motion sampling (:1363-1455) ------------------------------------------------------
+    def resample_motions(self):
+        if self.flag_test:
+            self.forward_motion_samples()
+            return
+        t = self.progress_buf.float() * (1.0 / 30.0) + self._motion_start_times + self._motion_start_times_offset
+        self._load(random_sample=True)
+        ms = self.engine.motion_state(self._sampled_motion_ids, t, want_dof=False)
+        self._global_offset[:, :2] = self.engine.root_states[:, :2] - ms["rg_pos"][:, 0, :2]
+        self.reset()
+
+    def begin_seq_motion_samples(self):
+        self._motion_sample_start_idx = 0
+        self._load(random_sample=False, start_idx=0)
+        self.reset()
+
+    def forward_motion_samples(self):
+        self._motion_sample_start_idx += self.cfg.num_envs
+        self._load(random_sample=False, start_idx=self._motion_sample_start_idx)
+        self.reset()
+
+    def toggle_eval_mode(self):
+        self.flag_test = True
+        self.flag_im_eval = True
+        self._term_dist = 0.5
+        self._motion_lib = self._motion_eval_lib
+        if len(self._reset_bodies) > 15:
+            self._reset_bodies = list(body_ids(EVAL_BODIES))
+        self._update_params()
+        self.begin_seq_motion_samples()
+        return self._motion_lib._num_unique_motions
+
+    def untoggle_eval_mode(self, failed_keys):
+        self.flag_test = False
+        self.flag_im_eval = False
+        self._term_dist = float(self.cfg.termination_distance)
+        self._motion_lib = self._motion_train_lib
+        self._reset_bodies = list(self._reset_bodies_backup)
+        self._update_params()
+        if self.cfg.auto_pmcp:
+            self._motion_lib.update_hard_sampling_weight(failed_keys)
+        elif self.cfg.auto_pmcp_soft:
+            self._motion_lib.update_soft_sampling_weight(failed_keys)
+        return self._motion_lib._termination_history.clone()
+
+    @property
+    def num_unique_motions(self):
+        return self._motion_lib._num_unique_motions
+
+    @property
+    def current_motion_ids(self):
+        return self._motion_lib._curr_motion_ids
+
+    @property
+    def motion_sample_start_idx(self):
+        return self._motion_sample_start_idx
+
+    @property
+    def motion_data_keys(self):
+        return self._motion_lib._motion_data_keys
+
+    def get_motion_steps(self):
+        return self._motion_lib.get_motion_num_steps()
+
+    # -- state views (humanoid_phc.py:497-554) ----------------------------------------------
+    @property
+    def _humanoid_root_states(self):
+        return self.engine.root_states
+
+    @property
+    def _dof_pos(self):
+        return self.engine.dof_state.view(self.cfg.num_envs, self.num_dof, 2)[..., 0]
+
+    @property
+    def _dof_vel(self):
+        return self.engine.dof_state.view(self.cfg.num_envs, self.num_dof, 2)[..., 1]
+
+    @property
+    def _rigid_body_pos(self):
+        return self.engine.rb_state.view(self.cfg.num_envs, self.num_bodies, 13)[..., :3]
+
+    @property
+    def _contact_forces(self):
+        return self.engine.contact_forces.view(self.cfg.num_envs, self.num_bodies, 3)
+
+    def render(self):
+        return None
+
+    def close(self):
+        self.engine = None
+
+
+# ------------------------------------------------------------------------------ PHCPufferEnv
+class PHCPufferEnv:
+    """``clean_pufferl/env.py:PHCPufferEnv`` over :class:`HumanoidPHC`, host-sync-free per step."""
+
+    def __init__(self, cfg: EnvConfig, motion_data=None):
+        import torch
+        self.render_mode = "native"
+        self.cfg = cfg
+        self.env = HumanoidPHC(cfg, motion_data=motion_data)
+        self.single_observation_space = self.env.single_observation_space
+        self.single_action_space = self.env.single_action_space
+        self.amp_observation_space = None
+        dev = self.env.device
+        n = cfg.num_envs
+        self.observations = self.env.obs_buf
+        self.rewards = self.env.rew_buf
+        self.terminals = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.truncations = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.masks = torch.ones(n, dtype=torch.bool, device=dev)
+        self.actions = torch.zeros(n, NUM_ACTIONS, dtype=torch.float, device=dev)
+        self.episode_returns = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.episode_lengths = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.episode_count = 0
+        self.raw_rewards = torch.zeros(5, dtype=torch.float32, device=dev)
+        # device-side accumulators of the reference's per-episode info lists (env.py:80-84)
+        self._acc = torch.zeros(5, dtype=torch.float64, device=dev)  # sum_ret, sum_len, n_ep, n_trunc, n_term
+        self.tick = 0
+
+    @property
+    def num_agents(self):
+        return self.cfg.num_envs
+
+    def reset(self, seed=None):
+        self.tick = 0
+        self.env.reset()
+        self.rewards[:] = 0
+        self.terminals[:] = False
+        self.truncations[:] = False
+        self.masks[:] = True
+        self.actions[:] = 0
+        self.raw_rewards[:] = 0
+        self._acc[:] = 0
+        return self.observations, []
+
+    def step(self, actions):
+        """``actions``: numpy [N,69] (copied to the device, as env.py:112) or a device tensor."""
+        import torch
+        if isinstance(actions, np.ndarray):
+            if self.cfg.clip_actions:
+                actions = np.clip(actions, -1, 1)
+            self.actions[:] = torch.from_numpy(np.ascontiguousarray(actions, np.float32))
+        else:
+            self.actions[:] = actions.clamp(-1, 1) if self.cfg.clip_actions else actions
+        e = self.env
+        e.engine.step_actions(self.actions, 2)
+        e.engine.imitation_reset_step(e._params, e._em, e.obs_buf, e.rew_buf, e.reward_raw, e._reset_u8, e._term_u8,
+                                      seed=self.cfg.seed, step_index=self.tick)
+        e.extras["terminate"] = e._terminate_buf.clone()
+        e.extras["reward_raw"] = e.reward_raw.detach()
+        rew = self.rewards.clone()
+        self.raw_rewards += e.reward_raw.mean(dim=0)
+        reset = e.reset_buf
+        term = e._terminate_buf & reset
+        trunc = reset & ~term
+        self.terminals.copy_(term)
+        self.truncations.copy_(trunc)
+        torch.logical_not(trunc, out=self.masks)
+        r = reset.to(torch.float64)
+        self._acc[0] += (self.episode_returns.double() * r).sum()
+        self._acc[1] += (self.episode_lengths.double() * r).sum()
+        self._acc[2] += r.sum()
+        self._acc[3] += trunc.double().sum()
+        self._acc[4] += term.double().sum()
+        keep = ~reset
+        self.episode_returns.mul_(keep).add_(self.rewards * keep)
+        self.episode_lengths.mul_(keep).add_(keep.to(torch.int32))
+        info = []
+        self.tick += 1
+        if self.tick % self.cfg.log_interval == 0:
+            info = self.mean_and_log()
+            li = self.cfg.log_interval
+            rr = (self.raw_rewards / li).tolist()
+            reward_info = {"rew_body_pos": rr[0], "rew_body_rot": rr[1], "rew_lin_vel": rr[2], "rew_ang_vel": rr[3],
+                           "rew_power": rr[4]}
+            self.raw_rewards[:] = 0
+            if len(info) > 0:
+                info[0].update(reward_info)
+            else:
+                info.append(reward_info)
+        return self.observations, rew, self.terminals, self.truncations, info
+
+    def mean_and_log(self):
+        s = self._acc.tolist()
+        self._acc[:] = 0
+        self.episode_count += int(s[2])
+        n_ep = s[2]
+        nan = float("nan")
+        return [{"episode_return": s[0] / n_ep if n_ep else nan, "episode_length": s[1] / n_ep if n_ep else nan,
+                 "truncated_rate": s[3] / (s[3] + s[4]) if (s[3] + s[4]) else nan}]
+
+    def render(self):
+        return self.env.render()
+
+    def close(self):
+        self.env.close()

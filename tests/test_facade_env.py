@@ -1,0 +1,202 @@
+"""The reference-facing host layer: the ``isaacgym`` facade
+(``humanoid_amd.isaacgym``) and the ``HumanoidPHC`` / ``PHCPufferEnv`` mirrors.
+
+CPU tests check the API surface and its error behaviour; GPU tests drive the facade the way
+``humanoid_phc.py`` does and check it against direct engine calls, and pin the PHCPufferEnv
+bookkeeping (terminals / truncations / masks / episode info, ``clean_pufferl/env.py:124-183``)
+against a line-by-line host restatement fed with the same per-step engine outputs."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import cases
+
+
+# ----------------------------------------------------------------------------------- CPU
+def test_gymapi_surface_and_errors():
+    from humanoid_amd.isaacgym import gymapi, gymtorch
+    from humanoid_amd.model import DEFAULT_MODEL_JSON
+    gym = gymapi.acquire_gym()
+    assert gym is gymapi.acquire_gym()
+    sp = gymapi.SimParams()
+    assert sp.physx.num_position_iterations == 4 and sp.gravity.z == -9.81  # isaacgym_env.py:18-33
+    with pytest.raises(NotImplementedError):
+        gym.create_sim(-1, -1, gymapi.SIM_PHYSX, sp)  # no CPU pipeline
+    with pytest.raises(NotImplementedError):
+        gym.create_sim(0, 0, gymapi.SIM_PHYSX, sp)  # no viewer
+    sim = gym.create_sim(0, -1, gymapi.SIM_PHYSX, sp)
+    opts = gymapi.AssetOptions()
+    opts.angular_damping, opts.max_angular_velocity = 0.01, 100.0
+    asset = gym.load_asset(sim, "/", DEFAULT_MODEL_JSON, opts)
+    assert gym.get_asset_rigid_body_count(asset) == 24 and gym.get_asset_dof_count(asset) == 69
+    assert gym.find_asset_rigid_body_index(asset, "L_Knee") == 2
+    props = gym.get_asset_dof_properties(asset)
+    assert props.dtype == gymapi.DofPropertiesDtype and props.shape == (69,)
+    props["stiffness"] *= 2.0  # numpy structured array semantics, as humanoid_phc.py:276-280
+    with pytest.raises(RuntimeError):
+        gym.prepare_sim(sim)  # no actors yet
+    with pytest.raises(ValueError):
+        gymtorch.unwrap_tensor(torch.zeros(4, 4).t())  # wrapper.py:52 contiguous check
+
+
+# ----------------------------------------------------------------------------------- GPU
+def _facade_sim(n, self_collision=True):
+    from humanoid_amd.isaacgym import gymapi
+    from humanoid_amd.model import DEFAULT_MODEL_JSON
+    gym = gymapi.acquire_gym()
+    sp = gymapi.SimParams()
+    sim = gym.create_sim(0, -1, gymapi.SIM_PHYSX, sp)
+    opts = gymapi.AssetOptions()
+    opts.angular_damping, opts.max_angular_velocity = 0.01, 100.0
+    opts.default_dof_drive_mode = gymapi.DOF_MODE_NONE
+    asset = gym.load_asset(sim, "/", DEFAULT_MODEL_JSON, opts)
+    plane = gymapi.PlaneParams()
+    gym.add_ground(sim, plane)
+    dof_prop = gym.get_asset_dof_properties(asset)
+    dof_prop["driveMode"] = gymapi.DOF_MODE_POS
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-5, -5, 0), gymapi.Vec3(5, 5, 5), 4)
+        gym.begin_aggregate(env, 160, 160, True)
+        pose = gymapi.Transform(gymapi.Vec3(0.1 * i, 0.0, 0.89), gymapi.Quat(0, 0, 0, 1))
+        h = gym.create_actor(env, asset, pose, f"humanoid_{i}", i, 0 if self_collision else 1, 0)
+        gym.enable_actor_dof_force_sensors(env, h)
+        assert abs(sum(p.mass for p in gym.get_actor_rigid_body_properties(env, h)) - 74.0) < 0.1
+        gym.set_actor_dof_properties(env, h, dof_prop)
+        sprops = gym.get_actor_rigid_shape_properties(env, h)
+        gym.set_actor_rigid_shape_properties(env, h, sprops)
+        gym.end_aggregate(env)
+    gym.prepare_sim(sim)
+    return gym, sim
+
+
+@pytest.mark.gpu
+def test_facade_matches_direct_engine(he_model):
+    from humanoid_amd import _abi
+    from humanoid_amd.engine import Engine
+    from humanoid_amd.isaacgym import gymtorch
+    n = 16
+    gym, sim = _facade_sim(n)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim))
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    assert root.shape == (n, 13) and dof.shape == (n * 69, 2) and rb.shape == (n * 24, 13)
+    rng = np.random.default_rng(5)
+    r0, d0 = cases.random_state(n, rng, height=(0.9, 1.1))
+    src_r = torch.from_numpy(r0).cuda()
+    src_d = torch.from_numpy(d0.reshape(n * 69, 2)).cuda()
+    ids = torch.arange(n, dtype=torch.int32, device="cuda")
+    gym.set_actor_root_state_tensor_indexed(sim, gymtorch.unwrap_tensor(src_r), gymtorch.unwrap_tensor(ids), n)
+    gym.set_dof_state_tensor_indexed(sim, gymtorch.unwrap_tensor(src_d), gymtorch.unwrap_tensor(ids), n)
+    tgt = torch.from_numpy(rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)).cuda()
+    gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(tgt))
+    gym.simulate(sim)
+    gym.simulate(sim)
+    gym.fetch_results(sim, True)
+    gym.refresh_actor_root_state_tensor(sim)
+    gym.refresh_dof_state_tensor(sim)
+    eng = Engine(he_model, n, device=0, sim_params=_abi.default_sim_params())
+    eng.root_states.copy_(src_r)
+    eng.dof_state.copy_(src_d)
+    eng.dof_targets.copy_(tgt)
+    eng.simulate(2)
+    torch.cuda.synchronize()
+    assert torch.equal(root, eng.root_states) and torch.equal(dof, eng.dof_state)
+    # the views alias engine memory: a write through the view is seen by the engine
+    root[0, 2] = 5.0
+    assert float(sim.engine.root_states[0, 2]) == 5.0
+
+
+def _clip_dict(model, k=4, frames=90):
+    from humanoid_amd import synthetic
+    return {f"clip{i}": synthetic.make_clip(model, np.random.default_rng(100 + i), num_frames=frames)
+            for i in range(k)}
+
+
+def _reference_bookkeeping(seq, n, log_interval):
+    """clean_pufferl/env.py:124-183 restated on host lists (the reference's own code path)."""
+    ep_ret = np.zeros(n, np.float32)
+    ep_len = np.zeros(n, np.int32)
+    infos = {"episode_return": [], "episode_length": [], "truncated_rate": []}
+    raw_sum = np.zeros(5, np.float64)
+    out = []
+    for tick, (rew, reset, term, raw) in enumerate(seq, 1):
+        raw_sum += raw.mean(0)
+        terminals = np.zeros(n, bool)
+        truncs = np.zeros(n, bool)
+        ridx = np.nonzero(reset)[0]
+        if len(ridx):
+            infos["episode_return"] += ep_ret[ridx].tolist()
+            infos["episode_length"] += ep_len[ridx].tolist()
+            ep_ret[ridx] = 0
+            ep_len[ridx] = 0
+            tidx = np.nonzero(term)[0]
+            terminals[tidx] = True
+            infos["truncated_rate"] += [0.0] * len(tidx)
+            tr = ridx[~np.isin(ridx, tidx)]
+            truncs[tr] = True
+            infos["truncated_rate"] += [1.0] * len(tr)
+        ep_ret[~reset] += rew[~reset]
+        ep_len[~reset] += 1
+        info = []
+        if tick % log_interval == 0:
+            info = [{k: float(np.mean(v)) if v else float("nan") for k, v in infos.items()}]
+            for v in infos.values():
+                v.clear()
+            info[0].update({"rew_body_pos": raw_sum[0] / log_interval, "rew_power": raw_sum[4] / log_interval})
+            raw_sum[:] = 0
+        out.append((terminals, truncs, info))
+    return out
+
+
+@pytest.mark.gpu
+def test_puffer_env_bookkeeping_matches_reference_logic(model):
+    from humanoid_amd.env import EnvConfig, PHCPufferEnv
+    n, li = 64, 5
+    cfg = EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=3, log_interval=li)
+    pe = PHCPufferEnv(cfg)
+    obs, info = pe.reset()
+    assert obs.shape == (n, 934) and torch.isfinite(obs).all() and info == []
+    rng = np.random.default_rng(0)
+    seq, got = [], []
+    for t in range(25):
+        a = rng.uniform(-1.5, 1.5, (n, 69)).astype(np.float32)  # clip_actions clamps
+        obs, rew, terminals, truncs, info = pe.step(a)
+        e = pe.env
+        seq.append((rew.cpu().numpy(), e.reset_buf.cpu().numpy().copy(), e.extras["terminate"].cpu().numpy(),
+                    e.extras["reward_raw"].cpu().numpy()))
+        got.append((terminals.cpu().numpy().copy(), truncs.cpu().numpy().copy(), pe.masks.cpu().numpy().copy(), info))
+        assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+    ref = _reference_bookkeeping(seq, n, li)
+    n_resets = sum(int(s[1].sum()) for s in seq)
+    assert n_resets > 0, "the action stream should make some envs fall"
+    for (tg, trg, mg, ig), (tr, trr, ir) in zip(got, ref):
+        assert (tg == tr).all() and (trg == trr).all() and (mg == ~trr).all()
+        assert len(ig) == len(ir)
+        for a, b in zip(ig, ir):
+            for k in ("episode_return", "episode_length", "truncated_rate", "rew_body_pos", "rew_power"):
+                assert (np.isnan(a[k]) and np.isnan(b[k])) or abs(a[k] - b[k]) <= 1e-4 * max(1.0, abs(b[k])), (k, a, b)
+
+
+@pytest.mark.gpu
+def test_humanoid_phc_reset_and_step(model):
+    from humanoid_amd.env import EnvConfig, HumanoidPHC
+    n = 32
+    env = HumanoidPHC(EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=1))
+    obs = env.reset()
+    assert obs.shape == (n, 934) and torch.isfinite(obs).all()
+    # after the reference-state init the simulated bodies sit on the reference motion
+    assert int(env.progress_buf.abs().sum()) == 0
+    obs, rew, reset, extras = env.step(torch.zeros(n, 69, device=env.device))
+    assert rew.shape == (n,) and reset.dtype == torch.bool and set(extras) >= {"terminate", "reward_raw"}
+    assert (env.progress_buf == 1).all() and torch.isfinite(rew).all()
+    assert bool(((rew >= 0) & (rew <= 1)).all())  # 4 weighted exp terms, power is 0 while progress <= 3
+    ids = torch.arange(0, n, 2, device=env.device)
+    env.reset(ids)
+    assert (env.progress_buf[ids] == 0).all() and (env.progress_buf[1::2] == 1).all()
+    n_unique = env.toggle_eval_mode()
+    assert n_unique == 4 and env.flag_im_eval
+    hist = env.untoggle_eval_mode(["clip1"])
+    assert hist.shape == (4,) and float(hist[1]) == 1.0
+    env.resample_motions()
+    assert torch.isfinite(env.obs_buf).all()
