@@ -220,7 +220,7 @@ def main():
     if rank == 0:
         phys_tflops = PHYS_FLOP_PER_ENV_STEP * n / (phys_ms * 1e-3) / 1e12
         imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = imit_traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
             try:
@@ -228,8 +228,9 @@ def main():
                 key = f"{args.config}:{n}"
                 if key in tr:
                     traffic = tr[key].get("physics_bytes_per_launch")
+                    imit_traffic = tr[key].get("imitation_bytes_per_launch")
             except Exception:
-                traffic = None
+                traffic = imit_traffic = None
         line = {
             "metric": "env-steps/sec (4096 SMPL humanoids per GPU)",
             "value": round(value, 1),
@@ -253,7 +254,8 @@ def main():
                          "kernel": "physics_kernel (fp32 vector; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
                          "avg_launch_ms": round(phys_ms, 4)},
             "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(imit_gbs / HBM_PEAK_GBS, 5), "avg_launch_ms": round(imit_ms, 4)},
+                                 "frac": round(imit_gbs / HBM_PEAK_GBS, 5), "avg_launch_ms": round(imit_ms, 4),
+                                 "traffic": imit_traffic},
         }
         if not args.no_cpu_baseline and world == 1:
             try:
