@@ -250,7 +250,7 @@ HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uin
 // one Gauss-Seidel sweep over the contacts: normal row clamped at 0, friction rows to the pyramid
 // |lambda_t| <= mu lambda_n; lane r holds w_r, lambda_r, A[r][r]; lane c holds column A[.][c]
 template <int CI>
-HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float diag, int nc, const float* cmu,
+HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float invd, int nc, const float* cmu,
                       int lane) {
     if constexpr (CI < MAXC) {
         if (CI >= nc) return;
@@ -260,8 +260,8 @@ HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float di
         for (int kind = 0; kind < 3; ++kind) {
             constexpr int R0 = 3 * CI;
             const int r = R0 + kind;
-            const float wr = regla::rdlane(w, r), lr = regla::rdlane(lamv, r), arr = regla::rdlane(diag, r);
-            float nl = lr - wr / arr;
+            const float wr = regla::rdlane(w, r), lr = regla::rdlane(lamv, r), ir = regla::rdlane(invd, r);
+            float nl = lr - wr * ir;
             if (kind == 0) {
                 nl = fmaxf(nl, 0.f);
                 lamn = nl;
@@ -272,7 +272,33 @@ HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float di
             w = fmaf(acol[R0 + kind], nl - lr, w);
             lamv = lane == r ? nl : lamv;
         }
-        pgs_sweep<CI + 1>(w, lamv, acol, diag, nc, cmu, lane);
+        pgs_sweep<CI + 1>(w, lamv, acol, invd, nc, cmu, lane);
+    }
+}
+
+// CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i for j in chain(i)
+// (compile-time lane masks), plus armature and the implicit-drive terms on the diagonal
+template <int I>
+HE_DEV void crba_rows(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], const Lds& L, const he_model& m,
+                      float dt, int lane) {
+    using namespace regla;
+    if constexpr (I < NG) {
+        const Lds& Lg = *opaque(&L);  // row I's reads stay here (no hoisting of all 75 rows)
+        float IS[6];
+        for (int x = 0; x < 6; ++x) IS[x] = Lg.IS[I][x];
+        float h = lanes<smpl::kAncLo[I]>() ? dot6(Sj, IS) : 0.f;
+        if constexpr (I >= 6 && I < 64) {
+            if (lane == I) h += m.armature[I - 6] + dt * L.coef[I];
+        }
+        asm volatile("" : "+v"(h));  // computed here, not sunk next to the factorisation
+        M.c[I] = h;
+        if constexpr (I >= 64) {
+            float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? dot6(Sj2, IS) : 0.f;
+            if (lane == I - 64) h2 += m.armature[I - 6] + dt * L.coef[I];
+            asm volatile("" : "+v"(h2));
+            M.c2[I - 64] = h2;
+        }
+        crba_rows<I + 1>(M, Sj, Sj2, L, m, dt, lane);
     }
 }
 
@@ -293,10 +319,7 @@ HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
         r1[4 * q] = v1.x; r1[4 * q + 1] = v1.y; r1[4 * q + 2] = v1.z; r1[4 * q + 3] = v1.w;
         r2[4 * q] = v2.x; r2[4 * q + 1] = v2.y; r2[4 * q + 2] = v2.z; r2[4 * q + 3] = v2.w;
     }
-    const uint64_t a1lo = smpl::kAncLo[lane];
-    const uint64_t a2lo = lane < NH ? smpl::kAncLo[64 + lane] : 0ull;
-    const uint32_t a2hi = lane < NH ? smpl::kAncHi[64 + lane] : 0u;
-    solve_L_rows<0>(r1, r2, a1lo, a2lo, a2hi, yl, y2, lane);
+    solve_L_rows<0>(r1, r2, yl, y2);
 }
 
 // ---------------------------------------------------------------------------------- kinematics
@@ -470,21 +493,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     {
         float Sj[6], Sj2[6];
         for (int x = 0; x < 6; ++x) { Sj[x] = L.S[lane][x]; Sj2[x] = lane < NH ? L.S[64 + lane][x] : 0.f; }
-#pragma unroll
-        for (int i = 0; i < NG; ++i) {
-            float IS[6];
-            for (int x = 0; x < 6; ++x) IS[x] = L.IS[i][x];
-            const bool in = (smpl::kAncLo[i] >> lane) & 1ull;
-            float h = in ? dot6(Sj, IS) : 0.f;
-            if (i >= 6 && lane == i) h += m.armature[i >= 6 ? i - 6 : 0] + dt * L.coef[i];
-            M.c[i] = h;
-            if (i >= 64) {
-                const bool in2 = lane < NH && ((smpl::kAncHi[i] >> lane) & 1u);
-                float h2 = in2 ? dot6(Sj2, IS) : 0.f;
-                if (lane == i - 64) h2 += m.armature[i - 6] + dt * L.coef[i];
-                M.c2[i >= 64 ? i - 64 : 0] = h2;
-            }
-        }
+        crba_rows<0>(M, Sj, Sj2, L, m, dt, lane);
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
@@ -662,8 +671,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
         {
             float w = lane < nr ? brow : 0.f;
-            diag = lane < nr ? diag + 1e-12f : 1.f;
-            for (int it = 0; it < p.solver_iterations; ++it) pgs_sweep<0>(w, lamv, acol, diag, nc, L.cmu, lane);
+            const float invd = 1.0f / (lane < nr ? diag + 1e-12f : 1.f);
+            for (int it = 0; it < p.solver_iterations; ++it) pgs_sweep<0>(w, lamv, acol, invd, nc, L.cmu, lane);
         }
         L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();

@@ -43,6 +43,13 @@ __device__ __forceinline__ float get(const RegMat& M) {
     else return rdlane(M.c2[ROW - 64], COL - 64);
 }
 
+// lanes whose bit is set in the compile-time mask C (v_cndmask on an SGPR-pair constant; no
+// per-lane compare or branch)
+template <uint64_t C>
+__device__ __forceinline__ bool lanes() {
+    return __builtin_amdgcn_inverse_ballot_w64(C);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
@@ -97,9 +104,11 @@ template <int K>
 __device__ __forceinline__ void solve_LT(const RegMat& M, float& yl, float& y2, int lane) {
     if constexpr (K >= 1) {
         const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-        if (lane < K) yl -= M.c[K] * yk;
+        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+        yl = lanes<lo>() ? yl - M.c[K] * yk : yl;
         if constexpr (K > 64) {
-            if (lane < K - 64) y2 -= M.c2[K - 64] * yk;
+            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+            y2 = lanes<hi>() ? y2 - M.c2[K - 64] * yk : y2;
         }
         solve_LT<K - 1>(M, yl, y2, lane);
     }
@@ -128,9 +137,11 @@ template <int K>
 __device__ __forceinline__ void store_packed(const RegMat& M, float* Lp, int lane, int lane_depth,
                                              int lane_depth2) {
     if constexpr (K >= 1) {
-        if (lane < K && ((kAncLo[K] >> lane) & 1ull)) Lp[kPackStart[K] + lane_depth] = M.c[K];
+        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+        if (lanes<lo>()) Lp[kPackStart[K] + lane_depth] = M.c[K];
         if constexpr (K > 64) {
-            if (lane < K - 64 && ((kAncHi[K] >> lane) & 1u)) Lp[kPackStart[K] + lane_depth2] = M.c2[K - 64];
+            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+            if (lanes<hi>()) Lp[kPackStart[K] + lane_depth2] = M.c2[K - 64];
         }
         store_packed<K - 1>(M, Lp, lane, lane_depth, lane_depth2);
     }
@@ -176,19 +187,18 @@ __device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG]) {
 // v_readlane of y_K plus a masked FMA -- no cross-lane reduction.
 constexpr int kRowRegs = 32;
 template <int K>
-__device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs],
-                                             uint64_t a1lo, uint64_t a2lo, uint32_t a2hi, float& yl,
-                                             float& y2, int lane) {
+__device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs], float& yl,
+                                             float& y2) {
     if constexpr (K < NG) {
         constexpr int d = kDofNanc[K] - 1 < kRowRegs ? kDofNanc[K] - 1 : 0;
-        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-        if constexpr (K < 64) {
-            if (((a1lo >> K) & 1ull) && lane != K) yl -= r1[d] * yk;
-            if ((a2lo >> K) & 1ull) y2 -= r2[d] * yk;
-        } else {
-            if (((a2hi >> (K - 64)) & 1u) && lane != K - 64) y2 -= r2[d] * yk;
+        constexpr uint64_t lo = kDescLo[K];
+        constexpr uint64_t hi = kDescHi[K];
+        if constexpr (lo != 0 || hi != 0) {
+            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
+            if constexpr (lo != 0) yl = lanes<lo>() ? yl - r1[d] * yk : yl;
+            if constexpr (hi != 0) y2 = lanes<hi>() ? y2 - r2[d] * yk : y2;
         }
-        solve_L_rows<K + 1>(r1, r2, a1lo, a2lo, a2hi, yl, y2, lane);
+        solve_L_rows<K + 1>(r1, r2, yl, y2);
     }
 }
 
@@ -199,9 +209,11 @@ template <int K>
 __device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, float& yl, float& y2, int lane) {
     if constexpr (K >= 1) {
         const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-        if (lane < K && ((kAncLo[K] >> lane) & 1ull)) yl -= Lp[kPackStart[K] + dj] * yk;
+        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+        if (lanes<lo>()) yl -= Lp[kPackStart[K] + dj] * yk;
         if constexpr (K > 64) {
-            if (lane < K - 64 && ((kAncHi[K] >> lane) & 1u)) y2 -= Lp[kPackStart[K] + dj2] * yk;
+            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+            if (lanes<hi>()) y2 -= Lp[kPackStart[K] + dj2] * yk;
         }
         solve_LT_cols<K - 1>(Lp, dj, dj2, yl, y2, lane);
     }
