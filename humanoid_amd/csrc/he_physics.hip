@@ -229,21 +229,31 @@ HE_DEV void ffma_ordered(float& acc, float a, float b) { asm volatile("v_fmac_f3
 constexpr int NGRP = (NG + 3) / 4;
 template <int RR>
 HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uint32_t live) {
+    // four rows at a time: four independent accumulation chains, and each v_readlane has three
+    // other instructions before its SGPR is consumed (no hazard s_nop)
     if constexpr (RR < MAXR) {
         if (RR >= nr) return;
-        float acc = 0.f;
+        constexpr int NQ = MAXR - RR < 4 ? MAXR - RR : 4;
+        float acc[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
 #pragma unroll
         for (int g = 0; g < NGRP; ++g) {
             if ((live >> g) & 1u) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int i = 4 * g + k < NG ? 4 * g + k : 0;
-                    if (4 * g + k < NG) acc = fmaf(regla::rdlane(z[i], RR), z[i], acc);
+                    if (4 * g + k < NG) {
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) acc[q] = fmaf(regla::rdlane(z[i], RR + q), z[i], acc[q]);
+                    }
                 }
             }
         }
-        acol[RR] = acc;
-        delassus_rows<RR + 1>(z, acol, nr, live);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acol[RR + q] = acc[q];  // rows >= nr come out 0 (their lanes hold z = 0)
+        __builtin_amdgcn_sched_barrier(0);
+        delassus_rows<RR + NQ>(z, acol, nr, live);
     }
 }
 
