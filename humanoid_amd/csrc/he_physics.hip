@@ -35,6 +35,7 @@ constexpr int MAXC = HE_MAX_CONTACTS;
 constexpr int MAXR = 3 * MAXC;  // <= 63: one contact row per lane
 constexpr int W = 64;
 static_assert(MAXR <= W - 1, "contact rows must fit one per lane");
+static_assert(MAXC <= NB, "per-contact impulses reuse a per-body scratch array");
 static_assert(smpl::kNG == NG && smpl::kNB == NB, "generated topology mismatch");
 
 struct BodyTopo {
@@ -293,22 +294,25 @@ HE_DEV void crba_rows(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)
                       float dt, int lane) {
     using namespace regla;
     if constexpr (I < NG) {
-        const Lds& Lg = *opaque(&L);  // row I's reads stay here (no hoisting of all 75 rows)
+        // rows are pinned in groups of four (opaque base): loads of a group overlap, groups stay
+        // in order, and each result is produced here rather than sunk next to the factorisation
+        const Lds& Lg = (I % 4 == 0) ? *opaque(&L) : L;
         float IS[6];
         for (int x = 0; x < 6; ++x) IS[x] = Lg.IS[I][x];
         float h = lanes<smpl::kAncLo[I]>() ? dot6(Sj, IS) : 0.f;
         if constexpr (I >= 6 && I < 64) {
-            if (lane == I) h += m.armature[I - 6] + dt * L.coef[I];
+            if (lane == I) h += m.armature[I - 6] + dt * Lg.coef[I];
         }
-        asm volatile("" : "+v"(h));  // computed here, not sunk next to the factorisation
+        asm volatile("" : "+v"(h));
         M.c[I] = h;
         if constexpr (I >= 64) {
             float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? dot6(Sj2, IS) : 0.f;
-            if (lane == I - 64) h2 += m.armature[I - 6] + dt * L.coef[I];
+            if (lane == I - 64) h2 += m.armature[I - 6] + dt * Lg.coef[I];
             asm volatile("" : "+v"(h2));
             M.c2[I - 64] = h2;
         }
-        crba_rows<I + 1>(M, Sj, Sj2, L, m, dt, lane);
+        if constexpr (I % 4 == 3) crba_rows<I + 1>(M, Sj, Sj2, *opaque(&L), m, dt, lane);
+        else crba_rows<I + 1>(M, Sj, Sj2, Lg, m, dt, lane);
     }
 }
 
@@ -595,6 +599,17 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         nc = total < maxc ? total : maxc;
     }
     if (p.self_collision && nc < maxc) {
+        // world-space collision segments once per body (lane = body) into the Ib scratch
+        // (dead after the subtree sums), so each pair lane only gathers two of them
+        float (*seg)[10] = L.Ib;
+        if (lane < NB) {
+            f3 a, c;
+            float r;
+            body_segment(m, L, lane, a, c, r);
+            seg[lane][0] = a.x; seg[lane][1] = a.y; seg[lane][2] = a.z;
+            seg[lane][3] = c.x; seg[lane][4] = c.y; seg[lane][5] = c.z; seg[lane][6] = r;
+        }
+        sync();
         for (int base = 0; base < m.num_pairs; base += W) {
             int pi = base + lane;
             bool hit = false;
@@ -604,10 +619,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             if (pi < m.num_pairs) {
                 i = m.pairs[pi][0];
                 j = m.pairs[pi][1];
-                f3 a0, a1, b0, b1, ci, cj;
-                float ri, rj;
-                body_segment(m, L, i, a0, a1, ri);
-                body_segment(m, L, j, b0, b1, rj);
+                const float* si = seg[i];
+                const float* sj = seg[j];
+                const f3 a0 = f3{si[0], si[1], si[2]}, a1 = f3{si[3], si[4], si[5]};
+                const f3 b0 = f3{sj[0], sj[1], sj[2]}, b1 = f3{sj[3], sj[4], sj[5]};
+                const float ri = si[6], rj = sj[6];
+                f3 ci, cj;
                 seg_seg(a0, a1, b0, b1, ci, cj);
                 f3 dv = ci - cj;
                 float len = norm3(dv);
@@ -644,9 +661,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             const uint32_t anc1 = (lane < nr && L.cb1[ci] >= 0) ? T.anc_mask[L.cb1[ci]] : 0u;
             const f3 dd = f3{dir[0], dir[1], dir[2]};
             const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o, dd);
+            const Lds* Lgp = &L;
 #pragma unroll
             for (int i = 0; i < NG; ++i) {
-                const Lds& Lg = *opaque(&L);  // the LDS reads of dof i stay at this point
+                if (i % 4 == 0) Lgp = opaque(&L);  // LDS reads pinned per group of four dofs
+                const Lds& Lg = *Lgp;
                 const int bi = smpl::kDofBody[i];
                 const float sgn = (float)((anc0 >> bi) & 1u) - (float)((anc1 >> bi) & 1u);
                 const float* S = Lg.S[i];
@@ -687,29 +706,40 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();
         STAMP(10);
-        // ---- contact impulses -> body spatial impulses (about o) and reported contact forces
+        // ---- contact impulses -> body spatial impulses (about o) and reported contact forces:
+        // lane c forms contact c's spatial impulse, lane b gathers the ones acting on body b
+        float (*imp)[6] = L.Acc;  // per-contact scratch (Acc is dead in the contact phase)
+        if (lane < nc) {
+            const int c = lane;
+            const float ln = L.lam[3 * c], la = L.lam[3 * c + 1], lb = L.lam[3 * c + 2];
+            const f3 f = f3{ln * L.cn[c][0] + la * L.ct1[c][0] + lb * L.ct2[c][0],
+                            ln * L.cn[c][1] + la * L.ct1[c][1] + lb * L.ct2[c][1],
+                            ln * L.cn[c][2] + la * L.ct1[c][2] + lb * L.ct2[c][2]};
+            const f3 n = cross3(f3{L.cx[c][0], L.cx[c][1], L.cx[c][2]} - o, f);
+            imp[c][0] = n.x; imp[c][1] = n.y; imp[c][2] = n.z; imp[c][3] = f.x; imp[c][4] = f.y; imp[c][5] = f.z;
+        }
+        sync();
         if (lane < NB) {
             float F6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            for (int c = 0; c < nc; ++c) {
-                const float s = L.cb0[c] == lane ? 1.f : (L.cb1[c] == lane ? -1.f : 0.f);
-                if (s == 0.f) continue;
-                const float ln = L.lam[3 * c], la = L.lam[3 * c + 1], lb = L.lam[3 * c + 2];
-                const f3 f = f3{ln * L.cn[c][0] + la * L.ct1[c][0] + lb * L.ct2[c][0],
-                                ln * L.cn[c][1] + la * L.ct1[c][1] + lb * L.ct2[c][1],
-                                ln * L.cn[c][2] + la * L.ct1[c][2] + lb * L.ct2[c][2]} * s;
-                const f3 n = cross3(f3{L.cx[c][0], L.cx[c][1], L.cx[c][2]} - o, f);
-                F6[0] += n.x; F6[1] += n.y; F6[2] += n.z; F6[3] += f.x; F6[4] += f.y; F6[5] += f.z;
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) {
+                if (c < nc) {
+                    const float s = (L.cb0[c] == lane ? 1.f : 0.f) - (L.cb1[c] == lane ? 1.f : 0.f);
+                    for (int x = 0; x < 6; ++x) F6[x] += s * imp[c][x];
+                }
             }
-            for (int x = 0; x < 6; ++x) L.Acc[lane][x] = F6[x];
+            for (int x = 0; x < 6; ++x) L.V[lane][x] = F6[x];
             L.cf[lane][0] = F6[3] / dt; L.cf[lane][1] = F6[4] / dt; L.cf[lane][2] = F6[5] / dt;
         }
         sync();
         if (lane < NB) {
             const uint32_t sm = T.sub_mask[lane];
             float Fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            for (int d = 0; d < NB; ++d)
-                if (sm >> d & 1u)
-                    for (int x = 0; x < 6; ++x) Fs[x] += L.Acc[d][x];
+#pragma unroll
+            for (int d = 0; d < NB; ++d) {
+                const float s = (sm >> d) & 1u ? 1.f : 0.f;
+                for (int x = 0; x < 6; ++x) Fs[x] += s * L.V[d][x];
+            }
             for (int x = 0; x < 6; ++x) L.F[lane][x] = Fs[x];
         }
         sync();

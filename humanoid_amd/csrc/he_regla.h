@@ -86,7 +86,7 @@ __device__ __forceinline__ void factor(RegMat& M, float& Dl, float& D2, int lane
     if constexpr (K >= 0) {
         constexpr int D = kDofNanc[K] - 1;
         const float dk = get<K, K>(M);
-        const float inv = uniform(1.0f / dk);
+        const float inv = uniform(__builtin_amdgcn_rcpf(dk));  // v_rcp_f32 (1 ulp): short pivot chain
         float hk[kMaxChain];
         read_row<K, 0, D>(M, hk);
         M.c[K] *= inv;  // row K -> L[K][.] on lanes j < K
