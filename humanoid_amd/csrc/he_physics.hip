@@ -259,30 +259,31 @@ HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uin
 }
 
 // one Gauss-Seidel sweep over the contacts: normal row clamped at 0, friction rows to the pyramid
-// |lambda_t| <= mu lambda_n; lane r holds w_r, lambda_r, A[r][r]; lane c holds column A[.][c]
+// |lambda_t| <= mu lambda_n. Lane r holds w_r, lambda_r and 1/A[r][r], so each row's candidate
+// impulse is computed lane-parallel from VGPRs (only lane r's result is used); one v_readlane
+// carries the impulse change to the column update w += A[.][r] * d of every lane.
+template <int R>
+HE_DEV void pgs_friction(float& w, float& lamv, const float (&acol)[MAXR], float invd, float bnd) {
+    const float nt = fminf(fmaxf(lamv - w * invd, -bnd), bnd);
+    const float d = regla::rdlane(nt - lamv, R);
+    lamv = regla::lanes<1ull << R>() ? nt : lamv;
+    w = fmaf(acol[R], d, w);
+}
+
 template <int CI>
 HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float invd, int nc, const float* cmu,
                       int lane) {
+    using regla::lanes;
     if constexpr (CI < MAXC) {
         if (CI >= nc) return;
-        const float mu_c = cmu[CI];
-        float lamn = 0.f;
-#pragma unroll
-        for (int kind = 0; kind < 3; ++kind) {
-            constexpr int R0 = 3 * CI;
-            const int r = R0 + kind;
-            const float wr = regla::rdlane(w, r), lr = regla::rdlane(lamv, r), ir = regla::rdlane(invd, r);
-            float nl = lr - wr * ir;
-            if (kind == 0) {
-                nl = fmaxf(nl, 0.f);
-                lamn = nl;
-            } else {
-                const float bnd = mu_c * lamn;
-                nl = fminf(fmaxf(nl, -bnd), bnd);
-            }
-            w = fmaf(acol[R0 + kind], nl - lr, w);
-            lamv = lane == r ? nl : lamv;
-        }
+        constexpr int R0 = 3 * CI;
+        float nl = fmaxf(lamv - w * invd, 0.f);
+        const float dn = regla::rdlane(nl - lamv, R0);
+        const float bnd = cmu[CI] * regla::rdlane(nl, R0);
+        lamv = lanes<1ull << R0>() ? nl : lamv;
+        w = fmaf(acol[R0], dn, w);
+        pgs_friction<R0 + 1>(w, lamv, acol, invd, bnd);
+        pgs_friction<R0 + 2>(w, lamv, acol, invd, bnd);
         pgs_sweep<CI + 1>(w, lamv, acol, invd, nc, cmu, lane);
     }
 }
@@ -400,8 +401,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     using namespace regla;
     // opaque per substep: keeps the compiler from hoisting ~1k uniform model loads out of the
     // substep loop into SGPRs (which then spill into VGPR lanes)
-    asm volatile("" : "+s"(mp));
-    const he_model& m = *mp;
+    // (an opaque byte offset rather than an opaque pointer: the pointer keeps its global address
+    // space, so the loads stay global_load / s_load instead of flat_load)
+    int mo = 0;
+    asm volatile("" : "+s"(mo));
+    const he_model& m = *reinterpret_cast<const he_model*>(reinterpret_cast<const char*>(mp) + mo);
     // likewise an opaque VGPR base for LDS: addresses become base + immediate offset instead of
     // hundreds of hoisted uniform address constants
     int lds_off = 0;
