@@ -665,37 +665,61 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             const uint32_t anc1 = (lane < nr && L.cb1[ci] >= 0) ? T.anc_mask[L.cb1[ci]] : 0u;
             const f3 dd = f3{dir[0], dir[1], dir[2]};
             const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o, dd);
+            // z = J_r^T and brow = J_r uf, four dofs per pinned group (their LDS reads overlap; the
+            // results are fixed in place so the loads cannot all be hoisted ahead of the math)
+            float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+            {
+                // root: S = unit axes, so z = sgn0 * (rho, dd)
+                const float s0 = (float)(anc0 & 1u) - (float)(anc1 & 1u);
+                z[0] = s0 * rho.x; z[1] = s0 * rho.y; z[2] = s0 * rho.z;
+                z[3] = s0 * dd.x; z[4] = s0 * dd.y; z[5] = s0 * dd.z;
+            }
+            for (int i = 0; i < 6; ++i) bacc[i & 3] = fmaf(z[i], L.uf[i], bacc[i & 3]);
+            const f3 cx = f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]};
             const Lds* Lgp = &L;
 #pragma unroll
-            for (int i = 0; i < NG; ++i) {
-                if (i % 4 == 0) Lgp = opaque(&L);  // LDS reads pinned per group of four dofs
+            for (int b = 1; b < NB; ++b) {
+                // joint b: S_i = [a_i; (p_b - o) x a_i], so S_i . (rho, dd) = a_i . ((x - p_b) x dd);
+                // LDS reads pinned per group of four bodies
+                if (b % 4 == 1) Lgp = opaque(&L);
                 const Lds& Lg = *Lgp;
-                const int bi = smpl::kDofBody[i];
-                const float sgn = (float)((anc0 >> bi) & 1u) - (float)((anc1 >> bi) & 1u);
-                const float* S = Lg.S[i];
-                z[i] = sgn * (S[0] * rho.x + S[1] * rho.y + S[2] * rho.z + S[3] * dd.x + S[4] * dd.y + S[5] * dd.z);
-                ffma_ordered(brow, z[i], Lg.uf[i]);
+                const float sgn = (float)((anc0 >> b) & 1u) - (float)((anc1 >> b) & 1u);
+                const f3 v = cross3(cx - f3{Lg.pw[b][0], Lg.pw[b][1], Lg.pw[b][2]}, dd) * sgn;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int i = 6 + 3 * (b - 1) + c;
+                    const float* S = Lg.S[i];
+                    z[i] = S[0] * v.x + S[1] * v.y + S[2] * v.z;
+                    bacc[c] = fmaf(z[i], Lg.uf[i], bacc[c]);
+                }
+                asm volatile("" : "+v"(z[6 + 3 * (b - 1)]), "+v"(z[7 + 3 * (b - 1)]), "+v"(z[8 + 3 * (b - 1)]),
+                             "+v"(bacc[0]), "+v"(bacc[1]), "+v"(bacc[2]));
             }
+            brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
             if (lane < nr && kind == 0) {
                 const float g = L.cgap[ci];
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             zbs<NG - 1>(L.Lp, z);
             uint32_t live = 0u;  // groups of 4 dofs with a nonzero entry in some row
+            float dacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int g = 0; g < NGRP; ++g) {
                 const Lds& Lg = *opaque(&L);
                 bool nz = false;
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4; ++k) {
+                    const int i = 4 * g + k < NG ? 4 * g + k : 0;
                     if (4 * g + k < NG) {
-                        fmul_ordered(z[4 * g + k < NG ? 4 * g + k : 0], Lg.sDinv[4 * g + k < NG ? 4 * g + k : 0]);
-                        nz |= z[4 * g + k < NG ? 4 * g + k : 0] != 0.f;
+                        z[i] *= Lg.sDinv[i];
+                        dacc[k] = fmaf(z[i], z[i], dacc[k]);
+                        nz |= z[i] != 0.f;
+                        asm volatile("" : "+v"(z[i]), "+v"(dacc[k]));
                     }
+                }
                 if (__ballot(nz)) live |= 1u << g;
             }
-#pragma unroll
-            for (int i = 0; i < NG; ++i) ffma_ordered(diag, z[i], z[i]);
+            diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
             delassus_rows<0>(z, acol, nr, live);

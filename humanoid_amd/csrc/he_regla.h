@@ -154,10 +154,22 @@ __device__ __forceinline__ void fnma(float& z, float a, float b) {
 }
 
 // ---------------------------------------------------------------- per-lane z <- L^-T z (each lane its own rhs)
+// the packed row K (D entries) as registers: ceil(D/4) 16-byte LDS broadcasts
+template <int D>
+struct Row {
+    float4 v[(D + 3) / 4 > 0 ? (D + 3) / 4 : 1];
+};
+template <int K>
+__device__ __forceinline__ Row<kDofNanc[K] - 1> load_row(const float* Lp, int off) {
+    Row<kDofNanc[K] - 1> r;
+#pragma unroll
+    for (int q = 0; q < (kDofNanc[K] - 1 + 3) / 4; ++q) r.v[q] = *reinterpret_cast<const float4*>(Lp + off + 4 * q);
+    return r;
+}
 template <int K, int X, int D>
-__device__ __forceinline__ void zbs_anc(const float* row, float (&z)[NG], float zk) {
+__device__ __forceinline__ void zbs_anc(const Row<D>& row, float (&z)[NG], float zk) {
     if constexpr (X < D) {
-        const float4 v = *reinterpret_cast<const float4*>(row + X);
+        const float4 v = row.v[X / 4];
         fnma(z[kChain[K][X]], v.x, zk);
         if constexpr (X + 1 < D) fnma(z[kChain[K][X + 1]], v.y, zk);
         if constexpr (X + 2 < D) fnma(z[kChain[K][X + 2]], v.z, zk);
@@ -165,19 +177,29 @@ __device__ __forceinline__ void zbs_anc(const float* row, float (&z)[NG], float 
         zbs_anc<K, X + 4, D>(row, z, zk);
     }
 }
+// z <- L^-T z, two dofs (K, K-1) per step: both rows' LDS reads are issued together behind one
+// opaque offset (one wait per pair instead of per dof); a dof whose entry is zero on every lane
+// after its descendants were processed is skipped (the support is ancestor-closed)
 template <int K>
 __device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG]) {
-    if constexpr (K >= 1) {
-        // the row offset passes through an opaque VGPR at this point of the program, so the LDS
-        // reads of row K cannot be hoisted ahead of the sweep (which would need ~1k VGPRs)
-        const float zk = z[K];
-        if (__ballot(zk != 0.f)) {  // dof outside every row's (ancestor-closed) support: no-op
-            int off = kPackStart[K];
+    if constexpr (K >= 2) {
+        if (__ballot(z[K] != 0.f) || __ballot(z[K - 1] != 0.f)) {
+            int off = 0;
             asm volatile("" : "+v"(off));
-            zbs_anc<K, 0, kDofNanc[K] - 1>(Lp + off, z, zk);
+            const auto rk = load_row<K>(Lp, off + kPackStart[K]);
+            const auto rk1 = load_row<K - 1>(Lp, off + kPackStart[K - 1]);
+            if (__ballot(z[K] != 0.f)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z, z[K]);
+            if (__ballot(z[K - 1] != 0.f)) zbs_anc<K - 1, 0, kDofNanc[K - 1] - 1>(rk1, z, z[K - 1]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        zbs<K - 1>(Lp, z);
+        zbs<K - 2>(Lp, z);
+    } else if constexpr (K == 1) {
+        if (__ballot(z[1] != 0.f)) {
+            int off = 0;
+            asm volatile("" : "+v"(off));
+            const auto r1 = load_row<1>(Lp, off + kPackStart[1]);
+            zbs_anc<1, 0, kDofNanc[1] - 1>(r1, z, z[1]);
+        }
     }
 }
 

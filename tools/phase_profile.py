@@ -47,6 +47,9 @@ def main():
     total = mean[:len(PHASES)].sum()
     rows = {PHASES[i]: {"cycles": round(float(mean[i])), "share": round(float(mean[i] / total), 4)}
             for i in range(len(PHASES))}
+    # sub-phase slots 14/15 (when a diagnostic build stamps them) are carved out of their phase
+    extra = {f"slot{i}": round(float(mean[i])) for i in range(len(PHASES), 16) if mean[i] != 0}
+    rows.update(extra)
     print(json.dumps({"config": args.config, "num_envs": args.num_envs, "mean_contacts": float(np.mean(nc)),
                       "cycles_per_env_step": round(float(total)), "phases": rows}, indent=1))
 
