@@ -44,6 +44,7 @@ struct BodyTopo {
     int8_t dof0[NB];
     uint32_t anc_mask[NB];
     uint32_t sub_mask[NB];
+    float local_pos[NB][3];  // joint offsets (model), read along every FK chain walk
 };
 
 struct Lds {
@@ -291,8 +292,8 @@ HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float in
 // CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i for j in chain(i)
 // (compile-time lane masks), plus armature and the implicit-drive terms on the diagonal
 template <int I>
-HE_DEV void crba_rows(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], const Lds& L, const he_model& m,
-                      float dt, int lane) {
+HE_DEV void crba_rows(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], float dadd, float dadd2,
+                      const Lds& L) {
     using namespace regla;
     if constexpr (I < NG) {
         // rows are pinned in groups of four (opaque base): loads of a group overlap, groups stay
@@ -301,19 +302,17 @@ HE_DEV void crba_rows(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)
         float IS[6];
         for (int x = 0; x < 6; ++x) IS[x] = Lg.IS[I][x];
         float h = lanes<smpl::kAncLo[I]>() ? dot6(Sj, IS) : 0.f;
-        if constexpr (I >= 6 && I < 64) {
-            if (lane == I) h += m.armature[I - 6] + dt * Lg.coef[I];
-        }
+        if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
         asm volatile("" : "+v"(h));
         M.c[I] = h;
         if constexpr (I >= 64) {
             float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? dot6(Sj2, IS) : 0.f;
-            if (lane == I - 64) h2 += m.armature[I - 6] + dt * Lg.coef[I];
+            h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
             asm volatile("" : "+v"(h2));
             M.c2[I - 64] = h2;
         }
-        if constexpr (I % 4 == 3) crba_rows<I + 1>(M, Sj, Sj2, *opaque(&L), m, dt, lane);
-        else crba_rows<I + 1>(M, Sj, Sj2, Lg, m, dt, lane);
+        if constexpr (I % 4 == 3) crba_rows<I + 1>(M, Sj, Sj2, dadd, dadd2, *opaque(&L));
+        else crba_rows<I + 1>(M, Sj, Sj2, dadd, dadd2, Lg);
     }
 }
 
@@ -356,7 +355,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
         int depth = T.depth[lane];
         for (int k = 1; k <= depth; ++k) {
             int a = T.chain[lane][k];
-            p = p + qapply(q, f3{m.local_pos[a][0], m.local_pos[a][1], m.local_pos[a][2]});
+            p = p + qapply(q, f3{T.local_pos[a][0], T.local_pos[a][1], T.local_pos[a][2]});
             q = qmul(q, f4{L.ql[a][0], L.ql[a][1], L.ql[a][2], L.ql[a][3]});
         }
         L.qw[lane][0] = q.x; L.qw[lane][1] = q.y; L.qw[lane][2] = q.z; L.qw[lane][3] = q.w;
@@ -511,7 +510,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     {
         float Sj[6], Sj2[6];
         for (int x = 0; x < 6; ++x) { Sj[x] = L.S[lane][x]; Sj2[x] = lane < NH ? L.S[64 + lane][x] : 0.f; }
-        crba_rows<0>(M, Sj, Sj2, L, m, dt, lane);
+        // per-lane diagonal addend (dof = lane, and 64 + lane on lanes < 11), loaded once
+        const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + dt * L.coef[lane] : 0.f;
+        const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + dt * L.coef[64 + lane] : 0.f;
+        crba_rows<0>(M, Sj, Sj2, dadd, dadd2, L);
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
@@ -832,6 +834,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         L.T.dof0[lane] = T.body_dof0[lane];
         L.T.anc_mask[lane] = T.anc_mask[lane];
         L.T.sub_mask[lane] = T.sub_mask[lane];
+        for (int c = 0; c < 3; ++c) L.T.local_pos[lane][c] = m.local_pos[lane][c];
     }
     // ---- load state
     const float* rs = a.root_states + (size_t)e * 13;
