@@ -291,28 +291,42 @@ HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float in
 
 // CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i for j in chain(i)
 // (compile-time lane masks), plus armature and the implicit-drive terms on the diagonal
+// one CRBA row I from its IS_I (registers)
 template <int I>
-HE_DEV void crba_rows(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], float dadd, float dadd2,
-                      const Lds& L) {
+HE_DEV void crba_row(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], float dadd, float dadd2,
+                     const float* IS) {
     using namespace regla;
-    if constexpr (I < NG) {
-        // rows are pinned in groups of four (opaque base): loads of a group overlap, groups stay
-        // in order, and each result is produced here rather than sunk next to the factorisation
-        const Lds& Lg = (I % 4 == 0) ? *opaque(&L) : L;
-        float IS[6];
-        for (int x = 0; x < 6; ++x) IS[x] = Lg.IS[I][x];
-        float h = lanes<smpl::kAncLo[I]>() ? dot6(Sj, IS) : 0.f;
-        if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
-        asm volatile("" : "+v"(h));
-        M.c[I] = h;
-        if constexpr (I >= 64) {
-            float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? dot6(Sj2, IS) : 0.f;
-            h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
-            asm volatile("" : "+v"(h2));
-            M.c2[I - 64] = h2;
+    float h = lanes<smpl::kAncLo[I]>() ? dot6(Sj, IS) : 0.f;
+    if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
+    asm volatile("" : "+v"(h));
+    M.c[I] = h;
+    if constexpr (I >= 64) {
+        float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? dot6(Sj2, IS) : 0.f;
+        h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
+        asm volatile("" : "+v"(h2));
+        M.c2[I - 64] = h2;
+    }
+}
+
+// CRBA straight into registers, four rows per group, software-pipelined: the LDS reads of group
+// G+1 are issued (behind an opaque base) before group G is computed from registers
+template <int G>
+HE_DEV void crba_groups(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], float dadd, float dadd2,
+                        const Lds& L, const float (&cur)[4][6]) {
+    if constexpr (4 * G < NG) {
+        float nxt[4][6];
+        if constexpr (4 * (G + 1) < NG) {
+            const Lds& Lg = *opaque(&L);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * (G + 1) + k < NG)
+                    for (int x = 0; x < 6; ++x) nxt[k][x] = Lg.IS[4 * (G + 1) + k < NG ? 4 * (G + 1) + k : 0][x];
         }
-        if constexpr (I % 4 == 3) crba_rows<I + 1>(M, Sj, Sj2, dadd, dadd2, *opaque(&L));
-        else crba_rows<I + 1>(M, Sj, Sj2, dadd, dadd2, Lg);
+        crba_row<4 * G>(M, Sj, Sj2, dadd, dadd2, cur[0]);
+        if constexpr (4 * G + 1 < NG) crba_row<4 * G + 1>(M, Sj, Sj2, dadd, dadd2, cur[1]);
+        if constexpr (4 * G + 2 < NG) crba_row<4 * G + 2>(M, Sj, Sj2, dadd, dadd2, cur[2]);
+        if constexpr (4 * G + 3 < NG) crba_row<4 * G + 3>(M, Sj, Sj2, dadd, dadd2, cur[3]);
+        crba_groups<G + 1>(M, Sj, Sj2, dadd, dadd2, L, nxt);
     }
 }
 
@@ -513,7 +527,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         // per-lane diagonal addend (dof = lane, and 64 + lane on lanes < 11), loaded once
         const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + dt * L.coef[lane] : 0.f;
         const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + dt * L.coef[64 + lane] : 0.f;
-        crba_rows<0>(M, Sj, Sj2, dadd, dadd2, L);
+        float first[4][6];
+        for (int k = 0; k < 4; ++k)
+            for (int x = 0; x < 6; ++x) first[k][x] = L.IS[k][x];
+        crba_groups<0>(M, Sj, Sj2, dadd, dadd2, L, first);
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
@@ -667,6 +684,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             const uint32_t anc1 = (lane < nr && L.cb1[ci] >= 0) ? T.anc_mask[L.cb1[ci]] : 0u;
             const f3 dd = f3{dir[0], dir[1], dir[2]};
             const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o, dd);
+            // bodies on some row's support (wave-uniform): the only ones whose dofs can be nonzero
+            uint32_t lb = anc0 | anc1;
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) lb |= (uint32_t)__shfl_xor((int)lb, sh, W);
+            lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)lb);
             // z = J_r^T and brow = J_r uf, four dofs per pinned group (their LDS reads overlap; the
             // results are fixed in place so the loads cannot all be hoisted ahead of the math)
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -684,6 +706,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 // joint b: S_i = [a_i; (p_b - o) x a_i], so S_i . (rho, dd) = a_i . ((x - p_b) x dd);
                 // LDS reads pinned per group of four bodies
                 if (b % 4 == 1) Lgp = opaque(&L);
+                if (!((lb >> b) & 1u)) {
+                    z[6 + 3 * (b - 1)] = 0.f; z[7 + 3 * (b - 1)] = 0.f; z[8 + 3 * (b - 1)] = 0.f;
+                    continue;
+                }
                 const Lds& Lg = *Lgp;
                 const float sgn = (float)((anc0 >> b) & 1u) - (float)((anc1 >> b) & 1u);
                 const f3 v = cross3(cx - f3{Lg.pw[b][0], Lg.pw[b][1], Lg.pw[b][2]}, dd) * sgn;
@@ -702,7 +728,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 const float g = L.cgap[ci];
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
-            zbs<NG - 1>(L.Lp, z);
+            zbs<NG - 1>(L.Lp, z, lb);
             uint32_t live = 0u;  // groups of 4 dofs with a nonzero entry in some row
             float dacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

@@ -177,30 +177,46 @@ __device__ __forceinline__ void zbs_anc(const Row<D>& row, float (&z)[NG], float
         zbs_anc<K, X + 4, D>(row, z, zk);
     }
 }
-// z <- L^-T z, two dofs (K, K-1) per step: both rows' LDS reads are issued together behind one
-// opaque offset (one wait per pair instead of per dof); a dof whose entry is zero on every lane
-// after its descendants were processed is skipped (the support is ancestor-closed)
+// z <- L^-T z, one dof per step, software-pipelined: the next row is read (16-byte LDS
+// broadcasts behind an opaque offset) while this one is applied. Only dofs of bodies
+// in `lb` (the union of every row's ancestor bodies, wave-uniform) can be nonzero; the others are
+// skipped without touching LDS.
 template <int K>
-__device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG]) {
-    if constexpr (K >= 2) {
-        if (__ballot(z[K] != 0.f) || __ballot(z[K - 1] != 0.f)) {
-            int off = 0;
-            asm volatile("" : "+v"(off));
-            const auto rk = load_row<K>(Lp, off + kPackStart[K]);
-            const auto rk1 = load_row<K - 1>(Lp, off + kPackStart[K - 1]);
-            if (__ballot(z[K] != 0.f)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z, z[K]);
-            if (__ballot(z[K - 1] != 0.f)) zbs_anc<K - 1, 0, kDofNanc[K - 1] - 1>(rk1, z, z[K - 1]);
-            __builtin_amdgcn_sched_barrier(0);
+__device__ __forceinline__ bool body_live(uint32_t lb) {
+    if constexpr (K < 0) return false;
+    else return (lb >> kDofBody[K]) & 1u;
+}
+template <int K>
+struct RowOf {
+    using T = Row<(K >= 0 ? kDofNanc[K < 0 ? 0 : K] : 1) - 1>;
+};
+template <int K>
+__device__ __forceinline__ typename RowOf<K>::T load_row_if(const float* Lp, int off) {
+    if constexpr (K >= 1) return load_row<K>(Lp, off + kPackStart[K]);
+    else return typename RowOf<K>::T{};
+}
+template <int K>
+__device__ __forceinline__ void zbs_pipe(const float* Lp, float (&z)[NG], uint32_t lb, const typename RowOf<K>::T& rk) {
+    if constexpr (K >= 1) {
+        typename RowOf<K - 1>::T nx;
+        if constexpr (K - 1 >= 1) {
+            if (body_live<K - 1>(lb)) {  // prefetch row K-1 while row K is applied
+                int off = 0;
+                asm volatile("" : "+v"(off));
+                nx = load_row_if<K - 1>(Lp, off);
+            }
         }
-        zbs<K - 2>(Lp, z);
-    } else if constexpr (K == 1) {
-        if (__ballot(z[1] != 0.f)) {
-            int off = 0;
-            asm volatile("" : "+v"(off));
-            const auto r1 = load_row<1>(Lp, off + kPackStart[1]);
-            zbs_anc<1, 0, kDofNanc[1] - 1>(r1, z, z[1]);
-        }
+        if (body_live<K>(lb)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z, z[K]);
+        __builtin_amdgcn_sched_barrier(0);
+        zbs_pipe<K - 1>(Lp, z, lb, nx);
     }
+}
+template <int K>
+__device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG], uint32_t lb) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    const auto r0 = load_row_if<K>(Lp, off);
+    zbs_pipe<K>(Lp, z, lb, r0);
 }
 
 // ---------------------------------------------------------------- y <- L^-1 y, row-distributed
