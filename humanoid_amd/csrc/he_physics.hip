@@ -291,7 +291,66 @@ HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float in
 
 // CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i for j in chain(i)
 // (compile-time lane masks), plus armature and the implicit-drive terms on the diagonal
-// one CRBA row I from its IS_I (registers)
+// ---- contact-row helpers (rows phase)
+// bodies touched by dof group g (4 dofs), as a mask over bodies
+struct GroupBodies {
+    uint32_t m[(NG + 3) / 4];
+    constexpr GroupBodies() : m() {
+        for (int g = 0; g < (NG + 3) / 4; ++g) {
+            m[g] = 0u;
+            for (int k = 0; k < 4; ++k)
+                if (4 * g + k < NG) m[g] |= 1u << smpl::kDofBody[4 * g + k];
+        }
+    }
+};
+constexpr GroupBodies kGroupBodiesT{};
+constexpr const uint32_t* kGroupBodies = kGroupBodiesT.m;
+
+// joint b's data for the row Jacobian: body origin (3), its 3 joint axes (9), their free velocities (3)
+HE_DEV void zrow_load(const Lds& L, int b, float (&d)[15]) {
+    const Lds& Lg = *opaque(&L);
+    for (int x = 0; x < 3; ++x) d[x] = Lg.pw[b][x];
+    for (int c = 0; c < 3; ++c) {
+        const int i = 6 + 3 * (b - 1) + c;
+        for (int x = 0; x < 3; ++x) d[3 + 3 * c + x] = Lg.S[i][x];
+        d[12 + c] = Lg.uf[i];
+    }
+}
+// z_i = S_i . (rho, dd) = a_i . ((x - p_b) x dd) for joint b's three dofs, bodies in order with
+// the next live body's data read while this one is computed
+template <int B>
+HE_DEV void zrow_bodies(float (&z)[NG], float (&bacc)[4], uint32_t lb, uint32_t anc0, uint32_t anc1, f3 cx, f3 dd,
+                        const Lds& L, const float (&cur)[15]) {
+    if constexpr (B < NB) {
+        float nxt[15];
+        if constexpr (B + 1 < NB) {
+            if ((lb >> (B + 1)) & 1u) zrow_load(L, B + 1, nxt);
+        }
+        constexpr int i0 = 6 + 3 * (B - 1);
+        if ((lb >> B) & 1u) {
+            const float sgn = (float)((anc0 >> B) & 1u) - (float)((anc1 >> B) & 1u);
+            const f3 v = cross3(cx - f3{cur[0], cur[1], cur[2]}, dd) * sgn;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                z[i0 + c] = cur[3 + 3 * c] * v.x + cur[4 + 3 * c] * v.y + cur[5 + 3 * c] * v.z;
+                bacc[c] = fmaf(z[i0 + c], cur[12 + c], bacc[c]);
+            }
+        } else {
+            z[i0] = 0.f; z[i0 + 1] = 0.f; z[i0 + 2] = 0.f;
+        }
+        asm volatile("" : "+v"(z[i0]), "+v"(z[i0 + 1]), "+v"(z[i0 + 2]), "+v"(bacc[0]), "+v"(bacc[1]), "+v"(bacc[2]));
+        zrow_bodies<B + 1>(z, bacc, lb, anc0, anc1, cx, dd, L, nxt);
+    }
+}
+template <int I>
+HE_DEV void scale_rows(float (&z)[NG], float sdl, float sdl2) {
+    if constexpr (I < NG) {
+        z[I] *= I < 64 ? regla::rdlane(sdl, I < 64 ? I : 0) : regla::rdlane(sdl2, I >= 64 ? I - 64 : 0);
+        scale_rows<I + 1>(z, sdl, sdl2);
+    }
+}
+
+// CRBA: one row I from its IS_I (registers)
 template <int I>
 HE_DEV void crba_row(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], float dadd, float dadd2,
                      const float* IS) {
@@ -700,28 +759,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             }
             for (int i = 0; i < 6; ++i) bacc[i & 3] = fmaf(z[i], L.uf[i], bacc[i & 3]);
             const f3 cx = f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]};
-            const Lds* Lgp = &L;
-#pragma unroll
-            for (int b = 1; b < NB; ++b) {
-                // joint b: S_i = [a_i; (p_b - o) x a_i], so S_i . (rho, dd) = a_i . ((x - p_b) x dd);
-                // LDS reads pinned per group of four bodies
-                if (b % 4 == 1) Lgp = opaque(&L);
-                if (!((lb >> b) & 1u)) {
-                    z[6 + 3 * (b - 1)] = 0.f; z[7 + 3 * (b - 1)] = 0.f; z[8 + 3 * (b - 1)] = 0.f;
-                    continue;
-                }
-                const Lds& Lg = *Lgp;
-                const float sgn = (float)((anc0 >> b) & 1u) - (float)((anc1 >> b) & 1u);
-                const f3 v = cross3(cx - f3{Lg.pw[b][0], Lg.pw[b][1], Lg.pw[b][2]}, dd) * sgn;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const int i = 6 + 3 * (b - 1) + c;
-                    const float* S = Lg.S[i];
-                    z[i] = S[0] * v.x + S[1] * v.y + S[2] * v.z;
-                    bacc[c] = fmaf(z[i], Lg.uf[i], bacc[c]);
-                }
-                asm volatile("" : "+v"(z[6 + 3 * (b - 1)]), "+v"(z[7 + 3 * (b - 1)]), "+v"(z[8 + 3 * (b - 1)]),
-                             "+v"(bacc[0]), "+v"(bacc[1]), "+v"(bacc[2]));
+            {
+                float cur[15];
+                if ((lb >> 1) & 1u) zrow_load(L, 1, cur);
+                zrow_bodies<1>(z, bacc, lb, anc0, anc1, cx, dd, L, cur);
             }
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
             if (lane < nr && kind == 0) {
@@ -729,25 +770,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             zbs<NG - 1>(L.Lp, z, lb);
-            uint32_t live = 0u;  // groups of 4 dofs with a nonzero entry in some row
+            // z <- D^-1/2 z: the scale of dof i is broadcast from lane i's register (no LDS)
+            const float sdl = L.sDinv[lane], sdl2 = lane < NH ? L.sDinv[64 + lane] : 0.f;
+            scale_rows<0>(z, sdl, sdl2);
             float dacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int g = 0; g < NGRP; ++g) {
-                const Lds& Lg = *opaque(&L);
-                bool nz = false;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int i = 4 * g + k < NG ? 4 * g + k : 0;
-                    if (4 * g + k < NG) {
-                        z[i] *= Lg.sDinv[i];
-                        dacc[k] = fmaf(z[i], z[i], dacc[k]);
-                        nz |= z[i] != 0.f;
-                        asm volatile("" : "+v"(z[i]), "+v"(dacc[k]));
-                    }
-                }
-                if (__ballot(nz)) live |= 1u << g;
-            }
+            for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(z[i], z[i], dacc[i & 3]);
             diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
+            // dof groups of four touching a support body (wave-uniform, from lb)
+            uint32_t live = 0u;
+#pragma unroll
+            for (int g = 0; g < NGRP; ++g)
+                if (lb & kGroupBodies[g]) live |= 1u << g;
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
             delassus_rows<0>(z, acol, nr, live);

@@ -190,6 +190,19 @@ def _cond_close(name, g, o, s, atol, rtol=0.0, k=4.0):
                            f"{(np.abs(g - o) - allow).max():.3e}")
 
 
+def _obs_tol(oo):
+    """Per-element obs tolerance: 5e-5 + 1e-5 rel, and for the velocity blocks (self lin/ang vel
+    214:358, task vel/ang-vel differences 574:718) 2e-6 of the 3-vector's norm: a body spinning at
+    the 100 rad/s clamp is rotated into the heading frame in fp32 by two different instruction
+    orders (kernel vs C oracle), so each component carries ~1e-6 x |v| of rounding."""
+    tol = 5e-5 + 1e-5 * np.abs(oo)
+    for a, b in ((214, 358), (574, 718)):
+        blk = oo[:, a:b].reshape(oo.shape[0], -1, 3)
+        nrm = np.repeat(np.linalg.norm(blk, axis=-1), 3, axis=-1)
+        tol[:, a:b] = np.maximum(tol[:, a:b], 5e-5 + 2e-6 * nrm)
+    return tol
+
+
 def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=1e-4, vel_tol=1e-2, max_skip=0.1,
                      **sim):
     n = root.shape[0]
@@ -351,7 +364,12 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
         np.testing.assert_array_equal(term.cpu().numpy(), im["terminate"])
         np.testing.assert_allclose(rew.cpu().numpy(), im["rew"], atol=5e-5, rtol=1e-5)
         np.testing.assert_allclose(raw.cpu().numpy(), im["reward_raw"], atol=5e-5, rtol=1e-5)
-        np.testing.assert_allclose(obs.cpu().numpy(), state["obs"], atol=5e-5, rtol=1e-5)
+        og, oo = obs.cpu().numpy(), state["obs"]
+        bad = np.abs(og - oo) > _obs_tol(oo)
+        assert not bad.any(), (f"obs mismatch at (env, col) {np.argwhere(bad)[:8].tolist()}: gpu {og[bad][:8]} "
+                               f"oracle {oo[bad][:8]}; step {step} reset ids {ids.tolist()} "
+                               f"start gpu {st.cpu().numpy()[np.argwhere(bad)[:1, 0]]} oracle "
+                               f"{state['start_times'][np.argwhere(bad)[:1, 0]]} prog {im['progress'][np.argwhere(bad)[:1, 0]]}")
         np.testing.assert_array_equal(prog.cpu().numpy(), state["progress"])
         np.testing.assert_array_equal(st.cpu().numpy(), state["start_times"])
         if len(ids):
