@@ -44,20 +44,59 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=20)
+    ap.add_argument("--no-puffer-level", action="store_true",
+                    help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
+    ap.add_argument("--puffer-steps", type=int, default=50)
     return ap.parse_args()
 
 
-def build_workload(args, model, rank):
+DATA = {
+    "standstill": "synthetic: one random-free stand-still clip (identity rotations, constant root), actions = 0",
+    "imitation": "synthetic: 128 AMASS-schema random-walk clips (SURVEY §8d recipe), env i -> clip i mod 128, "
+                 "one U(-1,1) action sample reused",
+    "dr": "synthetic: 128 random-walk clips, actions = 0, per-env mass scale U(0.8,1.2), friction U(0.5,1.25), "
+          "terrain by env % 3 (plane / 10 deg slope / steps)",
+}
+
+
+def make_clips(args, model):
     from humanoid_amd import synthetic
+    if args.config == "standstill":
+        return [synthetic.make_standstill_clip(model, num_frames=150)]
+    rng = np.random.default_rng(args.seed)
+    return [synthetic.make_clip(model, rng, num_frames=150) for _ in range(args.clips)]
+
+
+def puffer_level(args, model):
+    """PHCPufferEnv.step rate (clean_pufferl/env.py:109-183 semantics): numpy actions copied to the
+    device every step, fused physics + imitation + device resets, episode bookkeeping on device,
+    info every 32 ticks. PCIe-inclusive; reported beside `value`, never as it."""
+    import torch
+    from humanoid_amd.env import EnvConfig, PHCPufferEnv
+    clips = make_clips(args, model)
+    cfg = EnvConfig(num_envs=args.num_envs, motion_file={f"clip{i}": c for i, c in enumerate(clips)},
+                    seed=args.seed, max_contacts=args.max_contacts)
+    pe = PHCPufferEnv(cfg)
+    pe.reset()
+    _, actions, _ = build_workload(args, model, 0)
+    for _ in range(5):
+        pe.step(actions)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.puffer_steps):
+        pe.step(actions)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    pe.close()
+    return {"value": round(args.num_envs * args.puffer_steps / dt, 1), "unit": "env-steps/s",
+            "steps": args.puffer_steps, "actions": "numpy [N,69] float32 (H2D each step)"}
+
+
+def build_workload(args, model, rank):
     from humanoid_amd.motion_lib import build_tables, MotionTables
     n = args.num_envs
-    if args.config == "standstill":
-        clips = [synthetic.make_standstill_clip(model, num_frames=150)]
-        assign = np.zeros(n, np.int64)
-    else:
-        rng = np.random.default_rng(args.seed)
-        clips = [synthetic.make_clip(model, rng, num_frames=150) for _ in range(args.clips)]
-        assign = np.arange(n) % args.clips
+    clips = make_clips(args, model)
+    assign = np.zeros(n, np.int64) if args.config == "standstill" else np.arange(n) % args.clips
     base = build_tables(model, clips)
     tables = MotionTables(gts=base.gts, grs=base.grs, lrs=base.lrs, gvs=base.gvs, gavs=base.gavs, dvs=base.dvs,
                           num_frames=base.num_frames[assign], length_starts=base.length_starts[assign],
@@ -243,7 +282,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (AMASS-schema clips generated offline; random-free stand-still clip for configs[1])",
+            "data": DATA[args.config],
             "config": {"workload": {"standstill": "configs[1]: 4096 SMPL-neutral humanoids, PD stand-still, zero ref motion",
                                     "imitation": "configs[2]: 4096 humanoids over 128 synthetic clips, full PHC reward",
                                     "dr": "configs[4]: 4096 envs, mass/friction randomisation + 3 terrains"}[args.config],
@@ -257,6 +296,11 @@ def main():
                                  "frac": round(imit_gbs / HBM_PEAK_GBS, 5), "avg_launch_ms": round(imit_ms, 4),
                                  "traffic": imit_traffic},
         }
+        if not args.no_puffer_level and world == 1:
+            try:
+                line["puffer_env_step"] = puffer_level(args, model)
+            except Exception as exc:  # report, never fake
+                line["puffer_env_step"] = {"value": None, "error": repr(exc)}
         if not args.no_cpu_baseline and world == 1:
             try:
                 line["cpu_baseline"] = cpu_baseline(args, model)
