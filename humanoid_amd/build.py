@@ -15,6 +15,7 @@ ARCH = os.environ.get("HE_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     ("he_imitation.hip", ["-ffp-contract=off"]),
     ("he_physics.hip", []),
+    ("he_ingest.hip", []),
     ("he_engine.cpp", ["-x", "hip"]),
 ]
 HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", "he_regla.h", "he_smpl_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h")]

@@ -348,6 +348,79 @@ int he_load_motions(he_engine* h, int64_t F, int M, const float* gts, const floa
     return 0;
 }
 
+int he_ingest_clips(he_engine* h, int num_clips, const int64_t* host_num_frames, const float* host_fps,
+                    const float* pose_quat_global, const float* root_trans, int num_motions,
+                    const int32_t* host_motion_clip, void* stream) {
+    if (!h) return fail("he_ingest_clips: null handle");
+    if (!h->has_model) return fail("he_ingest_clips: call he_set_model first");
+    if (num_clips <= 0 || !host_num_frames || !host_fps || !pose_quat_global || !root_trans)
+        return fail("he_ingest_clips: bad arguments");
+    if (num_motions <= 0) num_motions = num_clips;
+    if (!host_motion_clip && num_motions != num_clips)
+        return fail("he_ingest_clips: motion->clip map required when num_motions != num_clips");
+    std::vector<int64_t> cstart(num_clips), cnf(num_clips);
+    std::vector<float> cdt(num_clips);
+    int64_t F = 0;
+    for (int c = 0; c < num_clips; ++c) {
+        if (host_num_frames[c] < 1 || !(host_fps[c] > 0.f))
+            return fail("he_ingest_clips: clip %d has %lld frames at %g fps", c, (long long)host_num_frames[c],
+                        (double)host_fps[c]);
+        cstart[c] = F;
+        cnf[c] = host_num_frames[c];
+        cdt[c] = (float)(1.0 / (double)host_fps[c]);
+        F += host_num_frames[c];
+    }
+    std::vector<int64_t> ms(num_motions), mn(num_motions);
+    std::vector<float> ml(num_motions), mdt(num_motions);
+    for (int i = 0; i < num_motions; ++i) {
+        const int c = host_motion_clip ? host_motion_clip[i] : i;
+        if (c < 0 || c >= num_clips) return fail("he_ingest_clips: motion %d maps to clip %d of %d", i, c, num_clips);
+        ms[i] = cstart[c];
+        mn[i] = cnf[c];
+        // motion_lib.py:376-379: curr_len = 1/fps * (num_frames - 1) in python floats -> float32
+        ml[i] = (float)(1.0 / (double)host_fps[c] * (double)(cnf[c] - 1));
+        mdt[i] = (float)(1.0 / (double)host_fps[c]);
+    }
+    HE_CHECK(hipSetDevice(h->device));
+    const hipStream_t st = (hipStream_t)stream;
+    HE_CHECK(hipStreamSynchronize(st));  // tables may be in use by queued kernels
+    void* old[] = {h->m_hot, h->m_cold, h->m_lengths, h->m_dt, h->m_starts, h->m_nframes};
+    for (void* p : old)
+        if (p) HE_CHECK(hipFree(p));
+    h->m_hot = h->m_cold = h->m_lengths = h->m_dt = nullptr;
+    h->m_starts = h->m_nframes = nullptr;
+    h->m_motions = 0;
+    const int B = HE_NUM_BODIES;
+    HE_CHECK(dalloc(&h->m_hot, (size_t)F * B * HE_MOTION_HOT));
+    HE_CHECK(dalloc(&h->m_cold, (size_t)F * B * HE_MOTION_COLD));
+    HE_CHECK(dalloc(&h->m_lengths, (size_t)num_motions));
+    HE_CHECK(dalloc(&h->m_dt, (size_t)num_motions));
+    HE_CHECK(dalloc(&h->m_starts, (size_t)num_motions));
+    HE_CHECK(dalloc(&h->m_nframes, (size_t)num_motions));
+    HE_CHECK(hipMemcpy(h->m_lengths, ml.data(), num_motions * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_dt, mdt.data(), num_motions * sizeof(float), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_starts, ms.data(), num_motions * sizeof(int64_t), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(h->m_nframes, mn.data(), num_motions * sizeof(int64_t), hipMemcpyHostToDevice));
+    int64_t *d_cs = nullptr, *d_cn = nullptr;
+    float *d_cdt = nullptr, *scratch = nullptr;
+    HE_CHECK(dalloc(&d_cs, (size_t)num_clips));
+    HE_CHECK(dalloc(&d_cn, (size_t)num_clips));
+    HE_CHECK(dalloc(&d_cdt, (size_t)num_clips));
+    HE_CHECK(dalloc(&scratch, (size_t)F * B * 3));
+    HE_CHECK(hipMemcpy(d_cs, cstart.data(), num_clips * sizeof(int64_t), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(d_cn, cnf.data(), num_clips * sizeof(int64_t), hipMemcpyHostToDevice));
+    HE_CHECK(hipMemcpy(d_cdt, cdt.data(), num_clips * sizeof(float), hipMemcpyHostToDevice));
+    hipError_t e = launch_ingest(pose_quat_global, root_trans, h->d_model->parents, &h->d_model->local_pos[0][0],
+                                 d_cs, d_cn, d_cdt, num_clips, F, h->m_hot, h->m_cold, scratch, st);
+    hipError_t e2 = hipStreamSynchronize(st);
+    hipFree(d_cs); hipFree(d_cn); hipFree(d_cdt); hipFree(scratch);
+    HE_CHECK(e);
+    HE_CHECK(e2);
+    h->m_frames = F;
+    h->m_motions = num_motions;
+    return 0;
+}
+
 namespace {
 MotionDev motion_dev(he_engine* h) {
     return MotionDev{h->m_hot, h->m_cold, h->m_starts, h->m_nframes, h->m_lengths, h->m_dt, h->m_motions};

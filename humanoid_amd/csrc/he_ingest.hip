@@ -1,0 +1,182 @@
+// he_ingest.hip -- device-side motion ingestion: AMASS-schema clips (global joint
+// rotations + root translation per frame) -> the engine's interleaved motion tables, replacing the
+// host path MotionLibSMPL.load_motion_with_skeleton (motion_lib.py:743-824) + the poselib
+// SkeletonState / SkeletonMotion construction (poselib_skeleton.py:518-539, 574-592, 1166-1251)
+// + compute_motion_dof_vels_jit (motion_lib.py:119-140). Restated on the host in
+// humanoid_amd/motion_lib.py:clip_to_motion, which the GPU tests use as the checker.
+//
+// Two launches over all frames of all clips (one 32-lane group per frame, lane = body):
+//   1. frame_kernel: local rotations, FK translations, raw angular velocity (successive global
+//      rotation difference), dof velocities (successive local rotation difference; the last frame
+//      repeats the previous one); hot/cold records except the two filtered velocity slots;
+//   2. filter_kernel: linear velocity = np.gradient of the translations / dt, then both velocity
+//      channels through a Gaussian filter (sigma 2, radius 8, mode "nearest") within each clip.
+#include <hip/hip_runtime.h>
+
+#include "../../include/humanoid_engine.h"
+#include "he_kernels.h"
+#include "he_math.h"
+
+namespace {
+
+constexpr int NB = HE_NUM_BODIES;
+constexpr int GROUP = 32;
+constexpr int HOT = HE_MOTION_HOT;
+constexpr int COLD = HE_MOTION_COLD;
+constexpr int RADIUS = 8;  // scipy gaussian_filter1d(sigma=2, truncate=4): int(4 * 2 + 0.5)
+
+// normalize(quat_pos(a*b)) (torch_utils.quat_mul_norm: quat_unit(quat_pos(quat_mul)))
+HE_DEV f4 qmul_norm(f4 a, f4 b) {
+    f4 q = qmul(a, b);
+    if (q.w < 0.f) q = qneg(q);
+    float n = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-9f);
+    return f4{q.x / n, q.y / n, q.z / n, q.w / n};
+}
+// torch_utils.quat_rotate (v + w t + qv x t, t = 2 qv x v)
+HE_DEV f3 qrotate(f4 q, f3 v) {
+    f3 qv = f3{q.x, q.y, q.z};
+    f3 t = cross3(qv, v) * 2.0f;
+    return v + t * q.w + cross3(qv, t);
+}
+HE_DEV f4 ld4(const float* p) { return f4{p[0], p[1], p[2], p[3]}; }
+
+HE_DEV int clip_of(const int64_t* starts, int num_clips, int64_t f) {
+    int lo = 0, hi = num_clips - 1;
+    while (lo < hi) {  // last clip whose start <= f
+        int mid = (lo + hi + 1) >> 1;
+        if (starts[mid] <= f) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+struct IngestArgs {
+    const float* pose;      // [F][24][4] global rotations xyzw
+    const float* trans;     // [F][3] root translation
+    const int32_t* parents; // [24]
+    const float* local_pos; // [24][3]
+    const int64_t* starts;  // [C] clip frame starts
+    const int64_t* nframes; // [C]
+    const float* dt;        // [C]
+    int num_clips;
+    int64_t F;
+    float* hot;             // [F][24][13]
+    float* cold;            // [F][24][8]
+    float* gav_raw;         // [F][24][3] scratch
+    float gauss[2 * RADIUS + 1];  // normalised taps
+};
+
+// local rotation of body b at frame f (poselib_skeleton.py:574-592): root = global
+HE_DEV f4 local_rot(const IngestArgs& a, int64_t f, int b) {
+    const float* g = a.pose + (size_t)f * NB * 4;
+    f4 gb = ld4(g + 4 * b);
+    if (b == 0) return gb;
+    return qmul_norm(qconj(ld4(g + 4 * a.parents[b])), gb);
+}
+
+__global__ void __launch_bounds__(256) frame_kernel(IngestArgs a) {
+    const int lane = threadIdx.x & (GROUP - 1);
+    const int64_t f = (int64_t)blockIdx.x * (blockDim.x / GROUP) + threadIdx.x / GROUP;
+    if (f >= a.F || lane >= NB) return;
+    const int b = lane;
+    const int c = clip_of(a.starts, a.num_clips, f);
+    const int64_t s = a.starts[c], n = a.nframes[c];
+    const float dt = a.dt[c];
+    const float* g = a.pose + (size_t)f * NB * 4;
+    // FK along b's chain (poselib_skeleton.py:518-539): walk up, then compose root -> b
+    int chain[10], depth = 0;
+    for (int x = b; x > 0; x = a.parents[x]) chain[depth++] = x;
+    f4 gr = local_rot(a, f, 0);
+    f3 gt = f3{a.trans[3 * f], a.trans[3 * f + 1], a.trans[3 * f + 2]};
+    for (int k = depth - 1; k >= 0; --k) {
+        const int x = chain[k];
+        const f3 lt = f3{a.local_pos[3 * x], a.local_pos[3 * x + 1], a.local_pos[3 * x + 2]};
+        gt = qrotate(gr, lt) + gt;
+        gr = qmul_norm(gr, local_rot(a, f, x));
+    }
+    const f4 grot = ld4(g + 4 * b);
+    const f4 lrot = local_rot(a, f, b);
+    float* h = a.hot + ((size_t)f * NB + b) * HOT;
+    h[0] = gt.x; h[1] = gt.y; h[2] = gt.z;
+    h[3] = grot.x; h[4] = grot.y; h[5] = grot.z; h[6] = grot.w;
+    // raw angular velocity (poselib_skeleton.py:1240-1251): last frame of a clip = identity
+    f3 w = f3{0.f, 0.f, 0.f};
+    if (f + 1 < s + n) {
+        f4 d = qmul_norm(ld4(g + NB * 4 + 4 * b), qconj(grot));
+        float cs = fminf(fmaxf(2.f * d.w * d.w - 1.f, -1.f), 1.f);
+        float ang = acosf(cs);
+        float an = fmaxf(sqrtf(d.x * d.x + d.y * d.y + d.z * d.z), 1e-9f);
+        const f3 ax = f3{d.x / an, d.y / an, d.z / an} * ang;
+        w = f3{ax.x / dt, ax.y / dt, ax.z / dt};  // (axis * angle) / dt, the host's order
+    }
+    float* wr = a.gav_raw + ((size_t)f * NB + b) * 3;
+    wr[0] = w.x; wr[1] = w.y; wr[2] = w.z;
+    // dof velocity (motion_lib.py:119-140): from (f, f+1); the clip's last frame repeats (f-1, f)
+    float* cr = a.cold + ((size_t)f * NB + b) * COLD;
+    cr[0] = lrot.x; cr[1] = lrot.y; cr[2] = lrot.z; cr[3] = lrot.w;
+    f3 dv = f3{0.f, 0.f, 0.f};
+    if (b > 0 && n > 1) {
+        const int64_t f0 = (f + 1 < s + n) ? f : f - 1;
+        f4 q = qmul(qconj(local_rot(a, f0, b)), local_rot(a, f0 + 1, b));
+        f3 ax;
+        float an = q_angle_axis(q, &ax);
+        ax = ax * an;
+        dv = f3{ax.x / dt, ax.y / dt, ax.z / dt};
+    }
+    cr[4] = dv.x; cr[5] = dv.y; cr[6] = dv.z; cr[7] = 0.f;
+}
+
+// np.gradient along frames of one clip (edge_order 1), divided by dt
+HE_DEV f3 grad_at(const IngestArgs& a, int64_t s, int64_t n, int64_t j, int b, float dt) {
+    auto P = [&](int64_t k) {
+        const float* h = a.hot + ((size_t)k * NB + b) * HOT;
+        return f3{h[0], h[1], h[2]};
+    };
+    if (n < 2) return f3{0.f, 0.f, 0.f};
+    f3 d;
+    if (j == s) d = P(s + 1) - P(s);
+    else if (j == s + n - 1) d = P(j) - P(j - 1);
+    else d = (P(j + 1) - P(j - 1)) * 0.5f;
+    return f3{d.x / dt, d.y / dt, d.z / dt};
+}
+
+__global__ void __launch_bounds__(256) filter_kernel(IngestArgs a) {
+    const int lane = threadIdx.x & (GROUP - 1);
+    const int64_t f = (int64_t)blockIdx.x * (blockDim.x / GROUP) + threadIdx.x / GROUP;
+    if (f >= a.F || lane >= NB) return;
+    const int b = lane;
+    const int c = clip_of(a.starts, a.num_clips, f);
+    const int64_t s = a.starts[c], n = a.nframes[c];
+    const float dt = a.dt[c];
+    f3 v = f3{0.f, 0.f, 0.f}, w = f3{0.f, 0.f, 0.f};
+    for (int k = -RADIUS; k <= RADIUS; ++k) {
+        int64_t j = f + k;
+        j = j < s ? s : (j > s + n - 1 ? s + n - 1 : j);  // mode "nearest" within the clip
+        const float wk = a.gauss[k + RADIUS];
+        v = v + grad_at(a, s, n, j, b, dt) * wk;
+        const float* r = a.gav_raw + ((size_t)j * NB + b) * 3;
+        w = w + f3{r[0], r[1], r[2]} * wk;
+    }
+    float* h = a.hot + ((size_t)f * NB + b) * HOT;
+    h[7] = v.x; h[8] = v.y; h[9] = v.z;
+    h[10] = w.x; h[11] = w.y; h[12] = w.z;
+}
+
+}  // namespace
+
+hipError_t launch_ingest(const float* pose, const float* trans, const int32_t* parents, const float* local_pos,
+                         const int64_t* starts, const int64_t* nframes, const float* dt, int num_clips, int64_t F,
+                         float* hot, float* cold, float* gav_raw, hipStream_t stream) {
+    IngestArgs a{pose, trans, parents, local_pos, starts, nframes, dt, num_clips, F, hot, cold, gav_raw, {}};
+    // normalised Gaussian taps (scipy: exp(-0.5 x^2 / sigma^2) / sum), computed in double
+    double w[2 * RADIUS + 1], sum = 0.0;
+    for (int k = -RADIUS; k <= RADIUS; ++k) sum += (w[k + RADIUS] = exp(-0.5 * k * k / 4.0));
+    for (int k = 0; k < 2 * RADIUS + 1; ++k) a.gauss[k] = (float)(w[k] / sum);
+    const int per_block = 256 / GROUP;
+    const unsigned grid = (unsigned)((F + per_block - 1) / per_block);
+    frame_kernel<<<grid, 256, 0, stream>>>(a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    filter_kernel<<<grid, 256, 0, stream>>>(a);
+    return hipGetLastError();
+}

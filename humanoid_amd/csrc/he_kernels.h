@@ -82,3 +82,6 @@ struct PhysArgs {
 hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream);
 hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream);
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);
+hipError_t launch_ingest(const float* pose, const float* trans, const int32_t* parents, const float* local_pos,
+                         const int64_t* starts, const int64_t* nframes, const float* dt, int num_clips, int64_t F,
+                         float* hot, float* cold, float* gav_raw, hipStream_t stream);

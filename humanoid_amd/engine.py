@@ -30,7 +30,7 @@ HE_SYMBOLS = (
     "he_get_buffer", "he_set_dof_targets", "he_set_root_state_indexed", "he_set_dof_state_indexed",
     "he_set_dof_targets_indexed", "he_set_env_properties", "he_simulate", "he_set_pd_params", "he_step_actions",
     "he_refresh", "he_load_motions", "he_imitation_step", "he_motion_state", "he_reset_envs", "he_env_step",
-    "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform",
+    "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips",
 )
 
 
@@ -55,6 +55,7 @@ def load_library(path: Optional[str] = None):
         "he_simulate": [V, I, V], "he_set_pd_params": [V, V, V, V, I], "he_step_actions": [V, V, I, V],
         "he_refresh": [V, V],
         "he_load_motions": [V, C.c_int64, I, V, V, V, V, V, V, V, V, V, V],
+        "he_ingest_clips": [V, I, V, V, V, V, I, V, V],
         "he_imitation_step": [V, V, V, V, V, V, V, V, V],
         "he_motion_state": [V, I, V, V, V, V, V, V, V, V, V, V],
         "he_reset_envs": [V, V, V, V, I, V, V, V, V, V],
@@ -254,6 +255,30 @@ class Engine:
         _check(self.lib.he_load_motions(self.h, int(F), int(nf.shape[0]), *[a.ctypes.data_as(C.c_void_p) for a in arrs],
                                         starts.ctypes.data_as(C.c_void_p), nf.ctypes.data_as(C.c_void_p),
                                         lens.ctypes.data_as(C.c_void_p), dts.ctypes.data_as(C.c_void_p)))
+        self.has_motions = True
+
+    def ingest_clips(self, clips, motion_clip=None):
+        """Device-side motion ingestion (he_ingest_clips): ``clips`` are dicts with the .pkl
+        schema's ``pose_quat_global`` [T,24,4] and ``root_trans_offset`` [T,3] (+ ``fps``);
+        library motion i uses clip ``motion_clip[i]`` (default: one motion per clip)."""
+        import torch
+        nf = np.array([len(c["pose_quat_global"]) for c in clips], np.int64)
+        fps = np.array([float(c.get("fps", 30)) for c in clips], np.float32)
+        pose = torch.as_tensor(np.concatenate([np.asarray(c["pose_quat_global"], np.float32) for c in clips], 0))
+        trans = torch.as_tensor(np.concatenate([np.asarray(c["root_trans_offset"], np.float32).reshape(-1, 3)
+                                                for c in clips], 0))
+        pose = pose.to(self.device).contiguous()
+        trans = trans.to(self.device).contiguous()
+        if pose.shape[1:] != (24, 4) or trans.shape[0] != pose.shape[0]:
+            raise EngineError(f"clip arrays have shapes {tuple(pose.shape)} / {tuple(trans.shape)}")
+        mc = None
+        m = len(clips)
+        if motion_clip is not None:
+            mc = np.ascontiguousarray(motion_clip, np.int32)
+            m = int(mc.shape[0])
+        _check(self.lib.he_ingest_clips(self.h, len(clips), nf.ctypes.data_as(C.c_void_p), fps.ctypes.data_as(C.c_void_p),
+                                        C.c_void_p(pose.data_ptr()), C.c_void_p(trans.data_ptr()), m,
+                                        None if mc is None else mc.ctypes.data_as(C.c_void_p), self.stream))
         self.has_motions = True
 
     def motion_state(self, ids, times, offset=None, want_dof=True):

@@ -198,9 +198,9 @@ class HumanoidPHC:
         self._update_params()
 
     def _load(self, **kw):
-        n = self.cfg.num_envs
-        tables = self._motion_lib.load_motions(n, **kw)
-        self.engine.load_motions(tables)
+        # sampling on the host (motion_lib.py:305-345), ingestion on the device (he_ingest_clips)
+        clips, motion_clip = self._motion_lib.select_motions(self.cfg.num_envs, **kw)
+        self.engine.ingest_clips(clips, motion_clip)
 
     # -- reset / step (:90-172) ----------------------------------------------------------
     def _reset_envs(self, env_ids):

@@ -164,8 +164,9 @@ class MotionLibSMPL:
         self._gen = None if seed is None else torch.Generator(device=device).manual_seed(seed)
 
     # -- loading (motion_lib.py:257-429) -------------------------------------------------
-    def load_motions(self, num_motion_to_load: int, random_sample=True, start_idx=0,
-                     sample_idxes=None) -> MotionTables:
+    def select_motions(self, num_motion_to_load: int, random_sample=True, start_idx=0, sample_idxes=None):
+        """Motion sampling of ``load_motions`` (motion_lib.py:305-345) without building tables:
+        returns (unique clip dicts, per-motion index into them) and sets the per-motion metadata."""
         import torch
         if sample_idxes is None or len(sample_idxes) != num_motion_to_load:
             if not self.is_deterministic and random_sample:
@@ -177,27 +178,39 @@ class MotionLibSMPL:
         sample_idxes = torch.as_tensor(sample_idxes).to(self._device)
         self._curr_motion_ids = sample_idxes
         self.curr_motion_keys = self._motion_data_keys[sample_idxes.cpu().numpy()]
-        # unique clips are ingested once and shared by all envs that sampled them
         idx = sample_idxes.cpu().numpy()
         uniq, inv = np.unique(idx, return_inverse=True)
-        base = build_tables(self.model, [self._motion_data_list[i] for i in uniq])
+        clips = [self._motion_data_list[i] for i in uniq]
+        nf = np.array([len(c["pose_quat_global"]) for c in clips], np.int64)[inv]
+        fps = np.array([int(c.get("fps", 30)) for c in clips], np.int64)[inv]
+        # motion_lib.py:376-379 (python floats -> float32)
+        lengths = np.array([1.0 / int(f) * (int(k) - 1) for f, k in zip(fps, nf)], np.float32)
+        self._motion_lengths = torch.as_tensor(lengths, device=self._device)
+        self._motion_num_frames = torch.as_tensor(nf, device=self._device)
+        self._motion_fps = torch.as_tensor(fps.astype(np.float32), device=self._device)
+        self._motion_dt = torch.as_tensor(np.array([1.0 / int(f) for f in fps], np.float32), device=self._device)
+        self._num_loaded = int(num_motion_to_load)
+        return clips, inv.astype(np.int32)
+
+    def load_motions(self, num_motion_to_load: int, random_sample=True, start_idx=0,
+                     sample_idxes=None) -> MotionTables:
+        """Host ingestion (the checker for the engine's he_ingest_clips): sample + build tables."""
+        clips, inv = self.select_motions(num_motion_to_load, random_sample, start_idx, sample_idxes)
+        # unique clips are ingested once and shared by all envs that sampled them
+        base = build_tables(self.model, clips)
         # per-env motion entries point into the unique-clip tables (same values as the
         # reference's per-env copies, ``motion_lib.py:407-419``, without duplicating frames)
         self.tables = MotionTables(
             gts=base.gts, grs=base.grs, lrs=base.lrs, gvs=base.gvs, gavs=base.gavs, dvs=base.dvs,
             num_frames=base.num_frames[inv], length_starts=base.length_starts[inv],
             lengths=base.lengths[inv], dt=base.dt[inv], fps=base.fps[inv])
-        self._motion_lengths = torch.as_tensor(self.tables.lengths, device=self._device)
-        self._motion_num_frames = torch.as_tensor(self.tables.num_frames, device=self._device)
-        self._motion_fps = torch.as_tensor(self.tables.fps, device=self._device)
-        self._motion_dt = torch.as_tensor(self.tables.dt, device=self._device)
         return self.tables
 
     def num_motions(self) -> int:
-        return self.tables.num_motions
+        return self._num_loaded
 
     def get_total_length(self) -> float:
-        return float(self.tables.lengths.sum())
+        return float(self._motion_lengths.sum())
 
     # -- sampling weights (motion_lib.py:454-500) -----------------------------------------
     def update_hard_sampling_weight(self, failed_keys):

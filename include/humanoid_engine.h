@@ -159,6 +159,19 @@ int he_load_motions(he_engine* h, int64_t num_frames_total, int num_motions,
                     const float* gavs, const float* dvs, const int64_t* length_starts,
                     const int64_t* num_frames, const float* lengths, const float* dt);
 
+/* Device-side motion ingestion: replaces the host MotionLibSMPL.load_motions
+ * path (motion_lib.py:257-429, 743-824 with poselib_skeleton.py:518-539, 574-592, 1166-1251 and
+ * compute_motion_dof_vels_jit motion_lib.py:119-140). Clips are concatenated along frames:
+ * pose_quat_global [F,24,4] xyzw and root_trans [F,3] (the .pkl schema's pose_quat_global /
+ * root_trans_offset), DEVICE pointers; host_num_frames / host_fps [num_clips] HOST arrays. Builds
+ * the motion tables on the device (local rotations, FK translations, Gaussian-filtered linear and
+ * angular velocities, dof velocities). Motion i of the library refers to clip
+ * host_motion_clip[i] (HOST, [num_motions]; NULL = identity with num_motions = num_clips), as the
+ * reference's per-env motion entries share clips. Synchronises `stream`. */
+int he_ingest_clips(he_engine* h, int num_clips, const int64_t* host_num_frames, const float* host_fps,
+                    const float* pose_quat_global, const float* root_trans, int num_motions,
+                    const int32_t* host_motion_clip, void* stream);
+
 /* Per-env motion bookkeeping buffers (device, caller-owned, all [N] unless noted):
  * motion_ids i64, start_times f32, start_offsets f32, global_offset f32 [N,3], progress i16. */
 typedef struct he_env_motion {
