@@ -79,11 +79,14 @@ __device__ __forceinline__ void read_row(const RegMat& M, float (&hk)[kMaxChain]
     }
 }
 
-// eliminate dof K (deepest first); the pivot D_K is kept on its owning lane (Dl / D2). The pivot
-// reciprocal and the row entries H[K][I] are wave-uniform (SGPRs), so each update is one FMA.
-template <int K>
-__device__ __forceinline__ void factor(RegMat& M, float& Dl, float& D2, int lane) {
-    if constexpr (K >= 0) {
+// elimination step S eliminates dof kElimOrder[S] (deepest first, so consecutive steps mostly lie
+// on independent branches and can overlap; a scheduling barrier every two steps bounds the live
+// SGPR/VGPR ranges). The pivot D_K is kept on its owning lane (Dl / D2); the pivot reciprocal and
+// the row entries H[K][I] are wave-uniform (SGPRs), so each update is one FMA.
+template <int S>
+__device__ __forceinline__ void factor_steps(RegMat& M, float& Dl, float& D2) {
+    if constexpr (S < NG) {
+        constexpr int K = kElimOrder[S];
         constexpr int D = kDofNanc[K] - 1;
         const float dk = get<K, K>(M);
         const float inv = uniform(__builtin_amdgcn_rcpf(dk));  // v_rcp_f32 (1 ulp): short pivot chain
@@ -94,9 +97,13 @@ __device__ __forceinline__ void factor(RegMat& M, float& Dl, float& D2, int lane
         fac_anc<K, 0, D>(M, hk);
         if constexpr (K < 64) Dl = wrlane<K>(dk, Dl);
         else D2 = wrlane<K - 64>(dk, D2);
-        __builtin_amdgcn_sched_barrier(0);  // one elimination step at a time: bounded SGPR/VGPR live ranges
-        factor<K - 1>(M, Dl, D2, lane);
+        if constexpr (S % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+        factor_steps<S + 1>(M, Dl, D2);
     }
+}
+template <int K>
+__device__ __forceinline__ void factor(RegMat& M, float& Dl, float& D2, int) {
+    factor_steps<0>(M, Dl, D2);
 }
 
 // ---------------------------------------------------------------- y <- L^-T y (y distributed: lane i holds y[i], y2 = y[64+i])
@@ -224,10 +231,12 @@ __device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG], uint32_t lb
 // ancestor K in any chain through it is its depth, a compile-time constant, so each step is one
 // v_readlane of y_K plus a masked FMA -- no cross-lane reduction.
 constexpr int kRowRegs = 32;
-template <int K>
+template <int S>
 __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs], float& yl,
                                              float& y2) {
-    if constexpr (K < NG) {
+    // sources in increasing depth (elimination order reversed): y_K is final once its ancestors ran
+    if constexpr (S >= 0) {
+        constexpr int K = kElimOrder[S];
         constexpr int d = kDofNanc[K] - 1 < kRowRegs ? kDofNanc[K] - 1 : 0;
         constexpr uint64_t lo = kDescLo[K];
         constexpr uint64_t hi = kDescHi[K];
@@ -236,24 +245,28 @@ __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const 
             if constexpr (lo != 0) yl = lanes<lo>() ? yl - r1[d] * yk : yl;
             if constexpr (hi != 0) y2 = lanes<hi>() ? y2 - r2[d] * yk : y2;
         }
-        solve_L_rows<K + 1>(r1, r2, yl, y2);
+        solve_L_rows<S - 1>(r1, r2, yl, y2);
     }
 }
 
 // ---------------------------------------------------------------- y <- L^-T y, column-distributed
 // lane j gathers L[K][j] = Lp[kPackStart[K] + depth(j)] for every descendant K (masked by the
 // compile-time ancestor sets) and updates its own y_j; y_K travels by v_readlane
-template <int K>
+template <int S>
 __device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, float& yl, float& y2, int lane) {
-    if constexpr (K >= 1) {
-        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-        if (lanes<lo>()) yl -= Lp[kPackStart[K] + dj] * yk;
-        if constexpr (K > 64) {
-            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-            if (lanes<hi>()) y2 -= Lp[kPackStart[K] + dj2] * yk;
+    // sources deepest first (elimination order): y_K is final once its descendants ran
+    if constexpr (S < NG) {
+        constexpr int K = kElimOrder[S];
+        if constexpr (K >= 1) {
+            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
+            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+            if (lanes<lo>()) yl -= Lp[kPackStart[K] + dj] * yk;
+            if constexpr (K > 64) {
+                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+                if (lanes<hi>()) y2 -= Lp[kPackStart[K] + dj2] * yk;
+            }
         }
-        solve_LT_cols<K - 1>(Lp, dj, dj2, yl, y2, lane);
+        solve_LT_cols<S + 1>(Lp, dj, dj2, yl, y2, lane);
     }
 }
 
