@@ -224,8 +224,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # HE_BENCH_SHARED_DEVICE=1 (rehearsal only): every rank on cuda:0 with gloo collectives, to
+    # exercise the multi-rank path on a one-GPU box; the real run is one rank per GPU over RCCL
+    shared = os.environ.get("HE_BENCH_SHARED_DEVICE") == "1"
+    if shared:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     model = load_default_model()
     ro = Rollout(args, model, local, rank)
@@ -250,7 +258,7 @@ def main():
     phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda")
+        t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     n = args.num_envs
