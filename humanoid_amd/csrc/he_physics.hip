@@ -394,7 +394,7 @@ template <class LdsT>
 HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
     using namespace regla;
     const int dj = smpl::kDofNanc[lane] - 1, dj2 = lane < NH ? smpl::kDofNanc[64 + lane] - 1 : 0;
-    solve_LT_cols<0>(L.Lp, dj, dj2, yl, y2, lane);
+    solve_LT_cols<smpl::kNumLevels - 1>(L.Lp, dj, dj2, yl, y2, lane);
     yl *= L.Dinv[lane];
     if (lane < NH) y2 *= L.Dinv[64 + lane];
     float r1[kRowRegs], r2[kRowRegs];
@@ -406,7 +406,7 @@ HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
         r1[4 * q] = v1.x; r1[4 * q + 1] = v1.y; r1[4 * q + 2] = v1.z; r1[4 * q + 3] = v1.w;
         r2[4 * q] = v2.x; r2[4 * q + 1] = v2.y; r2[4 * q + 2] = v2.z; r2[4 * q + 3] = v2.w;
     }
-    solve_L_rows<NG - 1>(r1, r2, yl, y2);
+    solve_L_rows<0>(r1, r2, yl, y2);
 }
 
 // ---------------------------------------------------------------------------------- kinematics

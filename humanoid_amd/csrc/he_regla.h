@@ -47,7 +47,12 @@ __device__ __forceinline__ float get(const RegMat& M) {
 // per-lane compare or branch)
 template <uint64_t C>
 __device__ __forceinline__ bool lanes() {
-    return __builtin_amdgcn_inverse_ballot_w64(C);
+    // the constant is materialised here by two s_mov_b32 (volatile: never hoisted out of the
+    // substep loop, where dozens of distinct masks would otherwise be kept live and spilled)
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)C));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(C >> 32)));
+    return __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -231,43 +236,97 @@ __device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG], uint32_t lb
 // ancestor K in any chain through it is its depth, a compile-time constant, so each step is one
 // v_readlane of y_K plus a masked FMA -- no cross-lane reduction.
 constexpr int kRowRegs = 32;
-template <int S>
+
+// union over a depth level of the (disjoint) descendant lane sets
+template <int D, int J = kLevelStart[D]>
+constexpr uint64_t level_desc_lo() {
+    if constexpr (J < kLevelStart[D + 1]) return kDescLo[kLevelDofs[J]] | level_desc_lo<D, J + 1>();
+    else return 0ull;
+}
+template <int D, int J = kLevelStart[D]>
+constexpr uint64_t level_desc_hi() {
+    if constexpr (J < kLevelStart[D + 1]) return kDescHi[kLevelDofs[J]] | level_desc_hi<D, J + 1>();
+    else return 0ull;
+}
+// per level: every descendant lane picks the y of its (unique) ancestor at this depth
+template <int D, int J>
+__device__ __forceinline__ void level_pick(float yl, float y2, float& t1, float& t2) {
+    if constexpr (J < kLevelStart[D + 1]) {
+        constexpr int K = kLevelDofs[J];
+        if constexpr (kDescLo[K] != 0 || kDescHi[K] != 0) {
+            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
+            if constexpr (kDescLo[K] != 0) t1 = lanes<kDescLo[K]>() ? yk : t1;
+            if constexpr (kDescHi[K] != 0) t2 = lanes<(uint64_t)kDescHi[K]>() ? yk : t2;
+        }
+        level_pick<D, J + 1>(yl, y2, t1, t2);
+    }
+}
+// y <- L^-1 y by depth levels, shallowest first: the dofs of one level have disjoint descendant
+// sets, so a level is n readlanes + n selects + ONE fma with the row entry at that depth
+template <int D>
 __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs], float& yl,
                                              float& y2) {
-    // sources in increasing depth (elimination order reversed): y_K is final once its ancestors ran
-    if constexpr (S >= 0) {
-        constexpr int K = kElimOrder[S];
-        constexpr int d = kDofNanc[K] - 1 < kRowRegs ? kDofNanc[K] - 1 : 0;
-        constexpr uint64_t lo = kDescLo[K];
-        constexpr uint64_t hi = kDescHi[K];
-        if constexpr (lo != 0 || hi != 0) {
-            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-            if constexpr (lo != 0) yl = lanes<lo>() ? yl - r1[d] * yk : yl;
-            if constexpr (hi != 0) y2 = lanes<hi>() ? y2 - r2[d] * yk : y2;
+    if constexpr (D < kNumLevels - 1) {
+        constexpr uint64_t ulo = level_desc_lo<D>();
+        constexpr uint64_t uhi = level_desc_hi<D>();
+        if constexpr (ulo != 0 || uhi != 0) {
+            float t1 = 0.f, t2 = 0.f;
+            level_pick<D, kLevelStart[D]>(yl, y2, t1, t2);
+            if constexpr (ulo != 0) yl = lanes<ulo>() ? yl - r1[D] * t1 : yl;
+            if constexpr (uhi != 0) y2 = lanes<uhi>() ? y2 - r2[D] * t2 : y2;
         }
-        solve_L_rows<S - 1>(r1, r2, yl, y2);
+        solve_L_rows<D + 1>(r1, r2, yl, y2);
     }
 }
 
 // ---------------------------------------------------------------- y <- L^-T y, column-distributed
-// lane j gathers L[K][j] = Lp[kPackStart[K] + depth(j)] for every descendant K (masked by the
-// compile-time ancestor sets) and updates its own y_j; y_K travels by v_readlane
-template <int S>
-__device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, float& yl, float& y2, int lane) {
-    // sources deepest first (elimination order): y_K is final once its descendants ran
-    if constexpr (S < NG) {
-        constexpr int K = kElimOrder[S];
+// by depth levels, deepest first. Lane j first gathers its whole column of L (g1[K] = L[K][j] =
+// Lp[kPackStart[K] + depth(j)], 75 independent LDS reads issued back to back; entries of non-
+// descendants are never selected), then each level is n readlanes of the final y_K plus n masked
+// FMAs into an accumulator and one subtraction.
+template <int K>
+__device__ __forceinline__ void gather_cols(const float* Lp, int dj, int dj2, float (&g1)[NG], float (&g2)[NG - 64]) {
+    if constexpr (K < NG) {
+        if constexpr (K >= 1) g1[K] = Lp[kPackStart[K] + dj];
+        if constexpr (K > 64) g2[K - 64] = Lp[kPackStart[K] + dj2];
+        gather_cols<K + 1>(Lp, dj, dj2, g1, g2);
+    }
+}
+template <int D, int J>
+__device__ __forceinline__ void level_push(const float (&g1)[NG], const float (&g2)[NG - 64], float yl, float y2,
+                                           float& t1, float& t2) {
+    if constexpr (J < kLevelStart[D + 1]) {
+        constexpr int K = kLevelDofs[J];
         if constexpr (K >= 1) {
             const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
             constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-            if (lanes<lo>()) yl -= Lp[kPackStart[K] + dj] * yk;
+            t1 = lanes<lo>() ? fmaf(g1[K], yk, t1) : t1;
             if constexpr (K > 64) {
                 constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-                if (lanes<hi>()) y2 -= Lp[kPackStart[K] + dj2] * yk;
+                t2 = lanes<hi>() ? fmaf(g2[K - 64], yk, t2) : t2;
             }
         }
-        solve_LT_cols<S + 1>(Lp, dj, dj2, yl, y2, lane);
+        level_push<D, J + 1>(g1, g2, yl, y2, t1, t2);
     }
+}
+template <int D>
+__device__ __forceinline__ void solve_LT_levels(const float (&g1)[NG], const float (&g2)[NG - 64], float& yl,
+                                                float& y2) {
+    if constexpr (D >= 1) {
+        float t1 = 0.f, t2 = 0.f;
+        level_push<D, kLevelStart[D]>(g1, g2, yl, y2, t1, t2);
+        yl -= t1;
+        y2 -= t2;
+        solve_LT_levels<D - 1>(g1, g2, yl, y2);
+    }
+}
+template <int D>
+__device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, float& yl, float& y2, int) {
+    float g1[NG], g2[NG - 64];
+    g1[0] = 0.f;
+    g2[0] = 0.f;
+    gather_cols<0>(Lp, dj, dj2, g1, g2);
+    solve_LT_levels<D>(g1, g2, yl, y2);
 }
 
 }  // namespace regla
