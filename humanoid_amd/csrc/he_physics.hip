@@ -267,21 +267,21 @@ template <int R>
 HE_DEV void pgs_friction(float& w, float& lamv, const float (&acol)[MAXR], float invd, float bnd) {
     const float nt = fminf(fmaxf(lamv - w * invd, -bnd), bnd);
     const float d = regla::rdlane(nt - lamv, R);
-    lamv = regla::lanes<1ull << R>() ? nt : lamv;
+    lamv = regla::wrlane<R>(regla::rdlane(nt, R), lamv);  // lane R only, no lane mask
     w = fmaf(acol[R], d, w);
 }
 
 template <int CI>
 HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float invd, int nc, const float* cmu,
                       int lane) {
-    using regla::lanes;
     if constexpr (CI < MAXC) {
         if (CI >= nc) return;
         constexpr int R0 = 3 * CI;
         float nl = fmaxf(lamv - w * invd, 0.f);
         const float dn = regla::rdlane(nl - lamv, R0);
-        const float bnd = cmu[CI] * regla::rdlane(nl, R0);
-        lamv = lanes<1ull << R0>() ? nl : lamv;
+        const float ln = regla::rdlane(nl, R0);
+        const float bnd = cmu[CI] * ln;
+        lamv = regla::wrlane<R0>(ln, lamv);
         w = fmaf(acol[R0], dn, w);
         pgs_friction<R0 + 1>(w, lamv, acol, invd, bnd);
         pgs_friction<R0 + 2>(w, lamv, acol, invd, bnd);
