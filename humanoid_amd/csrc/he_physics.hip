@@ -226,9 +226,52 @@ HE_DEV const T* opaque(const T* p) {  // same address through an opaque offset: 
 HE_DEV void fmul_ordered(float& z, float a) { asm volatile("v_mul_f32 %0, %0, %1" : "+v"(z) : "v"(a)); }
 HE_DEV void ffma_ordered(float& acc, float a, float b) { asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "v"(a), "v"(b)); }
 
+// Delassus operator on the matrix cores: A = Zh Zh^T as four 32x32 tiles of
+// v_mfma_f32_32x32x2_f32 (exact f32, k-ordered fma chain), K = live dofs two at a time. Lane r
+// holds row r of Zh; one v_permlane32_swap per dof pair turns (z[k], z[k+1]) into the A/B operand
+// of rows 0-31 (p0) and of rows 32-63 (p1). A second round of swaps moves the C tiles
+// (col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5)) into "lane c holds column c".
+constexpr int NGRP = (NG + 3) / 4;  // dof groups of four
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+HE_DEV void swap32(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+HE_DEV void delassus_mfma(const float (&z)[NG], float (&acol)[MAXR], uint32_t live) {
+    f32x16 t00 = {}, t01 = {}, t10 = {}, t11 = {};
+#pragma unroll
+    for (int g = 0; g < NGRP; ++g) {
+        if ((live >> g) & 1u) {
+#pragma unroll
+            for (int h = 0; h < 4; h += 2) {
+                const int k0 = 4 * g + h;
+                if (k0 < NG) {
+                    float p0 = z[k0], p1 = k0 + 1 < NG ? z[k0 + 1 < NG ? k0 + 1 : 0] : 0.f;
+                    swap32(p0, p1);
+                    t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(p0, p0, t00, 0, 0, 0);
+                    t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(p0, p1, t01, 0, 0, 0);
+                    t10 = __builtin_amdgcn_mfma_f32_32x32x2f32(p1, p0, t10, 0, 0, 0);
+                    t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(p1, p1, t11, 0, 0, 0);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int r = (v & 3) + 8 * (v >> 2);
+        float a = t00[v], b = t01[v], c = t10[v], d = t11[v];
+        swap32(a, b);  // a: A[r][lane], b: A[r + 4][lane]
+        swap32(c, d);  // c: A[32 + r][lane], d: A[36 + r][lane]
+        acol[r] = a;
+        acol[r + 4] = b;
+        if (32 + r < MAXR) acol[32 + r < MAXR ? 32 + r : 0] = c;
+        if (36 + r < MAXR) acol[36 + r < MAXR ? 36 + r : 0] = d;
+    }
+}
+
 // Delassus column entries A[RR][lane] for RR < nr, one row per step (constant register indices);
 // dof groups without a nonzero entry in any row are skipped
-constexpr int NGRP = (NG + 3) / 4;
 template <int RR>
 HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uint32_t live) {
     // four rows at a time: four independent accumulation chains, and each v_readlane has three
@@ -784,7 +827,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 if (lb & kGroupBodies[g]) live |= 1u << g;
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
-            delassus_rows<0>(z, acol, nr, live);
+            delassus_mfma(z, acol, live);
         }
         STAMP(9);
         // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
@@ -880,7 +923,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     STAMP(12);
 }
 
-__global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) physics_kernel(PhysArgs a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
     const int e = blockIdx.x;
