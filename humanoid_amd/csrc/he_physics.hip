@@ -452,6 +452,40 @@ HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
     solve_L_rows<0>(r1, r2, yl, y2);
 }
 
+// In-place subtree sums X[b] += sum over children of X[c], parents of the deepest level first: at
+// each level, lane (parent, component) pulls its (at most three) children's finished sums. The
+// levels are unrolled at compile time, so parents and children are immediates selected by lane
+// range. NC = 16 sums forces (6, stride 6) and inertias (10, stride 10) together; NC = 6 forces only.
+template <int NC, int J, int END>
+HE_DEV void subtree_parent(float* F, float* I, int lane, int j0) {
+    if constexpr (J < END) {
+        constexpr int p = smpl::kParentLevelBodies[J];
+        const int base = (J - j0) * NC;
+        if (lane >= base && lane < base + NC) {
+            const int x = lane - base;
+            float* X = x < 6 ? F : I;
+            const int st = x < 6 ? 6 : 10, xx = x < 6 ? x : x - 6;
+            float v = X[p * st + xx];
+            if constexpr (smpl::kChildren[p][0] >= 0) v += X[smpl::kChildren[p][0] * st + xx];
+            if constexpr (smpl::kChildren[p][1] >= 0) v += X[smpl::kChildren[p][1] * st + xx];
+            if constexpr (smpl::kChildren[p][2] >= 0) v += X[smpl::kChildren[p][2] * st + xx];
+            X[p * st + xx] = v;
+        }
+        subtree_parent<NC, J + 1, END>(F, I, lane, j0);
+    }
+}
+template <int NC, int D>
+HE_DEV void subtree_levels(float* F, float* I, int lane) {
+    if constexpr (D >= 0) {
+        constexpr int j0 = smpl::kParentLevelStart[D], j1 = smpl::kParentLevelStart[D + 1];
+        if constexpr (j1 > j0) {
+            subtree_parent<NC, j0, j1>(F, I, lane, j0);
+            sync();
+        }
+        subtree_levels<NC, D - 1>(F, I, lane);
+    }
+}
+
 // ---------------------------------------------------------------------------------- kinematics
 HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
     const BodyTopo& T = L.T;
@@ -558,7 +592,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             for (int c = 0; c < 3; ++c)
                 I[r][c] = (T1[r][0] * R[c][0] + T1[r][1] * R[c][1] + T1[r][2] * R[c][2]) * ms +
                           mass * ((r == c ? ss : 0.f) - sv[r] * sv[c]);
-        float* o10 = L.Ib[b];
+        float* o10 = L.Ic[b];  // own inertia; the subtree sums accumulate in place
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
         float Acc[6];
@@ -580,23 +614,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         si_apply(o10, Acc, IA);
         si_apply(o10, L.V[b], IV);
         crf(L.V[b], IV, X);
-        for (int x = 0; x < 6; ++x) L.Acc[b][x] = IA[x] + X[x];  // body force f_b
+        for (int x = 0; x < 6; ++x) L.F[b][x] = IA[x] + X[x];  // body force f_b (accumulated in place)
     }
     sync();
     STAMP(1);
-    // ---- subtree sums: F_b (forces) and composite inertias
-    if (lane < NB) {
-        uint32_t sm = T.sub_mask[lane];
-        float Fs[6] = {0, 0, 0, 0, 0, 0}, Ics[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int d = 0; d < NB; ++d)
-            if (sm >> d & 1u) {
-                for (int x = 0; x < 6; ++x) Fs[x] += L.Acc[d][x];
-                for (int x = 0; x < 10; ++x) Ics[x] += L.Ib[d][x];
-            }
-        for (int x = 0; x < 6; ++x) L.F[lane][x] = Fs[x];
-        for (int x = 0; x < 10; ++x) L.Ic[lane][x] = Ics[x];
-    }
-    sync();
+    // ---- subtree sums: F_b (forces) and composite inertias, in place by body levels
+    subtree_levels<16, smpl::kNumBodyLevels - 2>(&L.F[0][0], &L.Ic[0][0], lane);
     STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
     for (int i = lane; i < NG; i += W) {
@@ -861,21 +884,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                     for (int x = 0; x < 6; ++x) F6[x] += s * imp[c][x];
                 }
             }
-            for (int x = 0; x < 6; ++x) L.V[lane][x] = F6[x];
+            for (int x = 0; x < 6; ++x) L.F[lane][x] = F6[x];
             L.cf[lane][0] = F6[3] / dt; L.cf[lane][1] = F6[4] / dt; L.cf[lane][2] = F6[5] / dt;
         }
         sync();
-        if (lane < NB) {
-            const uint32_t sm = T.sub_mask[lane];
-            float Fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int d = 0; d < NB; ++d) {
-                const float s = (sm >> d) & 1u ? 1.f : 0.f;
-                for (int x = 0; x < 6; ++x) Fs[x] += s * L.V[d][x];
-            }
-            for (int x = 0; x < 6; ++x) L.F[lane][x] = Fs[x];
-        }
-        sync();
+        subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.F[0][0], nullptr, lane);
         // ---- du = L^-1 D^-1 L^-T (J^T lambda), generalized impulse tau_i = S_i . F_subtree(body(i))
         {
             float yl = dot6(L.S[lane], L.F[dof_body(lane)]);
