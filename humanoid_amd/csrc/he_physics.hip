@@ -45,6 +45,8 @@ struct BodyTopo {
     uint32_t anc_mask[NB];
     uint32_t sub_mask[NB];
     float local_pos[NB][3];  // joint offsets (model), read along every FK chain walk
+    int16_t pack_start[NG];  // packed-row offset of dof i (smpl::kPackStart)
+    int8_t dof_depth[NG];    // depth of dof i in the dof tree (smpl::kDofNanc - 1)
 };
 
 struct Lds {
@@ -436,13 +438,13 @@ HE_DEV void crba_groups(regla::RegMat& M, const float (&Sj)[6], const float (&Sj
 template <class LdsT>
 HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
     using namespace regla;
-    const int dj = smpl::kDofNanc[lane] - 1, dj2 = lane < NH ? smpl::kDofNanc[64 + lane] - 1 : 0;
+    const int dj = L.T.dof_depth[lane], dj2 = lane < NH ? L.T.dof_depth[64 + lane] : 0;
     solve_LT_cols<smpl::kNumLevels - 1>(L.Lp, dj, dj2, yl, y2, lane);
     yl *= L.Dinv[lane];
     if (lane < NH) y2 *= L.Dinv[64 + lane];
     float r1[kRowRegs], r2[kRowRegs];
-    const float4* p1 = reinterpret_cast<const float4*>(L.Lp + smpl::kPackStart[lane]);
-    const float4* p2 = reinterpret_cast<const float4*>(L.Lp + smpl::kPackStart[lane < NH ? 64 + lane : 0]);
+    const float4* p1 = reinterpret_cast<const float4*>(L.Lp + L.T.pack_start[lane]);
+    const float4* p2 = reinterpret_cast<const float4*>(L.Lp + L.T.pack_start[lane < NH ? 64 + lane : 0]);
 #pragma unroll
     for (int q = 0; q < kRowRegs / 4; ++q) {
         const float4 v1 = p1[q], v2 = p2[q];
@@ -665,8 +667,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
-        store_packed<NG - 1>(M, L.Lp, lane, smpl::kDofNanc[lane] - 1,
-                             lane < NH ? smpl::kDofNanc[64 + lane] - 1 : 0);
+        store_packed<NG - 1>(M, L.Lp, lane, L.T.dof_depth[lane],
+                             lane < NH ? L.T.dof_depth[64 + lane] : 0);
     }
     sync();
     STAMP(5);
@@ -951,6 +953,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         L.T.anc_mask[lane] = T.anc_mask[lane];
         L.T.sub_mask[lane] = T.sub_mask[lane];
         for (int c = 0; c < 3; ++c) L.T.local_pos[lane][c] = m.local_pos[lane][c];
+    }
+    for (int i = lane; i < NG; i += W) {  // per-dof tree tables (constant memory -> LDS once)
+        L.T.pack_start[i] = (int16_t)smpl::kPackStart[i];
+        L.T.dof_depth[i] = (int8_t)(smpl::kDofNanc[i] - 1);
     }
     // ---- load state
     const float* rs = a.root_states + (size_t)e * 13;
