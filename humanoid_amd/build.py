@@ -14,7 +14,7 @@ ARCH = os.environ.get("HE_OFFLOAD_ARCH", "gfx950")
 # reference's torch ops do (no FMA contraction); the physics kernel may contract.
 SOURCES = [
     ("he_imitation.hip", ["-ffp-contract=off"]),
-    ("he_physics.hip", []),
+    ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]),
     ("he_ingest.hip", []),
     ("he_engine.cpp", ["-x", "hip"]),
 ]

@@ -938,7 +938,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     STAMP(12);
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) physics_kernel(PhysArgs a) {
+__global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
     const int e = blockIdx.x;
