@@ -663,12 +663,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
     {
         float Dl = 1.f, D2 = 1.f;
-        factor<NG - 1>(M, Dl, D2, lane);
+        factor_lds_steps<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0);
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
-        store_packed<NG - 1>(M, L.Lp, lane, L.T.dof_depth[lane],
-                             lane < NH ? L.T.dof_depth[64 + lane] : 0);
     }
     sync();
     STAMP(5);

@@ -329,4 +329,48 @@ __device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, 
     solve_LT_levels<D>(g1, g2, yl, y2);
 }
 
+// ---------------------------------------------------------------- LTDL with LDS row broadcasts
+// As factor_steps, but row K of L leaves through LDS as soon as it is final (the packed store of
+// the factor, lanes in chain(K) write their entry) and comes back as 16-byte broadcasts: the
+// updates H[I][j] -= L[K][I] * H[K][j] then take both operands from VGPRs (one FMA, no v_readlane),
+// halving the VALU work of the elimination. Leaves Lp complete (no separate store_packed).
+template <int K, int X, int D>
+__device__ __forceinline__ void fac_anc_row(RegMat& M, const Row<D>& row, float t, float t2) {
+    if constexpr (X < D) {
+        constexpr int I = kChain[K][X];
+        const float4 v = row.v[X / 4];
+        const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
+        fnma(M.c[I], l, t);  // ordered: keeps the row's registers short-lived
+        if constexpr (I >= 64) fnma(M.c2[I - 64], l, t2);
+        fac_anc_row<K, X + 1, D>(M, row, t, t2);
+    }
+}
+template <int S>
+__device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2) {
+    if constexpr (S < NG) {
+        constexpr int K = kElimOrder[S];
+        constexpr int D = kDofNanc[K] - 1;
+        const float dk = get<K, K>(M);
+        const float inv = uniform(__builtin_amdgcn_rcpf(dk));
+        const float t = M.c[K];                        // H[K][j], unscaled
+        const float t2 = K >= 64 ? M.c2[K >= 64 ? K - 64 : 0] : 0.f;
+        M.c[K] = t * inv;                              // L[K][j] on lanes j < K
+        if constexpr (K >= 64) M.c2[K - 64] = t2 * inv;
+        if constexpr (D > 0) {
+            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+            if (lanes<lo>()) Lp[kPackStart[K] + dj] = M.c[K];
+            if constexpr (K > 64) {
+                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+                if (lanes<hi>()) Lp[kPackStart[K] + dj2] = M.c2[K - 64];
+            }
+            const auto row = load_row<K>(Lp, kPackStart[K]);  // in-order LDS: sees the writes above
+            fac_anc_row<K, 0, D>(M, row, t, t2);
+        }
+        if constexpr (K < 64) Dl = wrlane<K>(dk, Dl);
+        else D2 = wrlane<K - 64>(dk, D2);
+        __builtin_amdgcn_sched_barrier(0);
+        factor_lds_steps<S + 1>(M, Dl, D2, Lp, dj, dj2);
+    }
+}
+
 }  // namespace regla
