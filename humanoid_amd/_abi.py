@@ -131,3 +131,20 @@ def imitation_params(reward=None, control_dt=1.0 / 30.0, use_power_reward=True, 
     for b in range(NB):
         p.term_dist[b] = float(td[b])
     return p
+
+
+# include/humanoid_rollout.h
+ROLLOUT_MAX_FIELDS = 8
+ROLLOUT_F32 = 0
+ROLLOUT_U8 = 1
+
+
+class HeRolloutField(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("width", C.c_int32), ("src_kind", C.c_int32)]
+
+
+class HeRolloutIndex(C.Structure):
+    _fields_ = [("num_keys", C.c_int32), ("reserved", C.c_int32), ("capacity", C.c_int64),
+                ("scratch_rows", C.c_int64), ("key_count", C.c_void_p), ("key_last", C.c_void_p),
+                ("key_offset", C.c_void_p), ("row_env", C.c_void_p), ("row_rank", C.c_void_p),
+                ("scratch", C.c_void_p), ("status", C.c_void_p)]

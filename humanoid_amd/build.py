@@ -16,9 +16,11 @@ SOURCES = [
     ("he_imitation.hip", ["-ffp-contract=off"]),
     ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]),
     ("he_ingest.hip", []),
+    ("he_rollout.hip", ["-ffp-contract=off"]),  # GAE: the Cython module's float32 rounding
     ("he_engine.cpp", ["-x", "hip"]),
 ]
-HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", "he_regla.h", "he_smpl_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h")]
+HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", "he_regla.h", "he_smpl_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h"),
+           os.path.join("..", "..", "include", "humanoid_rollout.h")]
 
 
 def _hipcc():
@@ -43,13 +45,17 @@ def build(force=False, verbose=False):
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src + ".o")
         objs.append(o)
-        if force or _mtime(o) < max(_mtime(s), hdr_time):
-            cmd = [hipcc] + common + flags + ["-c", s, "-o", o]
+        cmd = [hipcc] + common + flags + ["-c", s, "-o", o]
+        stamp = o + ".cmd"  # a flag change rebuilds too
+        same_cmd = os.path.exists(stamp) and open(stamp).read() == " ".join(cmd)
+        if force or not same_cmd or _mtime(o) < max(_mtime(s), hdr_time):
             if verbose:
                 print(" ".join(cmd))
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+            with open(stamp, "w") as f:
+                f.write(" ".join(cmd))
             rebuilt = True
     if force or rebuilt or _mtime(LIB) < max(_mtime(o) for o in objs):
         cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs

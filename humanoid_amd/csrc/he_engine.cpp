@@ -29,6 +29,15 @@ int fail(const char* fmt, ...) {
     return 1;
 }
 
+}  // namespace
+
+// error text for the other C-ABI translation units (he_rollout.hip)
+int he_fail_text(const char* text) {
+    g_err = text;
+    return 1;
+}
+
+namespace {
 #define HE_CHECK(expr)                                                                         \
     do {                                                                                       \
         hipError_t _e = (expr);                                                                \

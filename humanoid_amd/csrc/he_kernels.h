@@ -6,6 +6,8 @@
 #include "../../include/humanoid_engine.h"
 #include "he_topo.h"
 
+int he_fail_text(const char* text);  // sets he_last_error(), returns 1
+
 #define HE_MOTION_HOT 13   // per body: pos3 rot4 vel3 angvel3 (same layout as a rigid-body row)
 #define HE_MOTION_COLD 8   // per body: local rot4, dof vel3, pad
 

@@ -31,6 +31,8 @@ HE_SYMBOLS = (
     "he_set_dof_targets_indexed", "he_set_env_properties", "he_simulate", "he_set_pd_params", "he_step_actions",
     "he_refresh", "he_load_motions", "he_imitation_step", "he_motion_state", "he_reset_envs", "he_env_step",
     "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips",
+    # include/humanoid_rollout.h
+    "he_rollout_store", "he_rollout_order", "he_rollout_gather", "he_gae", "he_gae_minibatch",
 )
 
 
@@ -63,6 +65,11 @@ def load_library(path: Optional[str] = None):
         "he_imitation_reset_step": [V, V, V, C.c_uint64, C.c_uint64, V, V, V, V, V, V],
         "he_device_count": [V],
         "he_set_debug_stamps": [V, V],
+        "he_rollout_store": [V, V, I, C.c_int64, V, V, C.c_int64, C.c_int32, V],
+        "he_rollout_order": [V, C.c_int64, V, I, V],
+        "he_rollout_gather": [V, I, V, C.c_int64, C.c_int32, C.c_int32, C.c_int32, V],
+        "he_gae": [V, V, V, C.c_int64, F, F, V, V],
+        "he_gae_minibatch": [V, V, V, V, V, C.c_int64, F, F, C.c_int32, C.c_int32, C.c_int32, V, V, V],
     }
     for name, args in sigs.items():
         fn = getattr(lib, name)

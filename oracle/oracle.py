@@ -167,3 +167,78 @@ def imitation_from_ref(params, pos, rot, vel, ang, rpos, rrot, rvel, rang, progr
                                 _p(np.ascontiguousarray(progress, np.int16)), _p(np.ascontiguousarray(pass_time, np.uint8)),
                                 *[_p(out[k]) for k in ("rew", "reward_raw", "reset", "terminate", "self_obs", "task_obs")])
     return out
+
+
+# ---------------------------------------------------------------- rollout handoff (he_oracle_rollout.c)
+def gae(dones, values, rewards, gamma, gae_lambda):
+    """c_gae.pyx:11-32 compute_gae restated in C (float32, the Cython operation order)."""
+    d, v, r = f32(dones).ravel(), f32(values).ravel(), f32(rewards).ravel()
+    n = r.size
+    out = np.zeros(n, np.float32)
+    lib().ho_gae(C.c_int64(n), _p(d), _p(v), _p(r), C.c_float(gamma), C.c_float(gae_lambda), _p(out))
+    return out
+
+
+def sort_keys(env_id, step):
+    """structs.py:128-129: sorted(range(n), key=(env_id, step)) (stable)."""
+    e = np.ascontiguousarray(env_id, np.int64)
+    s = np.ascontiguousarray(step, np.int64)
+    out = np.zeros(e.size, np.int64)
+    lib().ho_sort_keys(C.c_int64(e.size), _p(e), _p(s), _p(out))
+    return out
+
+
+class HostExperience:
+    """structs.py:22-179 Experience restated over NumPy (store / sort_training_data / flatten_batch) plus
+    the core.py:213-258 GAE block: the host checker for humanoid_amd.experience.Experience."""
+
+    def __init__(self, batch_size, bptt_horizon, num_minibatches, minibatch_rows, obs_dim, atn_dim):
+        self.batch_size, self.bptt, self.num_mb, self.rows = batch_size, bptt_horizon, num_minibatches, minibatch_rows
+        self.obs = np.zeros((batch_size, obs_dim), np.float32)
+        self.actions = np.zeros((batch_size, atn_dim), np.float32)
+        self.values, self.logprobs, self.rewards, self.dones, self.truncateds = (
+            np.zeros(batch_size, np.float32) for _ in range(5))
+        self.sort_keys = []
+        self.ptr = 0
+        self.step = 0
+
+    @property
+    def full(self):
+        return self.ptr >= self.batch_size
+
+    def store(self, obs, value, action, logprob, reward, done, trunc, env_id, mask):  # structs.py:108-126
+        ptr = self.ptr
+        indices = np.where(mask)[0][: self.batch_size - ptr]
+        end = ptr + len(indices)
+        self.obs[ptr:end] = obs[indices]
+        self.values[ptr:end] = value[indices]
+        self.actions[ptr:end] = action[indices]
+        self.logprobs[ptr:end] = logprob[indices]
+        self.rewards[ptr:end] = reward[indices]
+        self.dones[ptr:end] = done[indices]
+        self.truncateds[ptr:end] = trunc[indices]
+        self.sort_keys.extend([(env_id[i], self.step) for i in indices])
+        self.ptr = end
+        self.step += 1
+
+    def sort_training_data(self):  # structs.py:128-142
+        keys = np.array(self.sort_keys, np.int64).reshape(-1, 2)
+        idxs = sort_keys(keys[:, 0], keys[:, 1])
+        self.b_idxs = idxs.reshape(self.rows, self.num_mb, self.bptt).transpose(1, 0, 2)
+        self.b_flat = self.b_idxs.reshape(self.num_mb, -1)
+        self.sort_keys = []
+        return idxs
+
+    def flatten_batch(self):  # structs.py:144-160
+        b = self.b_idxs
+        self.b_obs, self.b_actions = self.obs[b], self.actions[b]
+        self.b_logprobs, self.b_dones, self.b_truncated = self.logprobs[b], self.dones[b], self.truncateds[b]
+        self.b_values = self.values[self.b_flat]
+
+    def compute_advantages(self, idxs, gamma, gae_lambda, extra=None):  # core.py:213-258
+        r = self.rewards[idxs] if extra is None else self.rewards[idxs] + f32(extra)
+        adv = gae(self.dones[idxs], self.values[idxs], r, gamma, gae_lambda)
+        self.b_advantages = adv.reshape(self.rows, self.num_mb, self.bptt).transpose(1, 0, 2).reshape(self.num_mb, -1)
+        self.b_returns = self.b_advantages + self.b_values
+        self.returns = adv + self.values
+        return adv

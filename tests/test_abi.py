@@ -13,7 +13,8 @@ HEADER = os.path.join(ROOT, "include", "humanoid_engine.h")
 
 
 def declared_symbols():
-    text = open(HEADER).read()
+    import glob
+    text = "".join(open(h).read() for h in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(he_[a-z_0-9]+)\s*\(", text)))
 
@@ -52,13 +53,16 @@ def test_errors_are_reported_without_gpu():
 def test_struct_sizes_match_header(tmp_path):
     from humanoid_amd import _abi
     src = tmp_path / "sz.c"
-    src.write_text('#include <stdio.h>\n#include "humanoid_engine.h"\nint main(){printf("%zu %zu %zu %zu\\n",'
-                   "sizeof(he_model),sizeof(he_sim_params),sizeof(he_imitation_params),sizeof(he_env_motion));}\n")
+    src.write_text('#include <stdio.h>\n#include "humanoid_engine.h"\n#include "humanoid_rollout.h"\n'
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu\\n",'
+                   "sizeof(he_model),sizeof(he_sim_params),sizeof(he_imitation_params),sizeof(he_env_motion),"
+                   "sizeof(he_rollout_field),sizeof(he_rollout_index));}\n")
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     assert [int(x) for x in out] == [C.sizeof(_abi.HeModel), C.sizeof(_abi.HeSimParams),
-                                     C.sizeof(_abi.HeImitationParams), C.sizeof(_abi.HeEnvMotion)]
+                                     C.sizeof(_abi.HeImitationParams), C.sizeof(_abi.HeEnvMotion),
+                                     C.sizeof(_abi.HeRolloutField), C.sizeof(_abi.HeRolloutIndex)]
 
 
 def test_model_blob(model):
