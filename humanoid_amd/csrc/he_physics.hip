@@ -307,30 +307,35 @@ HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uin
 // one Gauss-Seidel sweep over the contacts: normal row clamped at 0, friction rows to the pyramid
 // |lambda_t| <= mu lambda_n. Lane r holds w_r, lambda_r and 1/A[r][r], so each row's candidate
 // impulse is computed lane-parallel from VGPRs (only lane r's result is used); one v_readlane
-// carries the impulse change to the column update w += A[.][r] * d of every lane.
-template <int R>
-HE_DEV void pgs_friction(float& w, float& lamv, const float (&acol)[MAXR], float invd, float bnd) {
-    const float nt = fminf(fmaxf(lamv - w * invd, -bnd), bnd);
+// carries the impulse change d to the column update w += A[.][r] * d of every lane. muL: lane r
+// holds the friction coefficient of row r's contact (the bound is formed beside the candidate).
+template <int R, bool NORMAL>
+HE_DEV void pgs_row(float& w, float& lamv, const float (&acol)[MAXR], float invd, float muL, float& ln) {
+    const float c = fmaf(-w, invd, lamv);
+    float nt;
+    if constexpr (NORMAL) {
+        nt = fmaxf(c, 0.f);
+    } else {
+        const float bnd = muL * ln;
+        nt = __builtin_amdgcn_fmed3f(c, -bnd, bnd);
+    }
     const float d = regla::rdlane(nt - lamv, R);
-    lamv = regla::wrlane<R>(regla::rdlane(nt, R), lamv);  // lane R only, no lane mask
+    const float s = regla::rdlane(nt, R);
+    if constexpr (NORMAL) ln = s;
+    lamv = regla::wrlane<R>(s, lamv);  // lane R only, no lane mask
     w = fmaf(acol[R], d, w);
 }
 
 template <int CI>
-HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float invd, int nc, const float* cmu,
-                      int lane) {
+HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float invd, float muL, int nc) {
     if constexpr (CI < MAXC) {
         if (CI >= nc) return;
         constexpr int R0 = 3 * CI;
-        float nl = fmaxf(lamv - w * invd, 0.f);
-        const float dn = regla::rdlane(nl - lamv, R0);
-        const float ln = regla::rdlane(nl, R0);
-        const float bnd = cmu[CI] * ln;
-        lamv = regla::wrlane<R0>(ln, lamv);
-        w = fmaf(acol[R0], dn, w);
-        pgs_friction<R0 + 1>(w, lamv, acol, invd, bnd);
-        pgs_friction<R0 + 2>(w, lamv, acol, invd, bnd);
-        pgs_sweep<CI + 1>(w, lamv, acol, invd, nc, cmu, lane);
+        float ln = 0.f;
+        pgs_row<R0, true>(w, lamv, acol, invd, muL, ln);
+        pgs_row<R0 + 1, false>(w, lamv, acol, invd, muL, ln);
+        pgs_row<R0 + 2, false>(w, lamv, acol, invd, muL, ln);
+        pgs_sweep<CI + 1>(w, lamv, acol, invd, muL, nc);
     }
 }
 
@@ -857,7 +862,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         {
             float w = lane < nr ? brow : 0.f;
             const float invd = 1.0f / (lane < nr ? diag + 1e-12f : 1.f);
-            for (int it = 0; it < p.solver_iterations; ++it) pgs_sweep<0>(w, lamv, acol, invd, nc, L.cmu, lane);
+            const float muL = lane < nr ? L.cmu[lane / 3] : 0.f;
+            const int ncu = __builtin_amdgcn_readfirstlane(nc);
+            for (int it = 0; it < p.solver_iterations; ++it) pgs_sweep<0>(w, lamv, acol, invd, muL, ncu);
         }
         L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();

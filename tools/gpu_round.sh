@@ -5,7 +5,8 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-run}
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1 &&
+# SKIP_TESTS=1: measure only (a candidate kernel whose parity is being investigated)
+{ [ "${SKIP_TESTS:-0}" = 1 ] || timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1; } &&
 timeout -k 10 300 python tools/phase_profile.py > gpurun_out/phases_$TAG.json 2> gpurun_out/phases.err &&
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-puffer-level > gpurun_out/bench_prof_$TAG.log 2>&1
