@@ -148,3 +148,13 @@ class HeRolloutIndex(C.Structure):
                 ("scratch_rows", C.c_int64), ("key_count", C.c_void_p), ("key_last", C.c_void_p),
                 ("key_offset", C.c_void_p), ("row_env", C.c_void_p), ("row_rank", C.c_void_p),
                 ("scratch", C.c_void_p), ("status", C.c_void_p)]
+
+
+# include/humanoid_engine.h he_eval_buffers
+EVAL_SUMS = 8
+
+
+class HeEvalBuffers(C.Structure):
+    _fields_ = [("num_steps", C.c_void_p), ("mpjpe", C.c_void_p), ("body_pos", C.c_void_p),
+                ("body_pos_gt", C.c_void_p), ("history", C.c_void_p), ("sums", C.c_void_p),
+                ("frame", C.c_int32), ("reserved", C.c_int32)]

@@ -66,6 +66,8 @@ struct he_engine {
     int32_t* frozen = nullptr;
     int clip_actions = 1;
     bool has_pd = false;
+    he_eval_buffers eval{};
+    int has_eval = 0;
     // motion library
     float *m_hot = nullptr, *m_cold = nullptr, *m_lengths = nullptr, *m_dt = nullptr;
     int64_t *m_starts = nullptr, *m_nframes = nullptr;
@@ -455,6 +457,8 @@ int imit_common(he_engine* h, const he_imitation_params* p, const he_env_motion*
     a.start_offsets = em->start_offsets;
     a.global_offset = em->global_offset;
     a.progress = em->progress;
+    a.ev = h->eval;
+    a.has_eval = h->has_eval;
     return 0;
 }
 }  // namespace
@@ -468,6 +472,19 @@ int he_imitation_step(he_engine* h, const he_imitation_params* p, const he_env_m
     a.count = h->num_envs;
     a.mode = 0;
     HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    return 0;
+}
+
+int he_set_eval(he_engine* h, const he_eval_buffers* b) {
+    if (!h) return fail("he_set_eval: null engine");
+    if (!b) {
+        h->has_eval = 0;
+        return 0;
+    }
+    if (!b->num_steps || !b->history || !b->sums) return fail("he_set_eval: num_steps, history and sums are required");
+    if (b->frame < 0) return fail("he_set_eval: negative frame");
+    h->eval = *b;
+    h->has_eval = 1;
     return 0;
 }
 

@@ -174,6 +174,143 @@ HE_DEV void reset_body(const ImitArgs& a, int e, int b, int64_t mid, float t, f3
     }
 }
 
+// ---------------- eval-mode recording (include/humanoid_engine.h he_eval_buffers)
+HE_DEV double group_sum_d(double v) {
+#pragma unroll
+    for (int o = GROUP / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, GROUP);
+    return v;
+}
+
+// Largest eigenpair of a symmetric 4x4 by cyclic Jacobi (fp64, fully unrolled: register-resident)
+template <int P, int Q>
+HE_DEV void jacobi_rot(double (&A)[4][4], double (&V)[4][4]) {
+    const double apq = A[P][Q];
+    if (fabs(apq) < 1e-300) return;
+    const double th = (A[Q][Q] - A[P][P]) / (2.0 * apq);
+    const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+    const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double akp = A[k][P], akq = A[k][Q];
+        A[k][P] = c * akp - sn * akq;
+        A[k][Q] = sn * akp + c * akq;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double apk = A[P][k], aqk = A[Q][k];
+        A[P][k] = c * apk - sn * aqk;
+        A[Q][k] = sn * apk + c * aqk;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double vkp = V[k][P], vkq = V[k][Q];
+        V[k][P] = c * vkp - sn * vkq;
+        V[k][Q] = sn * vkp + c * vkq;
+    }
+}
+
+// p_mpjpe (smpl_sim smpl_eval, the VideoPose3D "protocol #2"): per-joint error after the
+// similarity transform (scale, rotation, translation) that best maps pred onto target. The
+// reference solves it by a 3x3 SVD with a reflection fix; the same optimum is the top eigenpair of
+// Horn's 4x4 quaternion matrix (eigenvalue = trace of the sign-fixed singular values), used here.
+// Lanes = joints; y = pred, x = target (both root-relative), fp64 inside.
+HE_DEV float pa_mpjpe_group(bool act, f3 yf, f3 xf) {
+    const double yx = act ? yf.x : 0.0, yy = act ? yf.y : 0.0, yz = act ? yf.z : 0.0;
+    const double xx = act ? xf.x : 0.0, xy = act ? xf.y : 0.0, xz = act ? xf.z : 0.0;
+    const double my[3] = {group_sum_d(yx) / NB, group_sum_d(yy) / NB, group_sum_d(yz) / NB};
+    const double mx[3] = {group_sum_d(xx) / NB, group_sum_d(xy) / NB, group_sum_d(xz) / NB};
+    const double Y[3] = {act ? yx - my[0] : 0.0, act ? yy - my[1] : 0.0, act ? yz - my[2] : 0.0};
+    const double X[3] = {act ? xx - mx[0] : 0.0, act ? xy - mx[1] : 0.0, act ? xz - mx[2] : 0.0};
+    double S[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) S[i][j] = group_sum_d(Y[i] * X[j]);
+    const double yn = group_sum_d(Y[0] * Y[0] + Y[1] * Y[1] + Y[2] * Y[2]);
+    double A[4][4] = {{S[0][0] + S[1][1] + S[2][2], S[1][2] - S[2][1], S[2][0] - S[0][2], S[0][1] - S[1][0]},
+                      {S[1][2] - S[2][1], S[0][0] - S[1][1] - S[2][2], S[0][1] + S[1][0], S[2][0] + S[0][2]},
+                      {S[2][0] - S[0][2], S[0][1] + S[1][0], -S[0][0] + S[1][1] - S[2][2], S[1][2] + S[2][1]},
+                      {S[0][1] - S[1][0], S[2][0] + S[0][2], S[1][2] + S[2][1], -S[0][0] - S[1][1] + S[2][2]}};
+    double V[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+#pragma unroll 1
+    for (int sweep = 0; sweep < 10; ++sweep) {
+        jacobi_rot<0, 1>(A, V); jacobi_rot<0, 2>(A, V); jacobi_rot<0, 3>(A, V);
+        jacobi_rot<1, 2>(A, V); jacobi_rot<1, 3>(A, V); jacobi_rot<2, 3>(A, V);
+    }
+    int k = 0;
+    double lam = A[0][0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (A[i][i] > lam) { lam = A[i][i]; k = i; }
+    double q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = k == 0 ? V[i][0] : (k == 1 ? V[i][1] : (k == 2 ? V[i][2] : V[i][3]));
+    const double qn = 1.0 / sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double w = q[0] * qn, vx = q[1] * qn, vy = q[2] * qn, vz = q[3] * qn;
+    const double scale = lam / yn;
+    // Q y = y + 2w (v x y) + 2 v x (v x y)
+    const double c1x = vy * Y[2] - vz * Y[1], c1y = vz * Y[0] - vx * Y[2], c1z = vx * Y[1] - vy * Y[0];
+    const double c2x = vy * c1z - vz * c1y, c2y = vz * c1x - vx * c1z, c2z = vx * c1y - vy * c1x;
+    const double ex = scale * (Y[0] + 2.0 * (w * c1x + c2x)) - X[0];
+    const double ey = scale * (Y[1] + 2.0 * (w * c1y + c2y)) - X[1];
+    const double ez = scale * (Y[2] + 2.0 * (w * c1z + c2z)) - X[2];
+    const double err = act ? sqrt(ex * ex + ey * ey + ez * ez) : 0.0;
+    return (float)(group_sum_d(err) / NB);
+}
+
+// One eval frame of env e (lane b = body): p = simulated body position, g = reference rg_pos.
+HE_DEV void eval_record(const he_eval_buffers& ev, int e, int lane, bool act, f3 p, f3 g) {
+    const int b = act ? lane : 0;
+    const int s = ev.frame;
+    // extras["mpjpe"] = (body_pos - rg_pos).norm(dim=-1).mean(dim=-1) (humanoid_phc.py:165)
+    const float dist = act ? norm3(p - g) : 0.0f;
+    const float mp = group_sum(dist) / NB;
+    if (lane == 0 && ev.mpjpe) ev.mpjpe[e] = mp;
+    if (act && ev.body_pos) { float* o = ev.body_pos + ((size_t)e * NB + b) * 3; o[0] = p.x; o[1] = p.y; o[2] = p.z; }
+    if (act && ev.body_pos_gt) { float* o = ev.body_pos_gt + ((size_t)e * NB + b) * 3; o[0] = g.x; o[1] = g.y; o[2] = g.z; }
+    double* sum = ev.sums + (size_t)e * HE_EVAL_SUMS;
+    float* hist = ev.history + (size_t)e * (2 * 2 * NB * 3);  // [slot][pred, gt][NB][3]
+    auto H = [&](int slot, int which) { return hist + ((slot * 2 + which) * NB + b) * 3; };
+    if (s == 0 && lane == 0)
+        for (int k = 0; k < HE_EVAL_SUMS; ++k) sum[k] = 0.0;
+    if (s < ev.num_steps[e] - 1) {  // the frame is inside the [: (i - 1)] slice (phc_train.py:146-151)
+        // compute_metrics_lite per frame (x 1000 = mm): mpjpe_g on world positions ...
+        const float mg = group_sum(act ? norm3(g - p) : 0.0f) / NB * 1000.0f;
+        // ... mpjpe_l and p_mpjpe on root-relative positions
+        const f3 p0 = f3{__shfl(p.x, 0, GROUP), __shfl(p.y, 0, GROUP), __shfl(p.z, 0, GROUP)};
+        const f3 g0 = f3{__shfl(g.x, 0, GROUP), __shfl(g.y, 0, GROUP), __shfl(g.z, 0, GROUP)};
+        const f3 pr = p - p0, gr = g - g0;
+        const float ml = group_sum(act ? norm3(pr - gr) : 0.0f) / NB * 1000.0f;
+        const float pa = pa_mpjpe_group(act, pr, gr) * 1000.0f;
+        float vel = 0.0f, acc = 0.0f;
+        if (s >= 1) {  // compute_error_vel: frame differences
+            const float* p1 = H((s - 1) & 1, 0);
+            const float* g1 = H((s - 1) & 1, 1);
+            const f3 vp = p - f3{p1[0], p1[1], p1[2]}, vg = g - f3{g1[0], g1[1], g1[2]};
+            vel = group_sum(act ? norm3(vp - vg) : 0.0f) / NB * 1000.0f;
+            if (s >= 2) {  // compute_error_accel: x[t-2] - 2 x[t-1] + x[t]
+                const float* p2 = H(s & 1, 0);
+                const float* g2 = H(s & 1, 1);
+                const f3 ap = (f3{p2[0], p2[1], p2[2]} - f3{p1[0], p1[1], p1[2]} * 2.0f) + p;
+                const f3 ag = (f3{g2[0], g2[1], g2[2]} - f3{g1[0], g1[1], g1[2]} * 2.0f) + g;
+                acc = group_sum(act ? norm3(ap - ag) : 0.0f) / NB * 1000.0f;
+            }
+        }
+        if (lane == 0) {
+            sum[0] += mg; sum[1] += ml; sum[2] += pa;
+            sum[5] += 1.0;
+            if (s >= 1) { sum[3] += vel; sum[6] += 1.0; }
+            if (s >= 2) { sum[4] += acc; sum[7] += 1.0; }
+        }
+    }
+    if (act) {  // this frame becomes history (slot s & 1 held frame s - 2, already read above)
+        float* hp = H(s & 1, 0);
+        float* hg = H(s & 1, 1);
+        hp[0] = p.x; hp[1] = p.y; hp[2] = p.z;
+        hg[0] = g.x; hg[1] = g.y; hg[2] = g.z;
+    }
+}
+
 __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
     const int lane = threadIdx.x & (GROUP - 1);
     const int slot = (blockIdx.x * blockDim.x + threadIdx.x) / GROUP;
@@ -241,6 +378,7 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
             fallen = fallen && prog > 1;
         }
         bool reset = pass_time || fallen;
+        if (a.has_eval) eval_record(a.ev, e, lane, act, s.pos, r.pos);  // before any fused reset
         if (lane == 0) {
             a.rew[e] = rew;
             float* raw = a.reward_raw + (size_t)e * HE_REWARD_RAW;

@@ -46,6 +46,8 @@ struct ImitArgs {
     int mode;                // 0 step, 1 step + fused device reset, 2 reset listed envs
     const float* phases;     // mode 2: [count]
     uint64_t seed, step;
+    he_eval_buffers ev;      // eval recording (modes 0/1) when has_eval
+    int has_eval;
 };
 
 struct MotionStateArgs {

@@ -30,7 +30,7 @@ HE_SYMBOLS = (
     "he_get_buffer", "he_set_dof_targets", "he_set_root_state_indexed", "he_set_dof_state_indexed",
     "he_set_dof_targets_indexed", "he_set_env_properties", "he_simulate", "he_set_pd_params", "he_step_actions",
     "he_refresh", "he_load_motions", "he_imitation_step", "he_motion_state", "he_reset_envs", "he_env_step",
-    "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips",
+    "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips", "he_set_eval",
     # include/humanoid_rollout.h
     "he_rollout_store", "he_rollout_order", "he_rollout_gather", "he_gae", "he_gae_minibatch",
 )
@@ -65,6 +65,7 @@ def load_library(path: Optional[str] = None):
         "he_imitation_reset_step": [V, V, V, C.c_uint64, C.c_uint64, V, V, V, V, V, V],
         "he_device_count": [V],
         "he_set_debug_stamps": [V, V],
+        "he_set_eval": [V, V],
         "he_rollout_store": [V, V, I, C.c_int64, V, V, C.c_int64, C.c_int32, V],
         "he_rollout_order": [V, C.c_int64, V, I, V],
         "he_rollout_gather": [V, I, V, C.c_int64, C.c_int32, C.c_int32, C.c_int32, V],
@@ -352,6 +353,10 @@ class Engine:
                                                 C.c_void_p(rew.data_ptr()), C.c_void_p(reward_raw.data_ptr()),
                                                 C.c_void_p(reset.data_ptr()), C.c_void_p(terminate.data_ptr()),
                                                 self.stream))
+
+    def set_eval(self, buffers: Optional[_abi.HeEvalBuffers]):
+        """Attach eval recording (he_set_eval; the struct is copied, call again per frame) or detach."""
+        _check(self.lib.he_set_eval(self.h, None if buffers is None else C.byref(buffers)))
 
     def set_debug_stamps(self, buf=None):
         """Diagnostics: int64 [num_envs, 16] device tensor receiving per-phase cycles, or None."""

@@ -166,6 +166,7 @@ class HumanoidPHC:
         self.all_env_ids = torch.arange(n, device=dev)
         self.flag_test = False
         self.flag_im_eval = False
+        self._eval_recorder = None
         self._gen = torch.Generator(device=dev).manual_seed(cfg.seed)
         self._term_dist = float(cfg.termination_distance)
         self._reset_bodies = list(range(self.num_bodies))
@@ -201,6 +202,18 @@ class HumanoidPHC:
         # sampling on the host (motion_lib.py:305-345), ingestion on the device (he_ingest_clips)
         clips, motion_clip = self._motion_lib.select_motions(self.cfg.num_envs, **kw)
         self.engine.ingest_clips(clips, motion_clip)
+        if self._eval_recorder is not None:
+            self._eval_recorder.set_num_steps(self.get_motion_steps())
+
+    def _attach_eval(self):
+        """Eval mode: the next stepping launch also records the frame's metrics (he_set_eval) and the
+        reference's eval extras (humanoid_phc.py:158-169; device tensors instead of host copies)."""
+        if self.flag_im_eval and self._eval_recorder is not None:
+            rec = self._eval_recorder
+            rec.attach()
+            self.extras["mpjpe"] = rec.mpjpe
+            self.extras["body_pos"] = rec.body_pos
+            self.extras["body_pos_gt"] = rec.body_pos_gt
 
     # -- reset / step (:90-172) ----------------------------------------------------------
     def _reset_envs(self, env_ids):
@@ -223,6 +236,7 @@ class HumanoidPHC:
 
     def step(self, actions):
         self.engine.step_actions(actions, 2)
+        self._attach_eval()
         self.engine.imitation_step(self._params, self._em, self.obs_buf, self.rew_buf, self.reward_raw,
                                    self._reset_u8, self._term_u8)
         self.extras["terminate"] = self._terminate_buf.clone()
@@ -258,12 +272,19 @@ class HumanoidPHC:
         if len(self._reset_bodies) > 15:
             self._reset_bodies = list(body_ids(EVAL_BODIES))
         self._update_params()
+        from .eval import EvalRecorder
+        self._eval_recorder = EvalRecorder(self.engine, self.cfg.num_envs, self.device)
         self.begin_seq_motion_samples()
         return self._motion_lib._num_unique_motions
 
     def untoggle_eval_mode(self, failed_keys):
         self.flag_test = False
         self.flag_im_eval = False
+        if self._eval_recorder is not None:
+            self._eval_recorder.detach()
+            self._eval_recorder = None
+        for k in ("mpjpe", "body_pos", "body_pos_gt"):
+            self.extras.pop(k, None)
         self._term_dist = float(self.cfg.termination_distance)
         self._motion_lib = self._motion_train_lib
         self._reset_bodies = list(self._reset_bodies_backup)
@@ -376,6 +397,7 @@ class PHCPufferEnv:
             self.actions[:] = actions.clamp(-1, 1) if self.cfg.clip_actions else actions
         e = self.env
         e.engine.step_actions(self.actions, 2)
+        e._attach_eval()
         e.engine.imitation_reset_step(e._params, e._em, e.obs_buf, e.rew_buf, e.reward_raw, e._reset_u8, e._term_u8,
                                       seed=self.cfg.seed, step_index=self.tick)
         e.extras["terminate"] = e._terminate_buf.clone()

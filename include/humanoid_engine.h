@@ -221,6 +221,31 @@ int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he
                             uint64_t step_index, float* obs, float* rew, float* reward_raw, uint8_t* reset,
                             uint8_t* terminate, void* stream);
 
+/* Eval-mode metric recording. While attached, every imitation launch that steps
+ * (he_imitation_step, he_imitation_reset_step, he_env_step) also records, per env and before any
+ * fused reset, what the reference copies to the host each eval step (humanoid_phc.py:158-169:
+ * extras "mpjpe", "body_pos", "body_pos_gt") and accumulates the per-frame metrics that
+ * EvalStats.get_final_stats computes over the stacked copies with smpl_sim's compute_metrics_lite
+ * (scripts/phc_train.py:126-128, 166-189; smpl_sim 0.0.1 @ fe22a5d9, un-vendored): mpjpe_g,
+ * mpjpe_l, mpjpe_pa, vel_dist, accel_dist in mm. Frame `frame` (EvalStats.curr_steps) of env e
+ * counts while frame < num_steps[e] - 1 (the `[: (i - 1)]` slices, phc_train.py:146-151); frame 0
+ * restarts the env's sums. sums[e] = {mpjpe_g, mpjpe_l, mpjpe_pa, vel_dist, accel_dist} summed over
+ * counted frames, then {n_frames, n_vel, n_accel}. */
+#define HE_EVAL_SUMS 8
+typedef struct he_eval_buffers {
+    const int32_t* num_steps;  /* [N] get_motion_num_steps() of each env's motion */
+    float* mpjpe;              /* [N] extras["mpjpe"] (m), NULL to skip */
+    float* body_pos;           /* [N,24,3] extras["body_pos"], NULL to skip */
+    float* body_pos_gt;        /* [N,24,3] extras["body_pos_gt"], NULL to skip */
+    float* history;            /* [N,2,2,24,3] scratch: the last two frames (pred, gt) */
+    double* sums;              /* [N,HE_EVAL_SUMS] */
+    int32_t frame;
+    int32_t reserved;
+} he_eval_buffers;
+
+/* Attach (copied by value; call again each step with the new frame) or detach (NULL). */
+int he_set_eval(he_engine* h, const he_eval_buffers* buffers);
+
 /* Diagnostics: when non-NULL, the physics kernel accumulates per-phase shader cycles into
  * device_buffer [N][16] (u64; phases listed in DESIGN.md §4). NULL disables (default). */
 int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer);
