@@ -31,7 +31,7 @@ PHYS_FLOP_PER_ENV_STEP = 1_309_278          # dense-equivalent physics, 2 subste
 IMIT_BYTES_PER_ENV_STEP = 13_200            # fused imitation kernel share of the 16.0 KB/env-step
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 DATA = {

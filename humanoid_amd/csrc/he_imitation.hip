@@ -236,6 +236,10 @@ HE_DEV float pa_mpjpe_group(bool act, f3 yf, f3 xf) {
     for (int sweep = 0; sweep < 10; ++sweep) {
         jacobi_rot<0, 1>(A, V); jacobi_rot<0, 2>(A, V); jacobi_rot<0, 3>(A, V);
         jacobi_rot<1, 2>(A, V); jacobi_rot<1, 3>(A, V); jacobi_rot<2, 3>(A, V);
+        const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[0][3] * A[0][3] + A[1][2] * A[1][2] +
+                           A[1][3] * A[1][3] + A[2][3] * A[2][3];
+        const double dia = A[0][0] * A[0][0] + A[1][1] * A[1][1] + A[2][2] * A[2][2] + A[3][3] * A[3][3];
+        if (off <= 1e-30 * dia) break;  // converged to fp64 rounding (typically 3-4 sweeps)
     }
     int k = 0;
     double lam = A[0][0];
