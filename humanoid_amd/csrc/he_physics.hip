@@ -240,6 +240,49 @@ HE_DEV void swap32(float& a, float& b) {
     a = __uint_as_float(r[0]);
     b = __uint_as_float(r[1]);
 }
+HE_DEV void swap16(float& a, float& b) {  // odd 16-lane rows of a <-> even rows of b
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+template <int CTRL>
+HE_DEV float dpp(float x) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false)); }
+
+// One butterfly stage of a wave reduce-scatter below 16 lanes: the partner (DPP pattern CTRL, an
+// involution flipping lane bit B) gets the half this lane drops; lanes with bit B keep the upper
+// half. H = values kept.
+template <int H, int CTRL, uint64_t BITMASK>
+HE_DEV void rs_dpp(float* v) {
+    const bool up = regla::lanes<BITMASK>();
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const float send = up ? v[j] : v[j + H];
+        const float keep = up ? v[j + H] : v[j];
+        v[j] = keep + dpp<CTRL>(send);
+    }
+}
+
+// Reduce-scatter of N = 64 or 16 per-lane values: returns sum over all lanes of v[idx(lane)], with
+// idx = lane (N = 64) or lane >> 2 (N = 16). Pairings by lane-bit flips 32, 16 (permlane swaps),
+// 15 (row mirror), 7 (half-row mirror), 2, 1 (quad perms): independent, so every lane's result
+// covers all 64 lanes once; 63 exchanges + 63 adds for 64 values (vs 6 x 64 for all-reduce).
+template <int N>
+HE_DEV float reduce_scatter(float (&v)[N]) {
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) { swap32(v[j], v[j + N / 2]); v[j] += v[j + N / 2]; }
+#pragma unroll
+    for (int j = 0; j < N / 4; ++j) { swap16(v[j], v[j + N / 4]); v[j] += v[j + N / 4]; }
+    rs_dpp<N / 8, 0x140, 0xFF00FF00FF00FF00ull>(v);  // row_mirror: lane ^ 15
+    rs_dpp<N / 16, 0x141, 0xF0F0F0F0F0F0F0F0ull>(v);  // row_half_mirror: lane ^ 7
+    if constexpr (N == 64) {
+        rs_dpp<2, 0x4E, 0xCCCCCCCCCCCCCCCCull>(v);  // quad_perm [2,3,0,1]: lane ^ 2
+        rs_dpp<1, 0xB1, 0xAAAAAAAAAAAAAAAAull>(v);  // quad_perm [1,0,3,2]: lane ^ 1
+    } else {
+        v[0] += dpp<0x4E>(v[0]);  // the 4 lanes of a quad hold the same index: all-reduce them
+        v[0] += dpp<0xB1>(v[0]);
+    }
+    return v[0];
+}
 HE_DEV void delassus_mfma(const float (&z)[NG], float (&acol)[MAXR], uint32_t live) {
     f32x16 t00 = {}, t01 = {}, t10 = {}, t11 = {};
 #pragma unroll
@@ -805,8 +848,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         const int nr = 3 * nc;
         float brow = 0.f, diag = 0.f, lamv = 0.f;
         float acol[MAXR];  // lane c: A[r][c]
+        float z[NG];       // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
         {
-            float z[NG];
             const int r = lane < nr ? lane : 0;
             const int ci = r / 3, kind = r - 3 * ci;
             const float* dir = kind == 0 ? L.cn[ci] : (kind == 1 ? L.ct1[ci] : L.ct2[ci]);
@@ -869,40 +912,51 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();
         STAMP(10);
-        // ---- contact impulses -> body spatial impulses (about o) and reported contact forces:
-        // lane c forms contact c's spatial impulse, lane b gathers the ones acting on body b
-        float (*imp)[6] = L.Acc;  // per-contact scratch (Acc is dead in the contact phase)
+        // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
+        // a wave reduce-scatter sums the 75 columns into lane = dof, then one L^-1 sweep
+        {
+            float v64[64], v16[16];
+#pragma unroll
+            for (int i = 0; i < 64; ++i) v64[i] = z[i] * lamv;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? z[64 + i] * lamv : 0.f;
+            float yl = reduce_scatter<64>(v64);
+            float y2 = __shfl(reduce_scatter<16>(v16), 4 * (lane & 15), W);
+            yl *= L.sDinv[lane];
+            y2 = lane < NH ? y2 * L.sDinv[64 + lane] : 0.f;
+            float r1[regla::kRowRegs], r2[regla::kRowRegs];
+            const float4* p1 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane]);
+            const float4* p2 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane < NH ? 64 + lane : 0]);
+#pragma unroll
+            for (int q = 0; q < regla::kRowRegs / 4; ++q) {
+                const float4 a1 = p1[q], a2 = p2[q];
+                r1[4 * q] = a1.x; r1[4 * q + 1] = a1.y; r1[4 * q + 2] = a1.z; r1[4 * q + 3] = a1.w;
+                r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
+            }
+            regla::solve_L_rows<0>(r1, r2, yl, y2);
+            L.uf[lane] += yl;
+            if (lane < NH) L.uf[64 + lane] += y2;
+        }
+        // ---- reported contact forces (net linear contact impulse per body / dt)
+        float (*fc)[6] = L.Acc;  // per-contact scratch (Acc is dead in the contact phase)
         if (lane < nc) {
             const int c = lane;
             const float ln = L.lam[3 * c], la = L.lam[3 * c + 1], lb = L.lam[3 * c + 2];
-            const f3 f = f3{ln * L.cn[c][0] + la * L.ct1[c][0] + lb * L.ct2[c][0],
-                            ln * L.cn[c][1] + la * L.ct1[c][1] + lb * L.ct2[c][1],
-                            ln * L.cn[c][2] + la * L.ct1[c][2] + lb * L.ct2[c][2]};
-            const f3 n = cross3(f3{L.cx[c][0], L.cx[c][1], L.cx[c][2]} - o, f);
-            imp[c][0] = n.x; imp[c][1] = n.y; imp[c][2] = n.z; imp[c][3] = f.x; imp[c][4] = f.y; imp[c][5] = f.z;
+            fc[c][0] = ln * L.cn[c][0] + la * L.ct1[c][0] + lb * L.ct2[c][0];
+            fc[c][1] = ln * L.cn[c][1] + la * L.ct1[c][1] + lb * L.ct2[c][1];
+            fc[c][2] = ln * L.cn[c][2] + la * L.ct1[c][2] + lb * L.ct2[c][2];
         }
         sync();
         if (lane < NB) {
-            float F6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            float F3[3] = {0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < MAXC; ++c) {
                 if (c < nc) {
-                    const float s = (L.cb0[c] == lane ? 1.f : 0.f) - (L.cb1[c] == lane ? 1.f : 0.f);
-                    for (int x = 0; x < 6; ++x) F6[x] += s * imp[c][x];
+                    const float sg = (L.cb0[c] == lane ? 1.f : 0.f) - (L.cb1[c] == lane ? 1.f : 0.f);
+                    for (int x = 0; x < 3; ++x) F3[x] += sg * fc[c][x];
                 }
             }
-            for (int x = 0; x < 6; ++x) L.F[lane][x] = F6[x];
-            L.cf[lane][0] = F6[3] / dt; L.cf[lane][1] = F6[4] / dt; L.cf[lane][2] = F6[5] / dt;
-        }
-        sync();
-        subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.F[0][0], nullptr, lane);
-        // ---- du = L^-1 D^-1 L^-T (J^T lambda), generalized impulse tau_i = S_i . F_subtree(body(i))
-        {
-            float yl = dot6(L.S[lane], L.F[dof_body(lane)]);
-            float y2 = lane < NH ? dot6(L.S[64 + lane], L.F[dof_body(64 + lane)]) : 0.f;
-            joint_space_solve(L, yl, y2, lane);
-            L.uf[lane] += yl;
-            if (lane < NH) L.uf[64 + lane] += y2;
+            L.cf[lane][0] = F3[0] / dt; L.cf[lane][1] = F3[1] / dt; L.cf[lane][2] = F3[2] / dt;
         }
         sync();
     }
