@@ -171,17 +171,19 @@ HE_DEV void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3& c1, f3& c2) {
     float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
     float s, t;
     const float eps = 1e-12f;
+    // divisions as v_rcp_f32 products (1 ulp; the fp64 oracle's tolerance covers it)
+    const float ia = __builtin_amdgcn_rcpf(a), ie = __builtin_amdgcn_rcpf(e);
     if (a <= eps && e <= eps) { s = t = 0.f; }
-    else if (a <= eps) { s = 0.f; t = fminf(fmaxf(f / e, 0.f), 1.f); }
+    else if (a <= eps) { s = 0.f; t = __builtin_amdgcn_fmed3f(f * ie, 0.f, 1.f); }
     else {
         float c = dot3(d1, r);
-        if (e <= eps) { t = 0.f; s = fminf(fmaxf(-c / a, 0.f), 1.f); }
+        if (e <= eps) { t = 0.f; s = __builtin_amdgcn_fmed3f(-c * ia, 0.f, 1.f); }
         else {
             float b = dot3(d1, d2), den = a * e - b * b;
-            s = den > eps ? fminf(fmaxf((b * f - c * e) / den, 0.f), 1.f) : 0.f;
-            t = (b * s + f) / e;
-            if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-c / a, 0.f), 1.f); }
-            else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((b - c) / a, 0.f), 1.f); }
+            s = den > eps ? __builtin_amdgcn_fmed3f((b * f - c * e) * __builtin_amdgcn_rcpf(den), 0.f, 1.f) : 0.f;
+            t = (b * s + f) * ie;
+            if (t < 0.f) { t = 0.f; s = __builtin_amdgcn_fmed3f(-c * ia, 0.f, 1.f); }
+            else if (t > 1.f) { t = 1.f; s = __builtin_amdgcn_fmed3f((b - c) * ia, 0.f, 1.f); }
         }
     }
     c1 = p1 + d1 * s;
@@ -208,11 +210,7 @@ HE_DEV void store_contact(Lds& L, int slot, int b0, int b1, f3 x, f3 n, float ga
     L.cb0[slot] = b0;
     L.cb1[slot] = b1;
     L.cx[slot][0] = x.x; L.cx[slot][1] = x.y; L.cx[slot][2] = x.z;
-    L.cn[slot][0] = n.x; L.cn[slot][1] = n.y; L.cn[slot][2] = n.z;
-    f3 t1, t2;
-    friction_basis(n, t1, t2);
-    L.ct1[slot][0] = t1.x; L.ct1[slot][1] = t1.y; L.ct1[slot][2] = t1.z;
-    L.ct2[slot][0] = t2.x; L.ct2[slot][1] = t2.y; L.ct2[slot][2] = t2.z;
+    L.cn[slot][0] = n.x; L.cn[slot][1] = n.y; L.cn[slot][2] = n.z;  // friction basis: one pass, lane = contact
     L.cgap[slot] = gap;
     L.cmu[slot] = mu;
 }
@@ -757,11 +755,16 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                     cand[e2] = cd[e2] < off;
                 }
             } else {
-                f4 bq = f4{g[6], g[7], g[8], g[9]};
+                // corners = world centre +- the three world half-axes (4 rotations, not 16)
+                const f4 bq = f4{g[6], g[7], g[8], g[9]};
+                const f4 qb = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
+                const f3 ctr = body_point(L, b, f3{g[0], g[1], g[2]});
+                const f3 ex = qapply(qb, qapply(bq, f3{g[3], 0.f, 0.f}));
+                const f3 ey = qapply(qb, qapply(bq, f3{0.f, g[4], 0.f}));
+                const f3 ez = qapply(qb, qapply(bq, f3{0.f, 0.f, g[5]}));
 #pragma unroll
                 for (int ci = 0; ci < 8; ++ci) {
-                    f3 lb = f3{(ci & 1) ? g[3] : -g[3], (ci & 2) ? g[4] : -g[4], (ci & 4) ? g[5] : -g[5]};
-                    cxs[ci] = body_point(L, b, f3{g[0], g[1], g[2]} + qapply(bq, lb));
+                    cxs[ci] = ((ctr + ((ci & 1) ? ex : ex * -1.f)) + ((ci & 2) ? ey : ey * -1.f)) + ((ci & 4) ? ez : ez * -1.f);
                     cd[ci] = terrain_dist(p, tkind, cxs[ci], cns[ci]);
                     cand[ci] = cd[ci] < off;
                 }
@@ -806,15 +809,24 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             seg[lane][3] = c.x; seg[lane][4] = c.y; seg[lane][5] = c.z; seg[lane][6] = r;
         }
         sync();
-        for (int base = 0; base < m.num_pairs; base += W) {
-            int pi = base + lane;
-            bool hit = false;
-            f3 x, n;
-            float gap = 0.f;
-            int i = 0, j = 0;
+        // every round's segment test first: four independent dependency chains per lane
+        constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
+        bool hit[ROUNDS];
+        f3 px[ROUNDS], pn[ROUNDS];
+        float pgap[ROUNDS];
+        int pi0[ROUNDS], pj0[ROUNDS];
+#pragma unroll
+        for (int rd = 0; rd < ROUNDS; ++rd) {
+            const int pi = rd * W + lane;
+            hit[rd] = false;
+            pgap[rd] = 0.f;
+            pi0[rd] = 0;
+            pj0[rd] = 0;
+            px[rd] = pn[rd] = f3{0.f, 0.f, 0.f};
             if (pi < m.num_pairs) {
-                i = m.pairs[pi][0];
-                j = m.pairs[pi][1];
+                const int i = m.pairs[pi][0], j = m.pairs[pi][1];
+                pi0[rd] = i;
+                pj0[rd] = j;
                 const float* si = seg[i];
                 const float* sj = seg[j];
                 const f3 a0 = f3{si[0], si[1], si[2]}, a1 = f3{si[3], si[4], si[5]};
@@ -822,23 +834,33 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 const float ri = si[6], rj = sj[6];
                 f3 ci, cj;
                 seg_seg(a0, a1, b0, b1, ci, cj);
-                f3 dv = ci - cj;
-                float len = norm3(dv);
-                gap = len - ri - rj;
-                if (gap < off) {
-                    hit = true;
-                    n = len > 1e-9f ? dv * (1.0f / len) : f3{0.f, 0.f, 1.f};
-                    x = cj + n * (rj + 0.5f * gap);
+                const f3 dv = ci - cj;
+                const float len = norm3(dv);
+                pgap[rd] = len - ri - rj;
+                if (pgap[rd] < off) {
+                    hit[rd] = true;
+                    pn[rd] = len > 1e-9f ? dv * __builtin_amdgcn_rcpf(len) : f3{0.f, 0.f, 1.f};
+                    px[rd] = cj + pn[rd] * (rj + 0.5f * pgap[rd]);
                 }
             }
+        }
+#pragma unroll
+        for (int rd = 0; rd < ROUNDS; ++rd) {
             int total;
-            int pre = wave_prefix(hit, lane, total);
-            if (hit && nc + pre < maxc) store_contact(L, nc + pre, i, j, x, n, gap, mu);
+            const int pre = wave_prefix(hit[rd], lane, total);
+            if (hit[rd] && nc + pre < maxc) store_contact(L, nc + pre, pi0[rd], pj0[rd], px[rd], pn[rd], pgap[rd], mu);
             nc = nc + total < maxc ? nc + total : maxc;
         }
     }
     if (lane == 0) L.nc = nc;
     if (lane < NB) { L.cf[lane][0] = 0.f; L.cf[lane][1] = 0.f; L.cf[lane][2] = 0.f; }
+    sync();
+    if (lane < nc) {  // tangent basis of every contact at once (lane = contact)
+        f3 t1, t2;
+        friction_basis(f3{L.cn[lane][0], L.cn[lane][1], L.cn[lane][2]}, t1, t2);
+        L.ct1[lane][0] = t1.x; L.ct1[lane][1] = t1.y; L.ct1[lane][2] = t1.z;
+        L.ct2[lane][0] = t2.x; L.ct2[lane][1] = t2.y; L.ct2[lane][2] = t2.z;
+    }
     sync();
     STAMP(7);
     if (nc > 0) {
