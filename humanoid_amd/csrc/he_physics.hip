@@ -19,6 +19,8 @@
 //   -> PGS -> velocity update -> damping / clamps -> semi-implicit integration.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/humanoid_engine.h"
 #include "he_kernels.h"
 #include "he_math.h"
@@ -535,58 +537,105 @@ HE_DEV void subtree_levels(float* F, float* I, int lane) {
 }
 
 // ---------------------------------------------------------------------------------- kinematics
+// 2^k-th ancestor of every body (-1: none), for pointer jumping over the body tree
+struct JumpTable {
+    int j[4][NB];
+    constexpr JumpTable() : j() {
+        for (int b = 0; b < NB; ++b) j[0][b] = smpl::kParentBody[b];
+        for (int k = 1; k < 4; ++k)
+            for (int b = 0; b < NB; ++b) j[k][b] = j[k - 1][b] < 0 ? -1 : j[k - 1][j[k - 1][b]];
+    }
+};
+constexpr JumpTable kJumpT{};
+static_assert(smpl::kNumBodyLevels <= 16, "four pointer-jumping rounds cover chains of 16 bodies");
+
+template <int K>
+HE_DEV int jump_of(int b) {  // kJumpT.j[K][b] as a select chain (no runtime-indexed constant memory)
+    int r = -1;
+#pragma unroll
+    for (int x = 0; x < NB; ++x) r = b == x ? kJumpT.j[K][x] : r;
+    return r;
+}
+
+// World poses and spatial velocities, lane = body, by pointer jumping: X_b <- X_{J_k(b)} o X_b and
+// V_b <- V_b + V_{J_k(b)} with J_k the 2^k-th ancestor, four rounds for chains of up to 16 bodies
+// (log depth instead of a chain walk per body). X = (q, p): (qa, pa) o (qb, pb) = (qa qb, pa + Ra pb).
+// Joint axes S (lane = dof) follow from the world poses.
 HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
     const BodyTopo& T = L.T;
-    if (lane < NB) {
-        if (lane == 0) {
-            L.ql[0][0] = L.root_q[0]; L.ql[0][1] = L.root_q[1]; L.ql[0][2] = L.root_q[2]; L.ql[0][3] = L.root_q[3];
-        } else {
-            int d = 3 * (lane - 1);
-            f4 q = qexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
-            L.ql[lane][0] = q.x; L.ql[lane][1] = q.y; L.ql[lane][2] = q.z; L.ql[lane][3] = q.w;
+    const bool act = lane < NB;
+    const int b = act ? lane : 0;
+    const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
+    f4 q;
+    f3 p;
+    float u[3];
+    if (b == 0) {
+        q = qnormalize(f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]});
+        p = o;
+        u[0] = L.u0[0]; u[1] = L.u0[1]; u[2] = L.u0[2];
+    } else {
+        const int d = 3 * (b - 1);
+        q = qexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
+        p = f3{T.local_pos[b][0], T.local_pos[b][1], T.local_pos[b][2]};
+        u[0] = L.u0[6 + d]; u[1] = L.u0[7 + d]; u[2] = L.u0[8 + d];
+    }
+    auto jump = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        const int j = act ? jump_of<K>(b) : -1;
+        const int src = j < 0 ? lane : j;
+        const f4 qa = f4{__shfl(q.x, src, W), __shfl(q.y, src, W), __shfl(q.z, src, W), __shfl(q.w, src, W)};
+        const f3 pa = f3{__shfl(p.x, src, W), __shfl(p.y, src, W), __shfl(p.z, src, W)};
+        if (j >= 0) {
+            p = pa + qapply(qa, p);
+            q = qmul(qa, q);
         }
+    };
+    jump(std::integral_constant<int, 0>{});
+    jump(std::integral_constant<int, 1>{});
+    jump(std::integral_constant<int, 2>{});
+    jump(std::integral_constant<int, 3>{});
+    // own joint's velocity contribution: root (w0, v0 at o); joint b: (w, (p_b - o) x w), w = R_b u_b
+    float V[6];
+    if (b == 0) {
+        V[0] = u[0]; V[1] = u[1]; V[2] = u[2]; V[3] = L.u0[3]; V[4] = L.u0[4]; V[5] = L.u0[5];
+    } else {
+        const f3 w = qapply(q, f3{u[0], u[1], u[2]});
+        const f3 l = cross3(p - o, w);
+        V[0] = w.x; V[1] = w.y; V[2] = w.z; V[3] = l.x; V[4] = l.y; V[5] = l.z;
+    }
+    auto vjump = [&](auto kc) {
+        constexpr int K = decltype(kc)::value;
+        const int j = act ? jump_of<K>(b) : -1;
+        const int src = j < 0 ? lane : j;
+        float Va[6];
+#pragma unroll
+        for (int x = 0; x < 6; ++x) Va[x] = __shfl(V[x], src, W);
+        if (j >= 0)
+#pragma unroll
+            for (int x = 0; x < 6; ++x) V[x] += Va[x];
+    };
+    vjump(std::integral_constant<int, 0>{});
+    vjump(std::integral_constant<int, 1>{});
+    vjump(std::integral_constant<int, 2>{});
+    vjump(std::integral_constant<int, 3>{});
+    if (act) {
+        L.qw[b][0] = q.x; L.qw[b][1] = q.y; L.qw[b][2] = q.z; L.qw[b][3] = q.w;
+        L.pw[b][0] = p.x; L.pw[b][1] = p.y; L.pw[b][2] = p.z;
+        for (int x = 0; x < 6; ++x) L.V[b][x] = V[x];
     }
     sync();
-    if (lane < NB) {  // walk this body's chain from the root
-        f4 q = qnormalize(f4{L.ql[0][0], L.ql[0][1], L.ql[0][2], L.ql[0][3]});
-        f3 p = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
-        int depth = T.depth[lane];
-        for (int k = 1; k <= depth; ++k) {
-            int a = T.chain[lane][k];
-            p = p + qapply(q, f3{T.local_pos[a][0], T.local_pos[a][1], T.local_pos[a][2]});
-            q = qmul(q, f4{L.ql[a][0], L.ql[a][1], L.ql[a][2], L.ql[a][3]});
-        }
-        L.qw[lane][0] = q.x; L.qw[lane][1] = q.y; L.qw[lane][2] = q.z; L.qw[lane][3] = q.w;
-        L.pw[lane][0] = p.x; L.pw[lane][1] = p.y; L.pw[lane][2] = p.z;
-    }
-    sync();
-    f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
     for (int i = lane; i < NG; i += W) {
         float* S = L.S[i];
         if (i < 6) {
             for (int c = 0; c < 6; ++c) S[c] = (c == i) ? 1.f : 0.f;
         } else {
-            int b = dof_body(i), c = (i - 6) % 3;
-            f4 q = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
+            int bb = dof_body(i), c = (i - 6) % 3;
+            f4 qb = f4{L.qw[bb][0], L.qw[bb][1], L.qw[bb][2], L.qw[bb][3]};
             f3 e = c == 0 ? f3{1.f, 0.f, 0.f} : (c == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
-            f3 a = qapply(q, e);
-            f3 l = cross3(f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} - o, a);
-            S[0] = a.x; S[1] = a.y; S[2] = a.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
+            f3 ax = qapply(qb, e);
+            f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]} - o, ax);
+            S[0] = ax.x; S[1] = ax.y; S[2] = ax.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
         }
-    }
-    sync();
-    if (lane < NB) {
-        float V[6] = {L.u0[0], L.u0[1], L.u0[2], L.u0[3], L.u0[4], L.u0[5]};
-        int depth = T.depth[lane];
-        for (int k = 1; k <= depth; ++k) {
-            int a = T.chain[lane][k];
-            int d0 = T.dof0[a];
-            for (int c = 0; c < 3; ++c) {
-                float uu = L.u0[d0 + c];
-                for (int x = 0; x < 6; ++x) V[x] += L.S[d0 + c][x] * uu;
-            }
-        }
-        for (int x = 0; x < 6; ++x) L.V[lane][x] = V[x];
     }
     sync();
 }
@@ -770,20 +819,24 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 }
             }
         }
+        // rank among this body's candidates: box corners by depth, ties (and sphere / capsule end
+        // points, keyed 0) by index; one comparison per unordered pair serves both ranks
         int rank[8];
+        float key[8];
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) { rank[ci] = 0; key[ci] = gt == HE_GEOM_BOX ? cd[ci] : 0.f; }
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci)
+#pragma unroll
+            for (int cj = ci + 1; cj < 8; ++cj) {
+                const bool j_first = key[cj] < key[ci];  // else i goes first (i < j breaks ties)
+                rank[ci] += (cand[cj] && j_first) ? 1 : 0;
+                rank[cj] += (cand[ci] && !j_first) ? 1 : 0;
+            }
         int myn = 0;
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) {
-            int rk = 0;
-#pragma unroll
-            for (int cj = 0; cj < 8; ++cj) {
-                // box corners by depth; sphere / capsule end points in geometric order
-                bool before = gt == HE_GEOM_BOX ? (cd[cj] < cd[ci] || (cd[cj] == cd[ci] && cj < ci)) : cj < ci;
-                if (cand[cj] && before) ++rk;
-            }
-            rank[ci] = rk;
-            if (cand[ci] && rk < 4) ++myn;
-        }
+        for (int ci = 0; ci < 8; ++ci)
+            if (cand[ci] && rank[ci] < 4) ++myn;
         int incl = myn;
         for (int s2 = 1; s2 < W; s2 <<= 1) {
             int v = __shfl_up(incl, s2, W);
