@@ -561,7 +561,8 @@ HE_DEV int jump_of(int b) {  // kJumpT.j[K][b] as a select chain (no runtime-ind
 // V_b <- V_b + V_{J_k(b)} with J_k the 2^k-th ancestor, four rounds for chains of up to 16 bodies
 // (log depth instead of a chain walk per body). X = (q, p): (qa, pa) o (qb, pb) = (qa qb, pa + Ra pb).
 // Joint axes S (lane = dof) follow from the world poses.
-HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
+template <bool ACC>
+HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params& sp) {
     const BodyTopo& T = L.T;
     const bool act = lane < NB;
     const int b = act ? lane : 0;
@@ -603,6 +604,9 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
         const f3 l = cross3(p - o, w);
         V[0] = w.x; V[1] = w.y; V[2] = w.z; V[3] = l.x; V[4] = l.y; V[5] = l.z;
     }
+    float vj[6];  // the joint's own velocity S_b u_b (RNEA velocity-product term below)
+#pragma unroll
+    for (int x = 0; x < 6; ++x) vj[x] = V[x];
     auto vjump = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
         const int j = act ? jump_of<K>(b) : -1;
@@ -622,6 +626,36 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane) {
         L.qw[b][0] = q.x; L.qw[b][1] = q.y; L.qw[b][2] = q.z; L.qw[b][3] = q.w;
         L.pw[b][0] = p.x; L.pw[b][1] = p.y; L.pw[b][2] = p.z;
         for (int x = 0; x < 6; ++x) L.V[b][x] = V[x];
+    }
+    if constexpr (ACC) {
+        // RNEA bias acceleration (gravity as base acceleration): a_b = a_0 + sum over the chain's
+        // joints j of V_j x (S_j u_j), the same prefix over the tree by pointer jumping. The base:
+        // (0, v0 x w0 - g) for the free root (u = [w0, v0 at o]).
+        float A[6];
+        if (b == 0) {
+            const f3 vxw = cross3(f3{L.u0[3], L.u0[4], L.u0[5]}, f3{L.u0[0], L.u0[1], L.u0[2]});
+            A[0] = 0.f; A[1] = 0.f; A[2] = 0.f;
+            A[3] = vxw.x - sp.gravity[0]; A[4] = vxw.y - sp.gravity[1]; A[5] = vxw.z - sp.gravity[2];
+        } else {
+            crm(V, vj, A);
+        }
+        auto ajump = [&](auto kc) {
+            constexpr int K = decltype(kc)::value;
+            const int j = act ? jump_of<K>(b) : -1;
+            const int src = j < 0 ? lane : j;
+            float Aa[6];
+#pragma unroll
+            for (int x = 0; x < 6; ++x) Aa[x] = __shfl(A[x], src, W);
+            if (j >= 0)
+#pragma unroll
+                for (int x = 0; x < 6; ++x) A[x] += Aa[x];
+        };
+        ajump(std::integral_constant<int, 0>{});
+        ajump(std::integral_constant<int, 1>{});
+        ajump(std::integral_constant<int, 2>{});
+        ajump(std::integral_constant<int, 3>{});
+        if (act)
+            for (int x = 0; x < 6; ++x) L.Acc[b][x] = A[x];
     }
     sync();
     for (int i = lane; i < NG; i += W) {
@@ -663,7 +697,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     const BodyTopo& T = L.T;
     const he_sim_params& p = a.p;
     const float dt = p.dt;
-    kinematics(L, m, lane);
+    kinematics<true>(L, m, lane, a.p);
     STAMP(0);
     const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
     // ---- body spatial inertias about o + RNEA body forces (gravity as base acceleration)
@@ -692,23 +726,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         float* o10 = L.Ic[b];  // own inertia; the subtree sums accumulate in place
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
-        float Acc[6];
-        f3 vxw = cross3(f3{L.u0[3], L.u0[4], L.u0[5]}, f3{L.u0[0], L.u0[1], L.u0[2]});
-        Acc[0] = 0.f; Acc[1] = 0.f; Acc[2] = 0.f;
-        Acc[3] = vxw.x - p.gravity[0]; Acc[4] = vxw.y - p.gravity[1]; Acc[5] = vxw.z - p.gravity[2];
-        int depth = T.depth[b];
-        for (int k = 1; k <= depth; ++k) {
-            int ab = T.chain[b][k];
-            int d0 = T.dof0[ab];
-            for (int c = 0; c < 3; ++c) {
-                float cr[6];
-                crm(L.V[ab], L.S[d0 + c], cr);
-                float uu = L.u0[d0 + c];
-                for (int x = 0; x < 6; ++x) Acc[x] += cr[x] * uu;
-            }
-        }
         float IA[6], IV[6], X[6];
-        si_apply(o10, Acc, IA);
+        si_apply(o10, L.Acc[b], IA);
         si_apply(o10, L.V[b], IV);
         crf(L.V[b], IV, X);
         for (int x = 0; x < 6; ++x) L.F[b][x] = IA[x] + X[x];  // body force f_b (accumulated in place)
@@ -1118,7 +1137,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     unsigned long long t_prev = __builtin_readcyclecounter();
     for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev);
     // ---- outputs: generalized state, FK rigid-body state, forces
-    kinematics(L, m, lane);
+    kinematics<false>(L, m, lane, a.p);
     STAMP(13);
     float* rso = a.root_states + (size_t)e * 13;
     if (lane < 3) { rso[lane] = L.root_pos[lane]; rso[7 + lane] = L.u0[3 + lane]; rso[10 + lane] = L.u0[lane]; }
