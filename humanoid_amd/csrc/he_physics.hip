@@ -775,19 +775,31 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
+    // with the free-velocity right-hand side y = L^-T (dt*rhs) carried through the elimination
+    float yl = L.rhs[lane], y2 = lane < NH ? L.rhs[64 + lane] : 0.f;
     {
         float Dl = 1.f, D2 = 1.f;
-        factor_lds_steps<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0);
+        factor_lds_steps<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
+        yl *= 1.0f / Dl;
+        y2 = lane < NH ? y2 * (1.0f / D2) : 0.f;
     }
     sync();
     STAMP(5);
-    // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs)
+    // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs): the L^-1 sweep
     {
-        float yl = L.rhs[lane], y2 = lane < NH ? L.rhs[64 + lane] : 0.f;
-        joint_space_solve(L, yl, y2, lane);
+        float r1[regla::kRowRegs], r2[regla::kRowRegs];
+        const float4* p1 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane]);
+        const float4* p2 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane < NH ? 64 + lane : 0]);
+#pragma unroll
+        for (int q = 0; q < regla::kRowRegs / 4; ++q) {
+            const float4 a1 = p1[q], a2 = p2[q];
+            r1[4 * q] = a1.x; r1[4 * q + 1] = a1.y; r1[4 * q + 2] = a1.z; r1[4 * q + 3] = a1.w;
+            r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
+        }
+        regla::solve_L_rows<0>(r1, r2, yl, y2);
         L.uf[lane] = L.u0[lane] + yl;
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
     }

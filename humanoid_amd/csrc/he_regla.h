@@ -346,7 +346,8 @@ __device__ __forceinline__ void fac_anc_row(RegMat& M, const Row<D>& row, float 
     }
 }
 template <int S>
-__device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2) {
+__device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2,
+                                                 float& yl, float& y2) {
     if constexpr (S < NG) {
         constexpr int K = kElimOrder[S];
         constexpr int D = kDofNanc[K] - 1;
@@ -358,10 +359,19 @@ __device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2
         if constexpr (K >= 64) M.c2[K - 64] = t2 * inv;
         if constexpr (D > 0) {
             constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-            if (lanes<lo>()) Lp[kPackStart[K] + dj] = M.c[K];
+            // forward substitution of the right-hand side fused in (y = L^-T rhs, the same
+            // deepest-first order): y[K] is final once K's descendants are eliminated
+            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
+            if (lanes<lo>()) {
+                Lp[kPackStart[K] + dj] = M.c[K];
+                yl = yl - M.c[K] * yk;
+            }
             if constexpr (K > 64) {
                 constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-                if (lanes<hi>()) Lp[kPackStart[K] + dj2] = M.c2[K - 64];
+                if (lanes<hi>()) {
+                    Lp[kPackStart[K] + dj2] = M.c2[K - 64];
+                    y2 = y2 - M.c2[K - 64] * yk;
+                }
             }
             const auto row = load_row<K>(Lp, kPackStart[K]);  // in-order LDS: sees the writes above
             fac_anc_row<K, 0, D>(M, row, t, t2);
@@ -369,7 +379,7 @@ __device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2
         if constexpr (K < 64) Dl = wrlane<K>(dk, Dl);
         else D2 = wrlane<K - 64>(dk, D2);
         __builtin_amdgcn_sched_barrier(0);
-        factor_lds_steps<S + 1>(M, Dl, D2, Lp, dj, dj2);
+        factor_lds_steps<S + 1>(M, Dl, D2, Lp, dj, dj2, yl, y2);
     }
 }
 
