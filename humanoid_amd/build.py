@@ -14,7 +14,7 @@ ARCH = os.environ.get("HE_OFFLOAD_ARCH", "gfx950")
 # reference's torch ops do (no FMA contraction); the physics kernel may contract.
 SOURCES = [
     ("he_imitation.hip", ["-ffp-contract=off"]),
-    ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]),
+    ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]),
     ("he_ingest.hip", []),
     ("he_rollout.hip", ["-ffp-contract=off"]),  # GAE: the Cython module's float32 rounding
     ("he_engine.cpp", ["-x", "hip"]),
