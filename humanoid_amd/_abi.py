@@ -158,3 +158,12 @@ class HeEvalBuffers(C.Structure):
     _fields_ = [("num_steps", C.c_void_p), ("mpjpe", C.c_void_p), ("body_pos", C.c_void_p),
                 ("body_pos_gt", C.c_void_p), ("history", C.c_void_p), ("sums", C.c_void_p),
                 ("frame", C.c_int32), ("reserved", C.c_int32)]
+
+
+AMP_OBS_STEP = 196  # include/humanoid_engine.h HE_AMP_OBS_STEP
+
+
+class HeAmpBuffers(C.Structure):
+    """include/humanoid_engine.h he_amp_buffers (device pointers)."""
+    _fields_ = [("amp_obs", C.c_void_p), ("amp_obs_demo", C.c_void_p), ("num_steps", C.c_int32),
+                ("reserved", C.c_int32)]

@@ -68,6 +68,8 @@ struct he_engine {
     bool has_pd = false;
     he_eval_buffers eval{};
     int has_eval = 0;
+    he_amp_buffers amp{};
+    int has_amp = 0;
     // motion library
     float *m_hot = nullptr, *m_cold = nullptr, *m_lengths = nullptr, *m_dt = nullptr;
     int64_t *m_starts = nullptr, *m_nframes = nullptr;
@@ -200,7 +202,7 @@ int he_set_dof_targets(he_engine* h, const float* src, void* stream) {
 }
 
 namespace {
-__global__ void copy_rows_kernel(float* dst, const float* src, const int32_t* ids, int k, int row, int num_rows) {
+static __global__ void copy_rows_kernel(float* dst, const float* src, const int32_t* ids, int k, int row, int num_rows) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= k * row) return;
     int i = t / row, c = t - i * row;
@@ -209,7 +211,7 @@ __global__ void copy_rows_kernel(float* dst, const float* src, const int32_t* id
     dst[(size_t)id * row + c] = src[(size_t)id * row + c];
 }
 
-int copy_rows(float* dst, const float* src, const int32_t* ids, int k, int row, int num_rows, void* stream,
+static int copy_rows(float* dst, const float* src, const int32_t* ids, int k, int row, int num_rows, void* stream,
               const char* what) {
     if (!src || !ids) return fail("%s: null argument", what);
     if (k < 0) return fail("%s: negative count", what);
@@ -261,7 +263,7 @@ int he_set_pd_params(he_engine* h, const float* host_offset, const float* host_s
 }
 
 namespace {
-PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
+static PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
     PhysArgs a{};
     a.p = h->params;
     a.model = h->d_model;
@@ -433,11 +435,11 @@ int he_ingest_clips(he_engine* h, int num_clips, const int64_t* host_num_frames,
 }
 
 namespace {
-MotionDev motion_dev(he_engine* h) {
+static MotionDev motion_dev(he_engine* h) {
     return MotionDev{h->m_hot, h->m_cold, h->m_starts, h->m_nframes, h->m_lengths, h->m_dt, h->m_motions};
 }
 
-int imit_common(he_engine* h, const he_imitation_params* p, const he_env_motion* em, ImitArgs& a, const char* what) {
+static int imit_common(he_engine* h, const he_imitation_params* p, const he_env_motion* em, ImitArgs& a, const char* what) {
     if (!h || !p || !em) return fail("%s: null argument", what);
     if (!h->num_envs) return fail("%s: no envs", what);
     if (!h->m_motions) return fail("%s: call he_load_motions first", what);
@@ -461,6 +463,23 @@ int imit_common(he_engine* h, const he_imitation_params* p, const he_env_motion*
     a.has_eval = h->has_eval;
     return 0;
 }
+// the AMP update that follows an imitation launch (he_set_amp)
+static hipError_t amp_after(he_engine* h, const ImitArgs& ia, int mode, hipStream_t stream) {
+    if (!h->has_amp) return hipSuccess;
+    AmpArgs a{};
+    a.m = ia.m;
+    a.rb_state = h->rb;
+    a.dof_state = h->dof_state;
+    a.motion_ids = ia.motion_ids;
+    a.start_times = ia.start_times;
+    a.reset = ia.reset;
+    a.env_ids = ia.env_ids;
+    a.count = ia.count;
+    a.mode = mode;
+    a.control_dt = ia.p.control_dt;
+    a.amp = h->amp;
+    return launch_amp(a, stream);
+}
 }  // namespace
 
 int he_imitation_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, float* obs, float* rew,
@@ -472,6 +491,7 @@ int he_imitation_step(he_engine* h, const he_imitation_params* p, const he_env_m
     a.count = h->num_envs;
     a.mode = 0;
     HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    HE_CHECK(amp_after(h, a, 0, (hipStream_t)stream));
     return 0;
 }
 
@@ -501,6 +521,7 @@ int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motio
     a.phases = phases;
     a.mode = 2;
     HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    HE_CHECK(amp_after(h, a, 2, (hipStream_t)stream));
     return 0;
 }
 
@@ -523,6 +544,38 @@ int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he
     a.seed = seed;
     a.step = step_index;
     HE_CHECK(launch_imitation(a, (hipStream_t)stream));
+    HE_CHECK(amp_after(h, a, 1, (hipStream_t)stream));
+    return 0;
+}
+
+int he_set_amp(he_engine* h, const he_amp_buffers* b) {
+    if (!h) return fail("he_set_amp: null engine");
+    if (!b) {
+        h->has_amp = 0;
+        return 0;
+    }
+    if (!b->amp_obs) return fail("he_set_amp: amp_obs is required");
+    if (b->num_steps < 1 || b->num_steps > HE_AMP_MAX_STEPS)
+        return fail("he_set_amp: num_steps must be in [1, %d]", HE_AMP_MAX_STEPS);
+    if ((reinterpret_cast<uintptr_t>(b->amp_obs) | reinterpret_cast<uintptr_t>(b->amp_obs_demo)) & 15)
+        return fail("he_set_amp: buffers must be 16-byte aligned");
+    h->amp = *b;
+    h->has_amp = 1;
+    return 0;
+}
+
+int he_amp_observations(int k, const float* root_pos, const float* root_rot, const float* root_vel,
+                        const float* root_ang_vel, const float* dof_pos, const float* dof_vel,
+                        const float* key_body_pos, float* out, void* stream) {
+    if (k < 0) return fail("he_amp_observations: negative count");
+    if (k == 0) return 0;
+    if (!root_pos || !root_rot || !root_vel || !root_ang_vel || !dof_pos || !dof_vel || !key_body_pos || !out)
+        return fail("he_amp_observations: null argument");
+    AmpArgs a{};
+    a.count = k;
+    a.root_pos = root_pos; a.root_rot = root_rot; a.root_vel = root_vel; a.root_ang_vel = root_ang_vel;
+    a.dof_pos = dof_pos; a.dof_vel = dof_vel; a.key_pos = key_body_pos; a.out = out;
+    HE_CHECK(launch_amp_function(a, (hipStream_t)stream));
     return 0;
 }
 

@@ -451,6 +451,149 @@ __global__ void __launch_bounds__(256) motion_state_kernel(MotionStateArgs a) {
     }
 }
 
+
+// ---------------- AMP observations ---------------------------------------------
+// Per body: the AMP dof-subset slot of its joint (humanoid_phc.py:186-194: joints outside
+// REMOVE_NAMES, in DOF_NAMES order) and its key-body slot (KEY_BODIES, body_sets.py:45).
+__constant__ int8_t kAmpSub[NB] = {-1, 0, 1, 2, -1, 3, 4, 5, -1, 6, 7, 8, 9, 10, 11, 12, 13, 14, -1, 15, 16, 17, 18, -1};
+__constant__ int8_t kAmpKey[NB] = {-1, -1, -1, 1, -1, -1, -1, 0, -1, -1, -1, -1, -1, -1, -1, -1, -1, 3, -1, -1, -1, -1, 2, -1};
+constexpr int AMP_W = HE_AMP_OBS_STEP;
+constexpr int AMP_J = 19;  // kept joints
+static_assert(13 + 9 * AMP_J + 3 * 4 == AMP_W, "AMP row layout");
+
+// build_amp_observations_smpl (common.py:191-267) for one row; lane b holds body b's position
+// (read on the root and key lanes), the root lane its rotation and velocities, lane b >= 1 its
+// joint's exp map and dof velocity. Writes to o (and o2 when non-null).
+HE_DEV void amp_row(float* o, float* o2, int lane, bool act, f3 pos, f4 rot, f3 vel, f3 ang, f3 dpos, f3 dvel) {
+    const f3 rp = f3{bcast0(pos.x), bcast0(pos.y), bcast0(pos.z)};
+    const f4 rq = f4{bcast0(rot.x), bcast0(rot.y), bcast0(rot.z), bcast0(rot.w)};
+    const f4 hinv = heading_quat(-calc_heading(rq));  // calc_heading_quat_inv, upright start
+    float v[13];
+    int n = 0, at = 0;
+    if (lane == 0) {
+        float tn[6];
+        tan_norm(qmul_ref(hinv, rq), tn);  // local_root_obs
+        const f3 lv = qrot_ref(hinv, vel), la = qrot_ref(hinv, ang);
+        v[0] = rp.z;
+        for (int c = 0; c < 6; ++c) v[1 + c] = tn[c];
+        v[7] = lv.x; v[8] = lv.y; v[9] = lv.z; v[10] = la.x; v[11] = la.y; v[12] = la.z;
+        n = 13;
+    }
+    const int sub = act ? kAmpSub[lane] : -1;
+    const int key = act ? kAmpKey[lane] : -1;
+    if (n) {
+        for (int c = 0; c < 13; ++c) { o[at + c] = v[c]; if (o2) o2[at + c] = v[c]; }
+    }
+    if (sub >= 0) {  // dof_to_obs_smpl (common.py:179-188) and the dof velocity subset
+        float tn[6];
+        tan_norm(exp_map_to_quat_ref(dpos), tn);
+        const int d = 13 + 6 * sub, w = 13 + 6 * AMP_J + 3 * sub;
+        for (int c = 0; c < 6; ++c) { o[d + c] = tn[c]; if (o2) o2[d + c] = tn[c]; }
+        const float dv[3] = {dvel.x, dvel.y, dvel.z};
+        for (int c = 0; c < 3; ++c) { o[w + c] = dv[c]; if (o2) o2[w + c] = dv[c]; }
+    }
+    if (key >= 0) {  // key-body positions in the heading frame
+        const f3 lk = qrot_ref(hinv, pos - rp);
+        const int k = 13 + 9 * AMP_J + 3 * key;
+        const float kv[3] = {lk.x, lk.y, lk.z};
+        for (int c = 0; c < 3; ++c) { o[k + c] = kv[c]; if (o2) o2[k + c] = kv[c]; }
+    }
+}
+
+// _update_hist_amp_obs shift (humanoid_phc.py:1341-1347) of one env's rows 0..S-2 to 1..S-1 by a
+// 32-lane group, as float4 (rows are 784 B). Every load of a chunk precedes its stores; chunks go
+// from the top down, and the shift (49 float4) exceeds a chunk (32), so no chunk reads what an
+// earlier chunk wrote.
+HE_DEV void amp_shift(float* buf, int S, int lane) {
+    const int n4 = (S - 1) * (AMP_W / 4);
+    float4* p = reinterpret_cast<float4*>(buf);
+    constexpr int SH = AMP_W / 4;
+    if (n4 <= 16 * GROUP) {  // S <= 11: every value in registers first
+        float4 r[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int idx = i * GROUP + lane;
+            if (idx < n4) r[i] = p[idx];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int idx = i * GROUP + lane;
+            if (idx < n4) p[idx + SH] = r[i];
+        }
+    } else {
+        for (int base = ((n4 - 1) / GROUP) * GROUP; base >= 0; base -= GROUP) {
+            const int idx = base + lane;
+            float4 r;
+            if (idx < n4) r = p[idx];
+            if (idx < n4) p[idx + SH] = r;
+        }
+    }
+}
+
+// One 32-lane group per (env, row): row 0's group does the history shift (envs that continue) and
+// writes the current row; for envs reset by the preceding launch, the group of row k >= 1 writes the
+// motion row k, so the S-1 motion samples of a reset env run in parallel instead of in series.
+__global__ void __launch_bounds__(256) amp_kernel(AmpArgs a) {
+    const int lane = threadIdx.x & (GROUP - 1);
+    const int S = a.amp.num_steps;
+    const int gid = (blockIdx.x * blockDim.x + threadIdx.x) / GROUP;
+    const int slot = gid / S, k = gid - slot * S;
+    if (slot >= a.count) return;  // whole 32-lane group leaves together
+    const int e = a.env_ids ? a.env_ids[slot] : slot;
+    const bool init = a.mode == 2 || (a.mode == 1 && a.reset[e]);
+    if (k > 0 && !init) return;
+    const bool act = lane < NB;
+    const int b = act ? lane : 0;
+    float* row = a.amp.amp_obs + ((size_t)e * S + k) * AMP_W;
+    float* demo = (init && a.amp.amp_obs_demo) ? a.amp.amp_obs_demo + ((size_t)e * S + k) * AMP_W : nullptr;
+    if (k == 0) {
+        if (!init && S > 1) amp_shift(row, S, lane);
+        // _compute_amp_observations from the simulated (or just reset) state
+        const SimBody s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);
+        f3 dp = f3{0.f, 0.f, 0.f}, dv = f3{0.f, 0.f, 0.f};
+        if (act && b > 0) {
+            const float* ds = a.dof_state + ((size_t)e * ND + 3 * (b - 1)) * 2;
+            dp = f3{ds[0], ds[2], ds[4]};
+            dv = f3{ds[1], ds[3], ds[5]};
+        }
+        amp_row(row, demo, lane, act, s.pos, s.rot, s.vel, s.ang, dp, dv);
+        return;
+    }
+    // _init_amp_obs_ref: the motion at t - k*dt without offset (humanoid_phc.py:805-838)
+    const int64_t mid = clamp_mid(a.m, a.motion_ids[e]);
+    const float t = a.start_times[e] + (-a.control_dt) * (float)k;
+    const FrameSel fs = frame_select(a.m, mid, t);
+    const BodyRef r = body_ref(a.m, fs, b, f3{0.f, 0.f, 0.f});
+    f3 mp = f3{0.f, 0.f, 0.f}, mv = f3{0.f, 0.f, 0.f};
+    if (act && b > 0) body_dof_ref(a.m, fs, b, mp, mv);
+    amp_row(row, demo, lane, act, r.pos, r.rot, r.vel, r.ang, mp, mv);
+}
+
+// he_amp_observations: explicit inputs, one 32-lane group per row
+__global__ void __launch_bounds__(256) amp_function_kernel(AmpArgs a) {
+    const int lane = threadIdx.x & (GROUP - 1);
+    const int q = (blockIdx.x * blockDim.x + threadIdx.x) / GROUP;
+    if (q >= a.count) return;
+    const bool act = lane < NB;
+    f3 pos = f3{0.f, 0.f, 0.f}, vel = pos, ang = pos, dp = pos, dv = pos;
+    f4 rot = f4{0.f, 0.f, 0.f, 1.f};
+    if (lane == 0) {
+        pos = f3{a.root_pos[3 * q], a.root_pos[3 * q + 1], a.root_pos[3 * q + 2]};
+        rot = f4{a.root_rot[4 * q], a.root_rot[4 * q + 1], a.root_rot[4 * q + 2], a.root_rot[4 * q + 3]};
+        vel = f3{a.root_vel[3 * q], a.root_vel[3 * q + 1], a.root_vel[3 * q + 2]};
+        ang = f3{a.root_ang_vel[3 * q], a.root_ang_vel[3 * q + 1], a.root_ang_vel[3 * q + 2]};
+    } else if (act) {
+        const int key = kAmpKey[lane];
+        if (key >= 0) {
+            const float* kp = a.key_pos + ((size_t)q * 4 + key) * 3;
+            pos = f3{kp[0], kp[1], kp[2]};
+        }
+        const size_t d = (size_t)q * ND + 3 * (lane - 1);
+        dp = f3{a.dof_pos[d], a.dof_pos[d + 1], a.dof_pos[d + 2]};
+        dv = f3{a.dof_vel[d], a.dof_vel[d + 1], a.dof_vel[d + 2]};
+    }
+    amp_row(a.out + (size_t)q * AMP_W, nullptr, lane, act, pos, rot, vel, ang, dp, dv);
+}
 }  // namespace
 
 hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream) {
@@ -466,5 +609,21 @@ hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream) {
     int threads = 256;
     int blocks = (a.k * GROUP + threads - 1) / threads;
     motion_state_kernel<<<blocks, threads, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_amp(const AmpArgs& a, hipStream_t stream) {
+    if (a.count <= 0) return hipSuccess;
+    int threads = 256;
+    int blocks = (int)(((int64_t)a.count * a.amp.num_steps * GROUP + threads - 1) / threads);
+    amp_kernel<<<blocks, threads, 0, stream>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_amp_function(const AmpArgs& a, hipStream_t stream) {
+    if (a.count <= 0) return hipSuccess;
+    int threads = 256;
+    int blocks = (a.count * GROUP + threads - 1) / threads;
+    amp_function_kernel<<<blocks, threads, 0, stream>>>(a);
     return hipGetLastError();
 }

@@ -50,6 +50,24 @@ struct ImitArgs {
     int has_eval;
 };
 
+// AMP observation update, launched after an imitation launch
+struct AmpArgs {
+    MotionDev m;
+    const float* rb_state;    // [N,24,13]
+    const float* dof_state;   // [N,69,2]
+    const int64_t* motion_ids;
+    const float* start_times;
+    const uint8_t* reset;     // mode 1: envs reset by the preceding launch
+    const int32_t* env_ids;   // mode 2: the reset envs; null = all envs [0, count)
+    int count;
+    int mode;                 // 0 step update, 1 step update or init by reset flag, 2 init listed envs
+    float control_dt;
+    he_amp_buffers amp;
+    // function-level form (he_amp_observations): explicit inputs, K rows into `out`
+    const float *root_pos, *root_rot, *root_vel, *root_ang_vel, *dof_pos, *dof_vel, *key_pos;
+    float* out;
+};
+
 struct MotionStateArgs {
     MotionDev m;
     int k;
@@ -84,6 +102,8 @@ struct PhysArgs {
 };
 
 hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream);
+hipError_t launch_amp(const AmpArgs& a, hipStream_t stream);
+hipError_t launch_amp_function(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream);
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);
 hipError_t launch_ingest(const float* pose, const float* trans, const int32_t* parents, const float* local_pos,

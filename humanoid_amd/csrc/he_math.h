@@ -70,6 +70,21 @@ HE_DEV f3 q_to_exp_map(f4 q) {
     return ax * a;
 }
 
+// torch_utils.py:334-365 exp_map_to_quat = exp_map_to_angle_axis + quat_from_angle_axis
+// (normalize and quat_unit clamp the norm at 1e-9), float32 in torch's operation order
+HE_DEV f4 exp_map_to_quat_ref(f3 e) {
+    float angle = sqrtf(e.x * e.x + e.y * e.y + e.z * e.z);
+    f3 axis = f3{e.x / angle, e.y / angle, e.z / angle};
+    angle = normalize_angle(angle);
+    if (!(fabsf(angle) > 1e-5f)) { angle = 0.0f; axis = f3{0.f, 0.f, 1.f}; }
+    float theta = angle / 2.0f;
+    float n = fmaxf(sqrtf(axis.x * axis.x + axis.y * axis.y + axis.z * axis.z), 1e-9f);
+    float st = sinf(theta);
+    f4 q = f4{axis.x / n * st, axis.y / n * st, axis.z / n * st, cosf(theta)};
+    float qn = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-9f);
+    return f4{q.x / qn, q.y / qn, q.z / qn, q.w / qn};
+}
+
 // torch_utils.py:109-131 in torch's float32 operation order (sequential dot product)
 HE_DEV f4 slerp_ref(f4 q0, f4 q1, float t) {
     float c = q0.x * q1.x;

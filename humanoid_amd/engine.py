@@ -31,6 +31,7 @@ HE_SYMBOLS = (
     "he_set_dof_targets_indexed", "he_set_env_properties", "he_simulate", "he_set_pd_params", "he_step_actions",
     "he_refresh", "he_load_motions", "he_imitation_step", "he_motion_state", "he_reset_envs", "he_env_step",
     "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips", "he_set_eval",
+    "he_set_amp", "he_amp_observations",
     # include/humanoid_rollout.h
     "he_rollout_store", "he_rollout_order", "he_rollout_gather", "he_gae", "he_gae_minibatch",
 )
@@ -66,6 +67,8 @@ def load_library(path: Optional[str] = None):
         "he_device_count": [V],
         "he_set_debug_stamps": [V, V],
         "he_set_eval": [V, V],
+        "he_set_amp": [V, V],
+        "he_amp_observations": [I, V, V, V, V, V, V, V, V, V],
         "he_rollout_store": [V, V, I, C.c_int64, V, V, C.c_int64, C.c_int32, V],
         "he_rollout_order": [V, C.c_int64, V, I, V],
         "he_rollout_gather": [V, I, V, C.c_int64, C.c_int32, C.c_int32, C.c_int32, V],
@@ -358,6 +361,28 @@ class Engine:
         """Attach eval recording (he_set_eval; the struct is copied, call again per frame) or detach."""
         _check(self.lib.he_set_eval(self.h, None if buffers is None else C.byref(buffers)))
 
+    def set_amp(self, amp_obs, amp_obs_demo=None):
+        """Attach the AMP buffers (he_set_amp): ``amp_obs`` / ``amp_obs_demo`` f32 [N, S, 196]
+        device tensors (humanoid_phc.py:600-611), updated by every following imitation launch;
+        ``None`` detaches."""
+        import torch
+        if amp_obs is None:
+            self._amp = None
+            _check(self.lib.he_set_amp(self.h, None))
+            return
+        for t in (amp_obs, amp_obs_demo):
+            if t is None:
+                continue
+            self._contig(t, torch.float32)
+            if t.dim() != 3 or t.shape[0] != self.num_envs or t.shape[2] != _abi.AMP_OBS_STEP:
+                raise EngineError(f"AMP buffer has shape {tuple(t.shape)}, expected [{self.num_envs}, S, 196]")
+        if amp_obs_demo is not None and amp_obs_demo.shape != amp_obs.shape:
+            raise EngineError("amp_obs_demo must have the shape of amp_obs")
+        b = _abi.HeAmpBuffers(amp_obs.data_ptr(), None if amp_obs_demo is None else amp_obs_demo.data_ptr(),
+                              int(amp_obs.shape[1]), 0)
+        self._amp = (amp_obs, amp_obs_demo)  # keep alive while attached
+        _check(self.lib.he_set_amp(self.h, C.byref(b)))
+
     def set_debug_stamps(self, buf=None):
         """Diagnostics: int64 [num_envs, 16] device tensor receiving per-phase cycles, or None."""
         import torch
@@ -368,3 +393,22 @@ class Engine:
 
     def hash_uniform(self, seed, step, env):
         return self.lib.he_hash_uniform(seed, step, env)
+
+
+def amp_observations(root_pos, root_rot, root_vel, root_ang_vel, dof_pos, dof_vel, key_body_pos):
+    """build_amp_observations_smpl (envs/common.py:191-267) with the reference's constant flags on
+    device tensors (he_amp_observations): key_body_pos [K,4,3] in KEY_BODIES order -> [K,196]."""
+    import torch
+    lib = load_library()
+    k = int(root_pos.shape[0])
+    ins = (root_pos, root_rot, root_vel, root_ang_vel, dof_pos, dof_vel, key_body_pos)
+    shapes = ((k, 3), (k, 4), (k, 3), (k, 3), (k, 69), (k, 69), (k, 4, 3))
+    dev = root_pos.device
+    for t, sh in zip(ins, shapes):
+        if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous() or tuple(t.shape) != sh:
+            raise EngineError(f"he_amp_observations: expected contiguous f32 {sh} on {dev}, got "
+                              f"{t.dtype} {tuple(t.shape)} on {t.device}")
+    out = torch.empty(k, _abi.AMP_OBS_STEP, device=dev)
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    _check(lib.he_amp_observations(k, *[C.c_void_p(t.data_ptr()) for t in ins], C.c_void_p(out.data_ptr()), stream))
+    return out

@@ -66,6 +66,7 @@ class EnvConfig:  # config.py:89-157
     headless: bool = True
     clip_actions: bool = True
     use_amp_obs: bool = False
+    num_amp_obs_steps: int = 10
     enable_early_termination: bool = True
     termination_distance: float = 0.25
     max_episode_length: int = 300
@@ -122,8 +123,6 @@ class HumanoidPHC:
         from .motion_lib import MotionLibSMPL
         if cfg.device_type != "cuda":
             raise ValueError("the engine runs on the GPU only (device_type='cuda')")
-        if cfg.use_amp_obs:
-            raise NotImplementedError("AMP observations are out of scope (SURVEY §8f item 4)")
         if cfg.robot.reduce_action:
             raise NotImplementedError("reduce_action is off in the reference defaults and not supported")
         self.cfg = cfg
@@ -149,6 +148,15 @@ class HumanoidPHC:
         self.single_action_space = Box(-1.0, 1.0, (NUM_ACTIONS,))
         self.amp_observation_space = None
         dev = self.device
+        if cfg.use_amp_obs:  # AMP buffers (humanoid_phc.py:469-491, 600-611), updated by the engine
+            self._num_amp_obs_per_step = _abi.AMP_OBS_STEP
+            self.num_amp_obs = cfg.num_amp_obs_steps * self._num_amp_obs_per_step
+            self.amp_observation_space = Box(-np.inf, np.inf, (self.num_amp_obs,))
+            self._amp_obs_buf = torch.zeros(n, cfg.num_amp_obs_steps, self._num_amp_obs_per_step, device=dev)
+            self._curr_amp_obs_buf = self._amp_obs_buf[:, 0]
+            self._hist_amp_obs_buf = self._amp_obs_buf[:, 1:]
+            self._amp_obs_demo_buf = torch.zeros_like(self._amp_obs_buf)
+            self.engine.set_amp(self._amp_obs_buf, self._amp_obs_demo_buf)
         self.obs_buf = torch.zeros(n, NUM_OBS, device=dev)
         self.rew_buf = torch.zeros(n, device=dev)
         self.reward_raw = torch.zeros(n, 5, device=dev)
@@ -241,7 +249,17 @@ class HumanoidPHC:
                                    self._reset_u8, self._term_u8)
         self.extras["terminate"] = self._terminate_buf.clone()
         self.extras["reward_raw"] = self.reward_raw.detach()
+        if self.cfg.use_amp_obs:  # the launch above also shifted the history and wrote row 0 (:154-157)
+            self.extras["amp_obs"] = self.amp_obs
         return self.obs_buf, self.rew_buf, self.reset_buf, self.extras
+
+    # -- AMP (:1352-1357) --------------------------------------------------------------------
+    @property
+    def amp_obs(self):
+        return self._amp_obs_buf.view(-1, self.num_amp_obs) if self.cfg.use_amp_obs else None
+
+    def fetch_amp_obs_demo(self):
+        return self._amp_obs_demo_buf.view(-1, self.num_amp_obs) if self.cfg.use_amp_obs else None
 
     # -- motion sampling (:1363-1455) ------------------------------------------------------
     def resample_motions(self):
@@ -353,7 +371,8 @@ class PHCPufferEnv:
         self.env = HumanoidPHC(cfg, motion_data=motion_data)
         self.single_observation_space = self.env.single_observation_space
         self.single_action_space = self.env.single_action_space
-        self.amp_observation_space = None
+        self.amp_observation_space = self.env.amp_observation_space if cfg.use_amp_obs else None  # env.py:59
+        self.amp_obs = self.env.amp_obs if cfg.use_amp_obs else None  # env.py:94 (a live view)
         dev = self.env.device
         n = cfg.num_envs
         self.observations = self.env.obs_buf
@@ -402,6 +421,8 @@ class PHCPufferEnv:
                                       seed=self.cfg.seed, step_index=self.tick)
         e.extras["terminate"] = e._terminate_buf.clone()
         e.extras["reward_raw"] = e.reward_raw.detach()
+        if self.cfg.use_amp_obs:
+            e.extras["amp_obs"] = e.amp_obs
         rew = self.rewards.clone()
         self.raw_rewards += e.reward_raw.mean(dim=0)
         reset = e.reset_buf
@@ -433,6 +454,9 @@ class PHCPufferEnv:
             else:
                 info.append(reward_info)
         return self.observations, rew, self.terminals, self.truncations, info
+
+    def fetch_amp_obs_demo(self):  # env.py:206-207
+        return self.env.fetch_amp_obs_demo()
 
     def mean_and_log(self):
         s = self._acc.tolist()

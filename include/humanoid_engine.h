@@ -246,6 +246,42 @@ typedef struct he_eval_buffers {
 /* Attach (copied by value; call again each step with the new frame) or detach (NULL). */
 int he_set_eval(he_engine* h, const he_eval_buffers* buffers);
 
+/* ---------------- AMP observations (off by default, config.py:98) ------------ */
+/* One AMP row (humanoid_phc.py:471-476 with has_dof_subset): root height 1, root rotation
+ * tan-norm 6, local root velocity 3 and angular velocity 3, tan-norm of the 19 kept joints'
+ * exp maps 114, their dof velocities 57, key-body positions 12 (body_sets.py:42-45). */
+#define HE_AMP_OBS_STEP 196
+#define HE_AMP_MAX_STEPS 64
+
+/* _amp_obs_buf / _amp_obs_demo_buf (humanoid_phc.py:600-611), DEVICE pointers owned by the
+ * caller, f32 [N, num_steps, 196] contiguous and 16-byte aligned: row 0 is the current AMP
+ * observation, rows 1.. the history (the `amp_obs` [N, 1960] view the trainer stores,
+ * clean_pufferl/core.py:174). */
+typedef struct he_amp_buffers {
+    float* amp_obs;       /* required */
+    float* amp_obs_demo;  /* NULL to skip the demo copy */
+    int32_t num_steps;    /* cfg.num_amp_obs_steps (config.py:141), 1..HE_AMP_MAX_STEPS */
+    int32_t reserved;
+} he_amp_buffers;
+
+/* Attach (copied by value) or detach (NULL). While attached, every imitation launch is followed
+ * by the AMP launch on the same stream:
+ *  - he_imitation_step: _update_hist_amp_obs + _compute_amp_observations for every env
+ *    (humanoid_phc.py:154-157, 1125-1176, 1341-1347): rows shift by one, row 0 from the state;
+ *  - he_reset_envs: _init_amp_obs for the listed envs (humanoid_phc.py:665-676, 791-838):
+ *    row 0 from the reset state, row k from the env's motion at start_time - k*dt (no offset),
+ *    then amp_obs_demo[env] = amp_obs[env];
+ *  - he_imitation_reset_step / he_env_step: the step update for envs not reset in the launch,
+ *    the init for those that were. */
+int he_set_amp(he_engine* h, const he_amp_buffers* buffers);
+
+/* build_amp_observations_smpl (envs/common.py:191-267) with the flags humanoid_phc.py:1195-1210
+ * passes, on K device rows: root_pos/vel/ang_vel [K,3], root_rot [K,4], dof_pos/dof_vel [K,69],
+ * key_body_pos [K,4,3] (R_Ankle, L_Ankle, R_Wrist, L_Wrist) -> out [K,196]. No engine needed. */
+int he_amp_observations(int k, const float* root_pos, const float* root_rot, const float* root_vel,
+                        const float* root_ang_vel, const float* dof_pos, const float* dof_vel,
+                        const float* key_body_pos, float* out, void* stream);
+
 /* Diagnostics: when non-NULL, the physics kernel accumulates per-phase shader cycles into
  * device_buffer [N][16] (u64; phases listed in DESIGN.md §4). NULL disables (default). */
 int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer);

@@ -500,3 +500,43 @@ void ho_imitation_from_ref(const he_imitation_params* p, int n, const float* pos
         task_obs(&s, &m, obs_task + (size_t)i * HE_OBS_TASK);
     }
 }
+
+/* ------------------------------------------------------------------------------------- */
+/* AMP observations                                                          */
+/* ------------------------------------------------------------------------------------- */
+/* common.py:191-267 build_amp_observations_smpl with the constant flags humanoid_phc.py:1195-1210
+ * passes (local_root_obs, amp_root_height_obs, has_dof_subset and has_upright_start true; no shape
+ * or limb-weight obs), and dof_to_obs_smpl common.py:179-188. The dof subset is given as joint
+ * indices (humanoid_phc.py:186-194: the joints outside REMOVE_NAMES). One row per env:
+ * [root_h, tan_norm(h^-1 q_root) 6, h^-1 v_root 3, h^-1 w_root 3, tan_norm(exp(dof_j)) 6*J,
+ *  dof_vel 3*J, h^-1 (p_key - p_root) 3*K], K = 4 key bodies (body_sets.py:45). */
+void ho_amp_obs(int n, int num_joints, const int32_t* joints, int num_key, const float* root_pos,
+                const float* root_rot, const float* root_vel, const float* root_ang_vel, const float* dof_pos,
+                const float* dof_vel, const float* key_pos, float* out) {
+    const int width = 13 + 9 * num_joints + 3 * num_key;
+    for (int i = 0; i < n; ++i) {
+        R rp[3], rq[4], rv[3], ra[3], hinv[4], q[4], tn[6], r[3];
+        for (int c = 0; c < 3; ++c) { rp[c] = root_pos[3 * i + c]; rv[c] = root_vel[3 * i + c]; ra[c] = root_ang_vel[3 * i + c]; }
+        for (int c = 0; c < 4; ++c) rq[c] = root_rot[4 * i + c];
+        heading_quat(-calc_heading(rq), hinv);
+        float* o = out + (size_t)i * width;
+        o[0] = (float)rp[2];
+        q_mul(hinv, rq, q); q_tan_norm(q, tn);
+        for (int c = 0; c < 6; ++c) o[1 + c] = (float)tn[c];
+        q_rot(hinv, rv, r); for (int c = 0; c < 3; ++c) o[7 + c] = (float)r[c];
+        q_rot(hinv, ra, r); for (int c = 0; c < 3; ++c) o[10 + c] = (float)r[c];
+        for (int s = 0; s < num_joints; ++s) {
+            const int j = joints[s];
+            R e[3] = {dof_pos[(size_t)i * ND + 3 * j], dof_pos[(size_t)i * ND + 3 * j + 1], dof_pos[(size_t)i * ND + 3 * j + 2]};
+            exp_map_to_q(e, q); q_tan_norm(q, tn);
+            for (int c = 0; c < 6; ++c) o[13 + 6 * s + c] = (float)tn[c];
+            for (int c = 0; c < 3; ++c) o[13 + 6 * num_joints + 3 * s + c] = dof_vel[(size_t)i * ND + 3 * j + c];
+        }
+        for (int k = 0; k < num_key; ++k) {
+            R d[3];
+            for (int c = 0; c < 3; ++c) d[c] = (R)key_pos[((size_t)i * num_key + k) * 3 + c] - rp[c];
+            q_rot(hinv, d, r);
+            for (int c = 0; c < 3; ++c) o[13 + 9 * num_joints + 3 * k + c] = (float)r[c];
+        }
+    }
+}

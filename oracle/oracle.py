@@ -242,3 +242,65 @@ class HostExperience:
         self.b_returns = self.b_advantages + self.b_values
         self.returns = adv + self.values
         return adv
+
+
+# ------------------------------------------------------------------------- AMP obs (§8f-4)
+def amp_joints():
+    """Joint indices of the AMP dof subset (humanoid_phc.py:186-194) and key bodies (body_sets.py:45)."""
+    from humanoid_amd import body_sets as BS
+    joints = [i for i, n in enumerate(BS.DOF_NAMES) if n not in BS.REMOVE_NAMES]
+    return np.array(joints, np.int32), BS.body_ids(BS.KEY_BODIES)
+
+
+def amp_obs(root_pos, root_rot, root_vel, root_ang_vel, dof_pos, dof_vel, key_pos):
+    """build_amp_observations_smpl (common.py:191-267) with the reference's constant flags."""
+    joints, keys = amp_joints()
+    n = root_pos.shape[0]
+    out = np.zeros((n, 13 + 9 * len(joints) + 3 * len(keys)), np.float32)
+    lib().ho_amp_obs(C.c_int(n), C.c_int(len(joints)), _p(joints), C.c_int(len(keys)),
+                     *[_p(f32(a)) for a in (root_pos, root_rot, root_vel, root_ang_vel, dof_pos, dof_vel, key_pos)],
+                     _p(out))
+    return out
+
+
+def amp_obs_from_sim(rb_state, dof_state):
+    """_compute_amp_observations (humanoid_phc.py:1125-1176) on rb rows [N,24,13] / dof [N,69,2]."""
+    _, keys = amp_joints()
+    rb = np.asarray(rb_state, np.float32)
+    return amp_obs(rb[:, 0, 0:3], rb[:, 0, 3:7], rb[:, 0, 7:10], rb[:, 0, 10:13], dof_state[..., 0],
+                   dof_state[..., 1], rb[:, keys, 0:3])
+
+
+def amp_obs_from_motion(mt: MotionTables, ids, times):
+    """_get_amp_obs (humanoid_phc.py:821-838): motion state without offset -> AMP row."""
+    _, keys = amp_joints()
+    ms = motion_state(mt, ids, times, None)
+    return amp_obs(ms["rg_pos"][:, 0], ms["rb_rot"][:, 0], ms["body_vel"][:, 0], ms["body_ang_vel"][:, 0],
+                   ms["dof_pos"], ms["dof_vel"], ms["rg_pos"][:, keys])
+
+
+def amp_step(buf, rb_state, dof_state):
+    """_update_hist_amp_obs + _compute_amp_observations (humanoid_phc.py:154-157): history shift,
+    then the current row from the simulated state. buf [N,S,W] is returned updated (a copy)."""
+    out = np.array(buf, np.float32, copy=True)
+    out[:, 1:] = buf[:, :-1]
+    out[:, 0] = amp_obs_from_sim(rb_state, dof_state)
+    return out
+
+
+def amp_init(buf, demo, env_ids, rb_state, dof_state, mt: MotionTables, motion_ids, times, control_dt):
+    """_init_amp_obs for reference-state resets (humanoid_phc.py:791-819): row 0 from the reset
+    state, rows k >= 1 from the motion at t - k*dt (float32 ops as torch does them), then
+    demo[env] = buf[env]. Returns updated copies."""
+    buf = np.array(buf, np.float32, copy=True)
+    demo = np.array(demo, np.float32, copy=True)
+    ids = np.asarray(env_ids, np.int64)
+    S = buf.shape[1]
+    buf[ids, 0] = amp_obs_from_sim(np.asarray(rb_state)[ids], np.asarray(dof_state)[ids])
+    if S > 1:
+        steps = np.float32(-control_dt) * (np.arange(S - 1, dtype=np.float32) + np.float32(1))
+        t = (np.asarray(times, np.float32)[ids][:, None] + steps[None, :]).astype(np.float32)
+        mids = np.repeat(np.asarray(motion_ids, np.int64)[ids], S - 1)
+        buf[ids, 1:] = amp_obs_from_motion(mt, mids, t.reshape(-1)).reshape(len(ids), S - 1, -1)
+    demo[ids] = buf[ids]
+    return buf, demo

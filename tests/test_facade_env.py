@@ -200,3 +200,36 @@ def test_humanoid_phc_reset_and_step(model):
     assert hist.shape == (4,) and float(hist[1]) == 1.0
     env.resample_motions()
     assert torch.isfinite(env.obs_buf).all()
+
+
+@pytest.mark.gpu
+def test_puffer_env_amp_obs(model):
+    """use_amp_obs (config.py:98): the AMP buffers ride along the device step (clean_pufferl/env.py:94,
+    206-207; humanoid_phc.py:154-157, 665-676): [N, 1960] view, history shifted each step for envs
+    that continue, demo rows written for every reset env."""
+    from humanoid_amd.env import EnvConfig, PHCPufferEnv
+    n = 64
+    cfg = EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=5, use_amp_obs=True)
+    pe = PHCPufferEnv(cfg)
+    assert pe.amp_observation_space.shape == (1960,) and pe.amp_obs.shape == (n, 1960)
+    pe.reset()
+    demo = pe.fetch_amp_obs_demo()
+    assert demo.shape == (n, 1960)
+    # after the full reset every env's history comes from its motion and demo = buffer
+    assert torch.equal(demo, pe.amp_obs) and torch.isfinite(demo).all()
+    rng = np.random.default_rng(1)
+    prev = pe.amp_obs.view(n, 10, 196).clone()
+    n_reset = 0
+    for _ in range(12):
+        pe.step(rng.uniform(-1.5, 1.5, (n, 69)).astype(np.float32))
+        cur = pe.amp_obs.view(n, 10, 196)
+        reset = pe.env.reset_buf
+        keep = ~reset
+        assert torch.equal(cur[keep, 1:], prev[keep, :-1])
+        assert torch.equal(pe.env.extras["amp_obs"], pe.amp_obs)
+        if reset.any():
+            n_reset += int(reset.sum())
+            assert torch.equal(demo.view(n, 10, 196)[reset], cur[reset])
+        prev = cur.clone()
+    assert n_reset > 0
+    assert torch.isfinite(pe.amp_obs).all()

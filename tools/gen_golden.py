@@ -10,7 +10,8 @@ simulator is called: the env-level fixtures call ``HumanoidPHC._compute_reward``
 ``__new__`` whose state tensors are plain CPU tensors filled by this script.
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
-Writes: tests/golden/{quat_prims,skeleton,motion_lib,imitation_funcs,env_step,env_reset,pd_targets}.npz
+        PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py amp     (one part only)
+Writes: tests/golden/{quat_prims,skeleton,motion_lib,imitation_funcs,env_step,env_reset,pd_targets,amp}.npz
 """
 import os
 import sys
@@ -390,15 +391,116 @@ def gen_pd():
                         scale=t2n(env._pd_action_scale), actions=t2n(a), pd_target=t2n(pd))
 
 
+# --------------------------------------------------------------------------------- AMP obs (§8f-4)
+def amp_dof_subset():
+    # the index list HumanoidPHC._config_robot builds (humanoid_phc.py:186-194); that method also
+    # creates gym assets, so the list is formed here from the same body sets
+    idx = [np.arange(i * 3, (i + 1) * 3) for i, n in enumerate(BS.DOF_NAMES) if n not in BS.REMOVE_NAMES]
+    return torch.from_numpy(np.concatenate(idx))
+
+
+def gen_amp(tree, clips):
+    """build_amp_observations_smpl (common.py:191-267) on random states, and the env-level AMP
+    buffer flow: _update_hist_amp_obs + _compute_amp_observations after a step
+    (humanoid_phc.py:154-157, 1125-1176, 1341-1350), then _init_amp_obs for a reset subset
+    (:665-676, 791-838)."""
+    g = torch.Generator().manual_seed(13)
+    subset = amp_dof_subset()
+    # -- function level
+    N = 48
+    root_pos = torch.randn(N, 3, generator=g) * 0.5
+    root_pos[:, 2] += 0.9
+    root_rot = rand_quat(g, N)
+    root_vel = torch.randn(N, 3, generator=g)
+    root_ang_vel = torch.randn(N, 3, generator=g) * 2
+    dof_pos = torch.randn(N, 69, generator=g) * 1.2
+    dof_pos[0] = 0.0                                   # exp map of zero: the default-axis branch
+    dof_pos[1, :9] = 1e-7                              # below min_theta
+    dof_pos[2, :3] = torch.tensor([3.14159, 0.0, 0.0])  # ~pi
+    dof_pos[3, :3] = torch.tensor([0.0, 4.5, 0.0])      # > pi: normalize_angle wraps
+    dof_pos[4, :3] = torch.tensor([0.0, 0.0, -7.0])     # > 2 pi
+    dof_vel = torch.randn(N, 69, generator=g) * 3
+    key_pos = root_pos[:, None, :] + torch.randn(N, 4, 3, generator=g) * 0.6
+    shape = torch.zeros(N, 11)
+    limb = torch.zeros(N, 10)
+    amp = C.build_amp_observations_smpl(root_pos, root_rot, root_vel, root_ang_vel, dof_pos, dof_vel, key_pos,
+                                        shape, limb, subset, True, True, True, False, False, True)
+    out = dict(root_pos=root_pos, root_rot=root_rot, root_vel=root_vel, root_ang_vel=root_ang_vel,
+               dof_pos=dof_pos, dof_vel=dof_vel, key_pos=key_pos, dof_subset=subset, amp_obs=amp)
+    # -- env level
+    NE, S = 24, 10
+    sample = [i % 5 for i in range(NE)]
+    lib = build_motion_lib(tree, clips, sample)
+    env = fake_env(lib, tree, NE)
+    env.cfg.use_amp_obs = True
+    env.cfg.num_amp_obs_steps = S
+    env.cfg.state_init = StateInit.Random
+    env.dof_subset = subset
+    env._reset_default_env_ids = []
+    env._num_amp_obs_per_step = 13 + 23 * 6 + 69 + 3 * len(BS.KEY_BODIES) - (6 + 3) * 4  # :471-476
+    env._amp_obs_buf = torch.randn(NE, S, env._num_amp_obs_per_step, generator=g)
+    env._curr_amp_obs_buf = env._amp_obs_buf[:, 0]
+    env._hist_amp_obs_buf = env._amp_obs_buf[:, 1:]
+    env._amp_obs_demo_buf = torch.randn(NE, S, env._num_amp_obs_per_step, generator=g)
+    lens = lib._motion_lengths
+    env._motion_start_times[:] = ((torch.rand(NE, generator=g) * lens) / (1 / 30)).long() * (1 / 30)
+    env._global_offset[:] = torch.randn(NE, 3, generator=g) * 0.1
+    env.progress_buf[:] = torch.randint(0, 30, (NE,), generator=g).to(torch.short)
+    t = env.progress_buf * env.isaac_base.dt + env._motion_start_times
+    ms = lib.get_motion_state(env._sampled_motion_ids, t, env._global_offset)
+    env._rigid_body_pos[:] = ms["rg_pos"] + 0.05 * torch.randn(NE, 24, 3, generator=g)
+    rot = ms["rb_rot"] + 0.05 * torch.randn(NE, 24, 4, generator=g)
+    env._rigid_body_rot[:] = rot / rot.norm(dim=-1, keepdim=True)
+    env._rigid_body_vel[:] = ms["body_vel"] + torch.randn(NE, 24, 3, generator=g)
+    env._rigid_body_ang_vel[:] = ms["body_ang_vel"] + torch.randn(NE, 24, 3, generator=g)
+    env._dof_pos[:] = ms["dof_pos"] + 0.05 * torch.randn(NE, 69, generator=g)
+    env._dof_vel[:] = ms["dof_vel"] + torch.randn(NE, 69, generator=g)
+    out.update(env_motion_ids=env._sampled_motion_ids, env_start_times=env._motion_start_times.clone(),
+               env_global_offset=env._global_offset.clone(), env_progress=env.progress_buf.clone(),
+               env_rb_state=env._rigid_body_state.view(NE, 24, 13).clone(),
+               env_dof_state=env._dof_state.view(NE, 69, 2).clone(), amp_buf_in=env._amp_obs_buf.clone(),
+               amp_demo_in=env._amp_obs_demo_buf.clone(), num_amp_obs_steps=np.array(S))
+    # step: HumanoidPHC.step's AMP tail (:154-157). The un-indexed branch of _update_hist_amp_obs
+    # (:1341-1347) assigns between overlapping views of one buffer. The reference's comment there
+    # records that its torch raised on that and it falls back to .clone(), i.e. a history shift; the
+    # CPU torch of this container raises nothing and smears row 0 over every history row. The
+    # indexed branch (:1349) gathers the source first, which is the shift for any torch, so the
+    # fixture is taken through it with every env id.
+    env._update_hist_amp_obs(env.all_env_ids)
+    env._compute_amp_observations()
+    out["amp_buf_step"] = env._amp_obs_buf.clone()
+    # reset of a subset: _reset_ref_state_init (the env state) then _init_amp_obs (:665-676)
+    env_ids = torch.tensor([1, 2, 5, 11, 16, 23])
+    torch.manual_seed(31)
+    phases = torch.rand(len(env_ids))
+    torch.manual_seed(31)
+    env._reset_ref_state_init(env_ids)
+    env.progress_buf[env_ids] = 0
+    env._init_amp_obs(env_ids)
+    out.update(reset_ids=env_ids, reset_phases=phases, amp_buf_reset=env._amp_obs_buf.clone(),
+               amp_demo_reset=env._amp_obs_demo_buf.clone(), reset_start_times=env._motion_start_times.clone(),
+               env_rb_state_reset=env._rigid_body_state.view(NE, 24, 13).clone(),
+               env_dof_state_reset=env._dof_state.view(NE, 69, 2).clone(),
+               gts=lib.gts, grs=lib.grs, lrs=lib.lrs, gvs=lib.gvs, gavs=lib.gavs, dvs=lib.dvs,
+               length_starts=lib.length_starts, num_frames=lib._motion_num_frames,
+               motion_lengths=lib._motion_lengths, motion_dt=lib._motion_dt)
+    np.savez_compressed(os.path.join(OUT, "amp.npz"), **{k: t2n(v) for k, v in out.items()})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)
+    if sys.argv[1:] == ["amp"]:
+        tree = SkeletonTree.from_mjcf(XML)
+        gen_amp(tree, make_clips())
+        return
     gen_quat_prims()
     tree = gen_skeleton()
     clips, _ = gen_motion_lib(tree)
     gen_imitation_funcs()
     gen_env(tree, clips)
     gen_pd()
+    gen_amp(tree, clips)
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
