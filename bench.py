@@ -24,6 +24,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+EV_EVERY = 10                  # timed steps between sampled kernel-duration event triples
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak (spec)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 # SURVEY.md §8(d) canonical algorithmic counts per env-step
@@ -247,16 +248,19 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    # kernel durations: HIP events around the two launches of every EV_EVERY-th timed step (an event
+    # pair costs ~3 us of stream time per step, 3.7% of the step if recorded on every step)
+    sampled = list(range(0, args.steps, EV_EVERY))
+    evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for k in sampled}
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ro.step(evs[k])
+        ro.step(evs.get(k))
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs.values()]))
+    imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs.values()]))
     if world > 1:
         t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

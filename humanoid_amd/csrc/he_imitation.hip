@@ -44,6 +44,28 @@ HE_DEV int64_t clamp_mid(const MotionDev& m, int64_t mid) {
     return mid < 0 ? 0 : (mid >= m.num_motions ? (int64_t)m.num_motions - 1 : mid);
 }
 
+struct MotionMeta {
+    float len, dt;
+    int64_t nf, start;
+};
+
+HE_DEV MotionMeta motion_meta(const MotionDev& m, int64_t mid) {  // mid already clamped
+    return MotionMeta{m.lengths[mid], m.dt[mid], m.num_frames[mid], m.length_starts[mid]};
+}
+
+HE_DEV FrameSel frame_select(const MotionMeta& mm, float time) {
+    const float len = mm.len, dt = mm.dt;
+    const int64_t nf = mm.nf;
+    float phase = time / len;
+    phase = phase < 0.0f ? 0.0f : (phase > 1.0f ? 1.0f : phase);
+    if (time < 0.0f) time = 0.0f;
+    int64_t f0 = (int64_t)(phase * (float)(nf - 1));
+    int64_t f1 = f0 + 1 < nf - 1 ? f0 + 1 : nf - 1;
+    float bl = (time - (float)f0 * dt) / dt;
+    bl = bl < 0.0f ? 0.0f : (bl > 1.0f ? 1.0f : bl);
+    return FrameSel{mm.start + f0, mm.start + f1, bl};
+}
+
 HE_DEV FrameSel frame_select(const MotionDev& m, int64_t mid, float time) {
     mid = clamp_mid(m, mid);
     float len = m.lengths[mid];
@@ -315,6 +337,9 @@ HE_DEV void eval_record(const he_eval_buffers& ev, int e, int lane, bool act, f3
     }
 }
 
+// EVAL: eval recording compiled in (its fp64 Procrustes solve would otherwise set the register
+// budget of every launch)
+template <bool EVAL>
 __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
     const int lane = threadIdx.x & (GROUP - 1);
     const int slot = (blockIdx.x * blockDim.x + threadIdx.x) / GROUP;
@@ -323,20 +348,31 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
     const bool act = lane < NB;
     const int b = act ? lane : 0;
     const he_imitation_params& p = a.p;
+    // Dependent global round trips are the cost of this kernel, so every load that does not depend
+    // on a motion-table index is issued first, and both motion samples (t for reward/reset, t+dt
+    // for the observation) are selected from one metadata read and loaded together before any store.
+    // trip 1: env bookkeeping, the simulated body row, the power-reward operands
     const int64_t mid = clamp_mid(a.m, a.motion_ids[e]);
     f3 off = f3{a.global_offset[3 * e], a.global_offset[3 * e + 1], a.global_offset[3 * e + 2]};
     float start = a.start_times[e], soff = a.start_offsets[e];
     int prog = a.progress[e];
+    SimBody s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);
+    float pw = 0.0f;
+    if (a.mode != 2 && p.use_power_reward && lane < NB - 1) {  // humanoid_phc.py:1297-1305
+        const float* f = a.dof_force + (size_t)e * ND + 3 * lane;
+        const float* v = a.dof_state + ((size_t)e * ND + 3 * lane) * 2 + 1;
+        pw = fabsf(f[0] * v[0]) + fabsf(f[1] * v[2]) + fabsf(f[2] * v[4]);
+    }
+    // trip 2: the motion's metadata; trip 3: both samples' frame records
+    const MotionMeta mm = motion_meta(a.m, mid);
     bool do_reset = false;
     float reset_time = 0.0f;
+    if (a.mode != 2) prog += 1;  // post-physics half of HumanoidPHC.step (humanoid_phc.py:138-149)
+    const float t = env_time(prog, p.control_dt, start, soff);
+    const BodyRef r = body_ref(a.m, frame_select(mm, t), b, off);
+    BodyRef r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
 
     if (a.mode != 2) {
-        // ---------------- post-physics half of HumanoidPHC.step (humanoid_phc.py:138-149)
-        prog += 1;
-        SimBody s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);
-        float t = env_time(prog, p.control_dt, start, soff);
-        FrameSel fs = frame_select(a.m, mid, t);
-        BodyRef r = body_ref(a.m, fs, b, off);
         // reward terms, common.py:298-317
         f3 d = r.pos - s.pos;
         float dp = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
@@ -353,20 +389,14 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
         float rp = expf(-p.k_pos * dp), rr = expf(-p.k_rot * dr), rv = expf(-p.k_vel * dv), ra = expf(-p.k_ang_vel * da);
         float rew = p.w_pos * rp + p.w_rot * rr + p.w_vel * rv + p.w_ang_vel * ra;
         float pr = 0.0f;
-        if (p.use_power_reward) {  // humanoid_phc.py:1297-1305
-            float pw = 0.0f;
-            if (lane < NB - 1) {
-                const float* f = a.dof_force + (size_t)e * ND + 3 * lane;
-                const float* v = a.dof_state + ((size_t)e * ND + 3 * lane) * 2 + 1;
-                pw = fabsf(f[0] * v[0]) + fabsf(f[1] * v[2]) + fabsf(f[2] * v[4]);
-            }
+        if (p.use_power_reward) {
             pw = group_sum(pw);
             pr = -p.power_coef * pw;
             if (prog <= 3) pr = 0.0f;
             rew += pr;
         }
         // termination, common.py:325-364 + humanoid_phc.py:1313-1335
-        bool pass_time = t >= a.m.lengths[mid];
+        bool pass_time = t >= mm.len;
         bool fallen = false;
         if (p.enable_early_termination) {
             bool inset = act && ((p.reset_body_mask >> b) & 1);
@@ -382,7 +412,7 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
             fallen = fallen && prog > 1;
         }
         bool reset = pass_time || fallen;
-        if (a.has_eval) eval_record(a.ev, e, lane, act, s.pos, r.pos);  // before any fused reset
+        if (EVAL) eval_record(a.ev, e, lane, act, s.pos, r.pos);  // before any fused reset
         if (lane == 0) {
             a.rew[e] = rew;
             float* raw = a.reward_raw + (size_t)e * HE_REWARD_RAW;
@@ -394,14 +424,14 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
         if (a.mode == 1 && reset) {
             do_reset = true;
             float ph = hash_uniform(a.seed, a.step, (uint32_t)e);
-            reset_time = sample_time_interval(ph, a.m.lengths[mid]);
+            reset_time = sample_time_interval(ph, mm.len);
         }
     } else {
         do_reset = true;
-        reset_time = sample_time_interval(a.phases[slot], a.m.lengths[mid]);
+        reset_time = sample_time_interval(a.phases[slot], mm.len);
     }
 
-    if (do_reset) {
+    if (do_reset) {  // the group's branch is uniform
         if (act) reset_body(a, e, b, mid, reset_time, off);
         off = f3{0.f, 0.f, 0.f};
         start = reset_time;
@@ -414,17 +444,15 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
             a.progress[e] = 0;
             if (a.mode == 2) { a.reset[e] = 0; a.terminate[e] = 0; }
         }
+        s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);  // the row this lane just wrote
+        r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
     }
 
     // ---------------- observations for the next step (humanoid_phc.py:937-961, 1063-1067)
-    SimBody s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);
     f3 root_pos = f3{bcast0(s.pos.x), bcast0(s.pos.y), bcast0(s.pos.z)};
     f4 root_rot = f4{bcast0(s.rot.x), bcast0(s.rot.y), bcast0(s.rot.z), bcast0(s.rot.w)};
     float h = calc_heading(root_rot);
     f4 hinv = heading_quat(-h), hq = heading_quat(h);
-    float t2 = env_time(prog + 1, p.control_dt, start, soff);
-    FrameSel fs2 = frame_select(a.m, mid, t2);
-    BodyRef r2 = body_ref(a.m, fs2, b, off);
     if (act) write_obs(a.obs + (size_t)e * HE_OBS_DIM, b, s, root_pos, hinv, hq, r2);
 }
 
@@ -600,7 +628,10 @@ hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream) {
     if (a.count <= 0) return hipSuccess;
     int threads = 256;
     int blocks = (a.count * GROUP + threads - 1) / threads;
-    imitation_kernel<<<blocks, threads, 0, stream>>>(a);
+    if (a.has_eval && a.mode != 2)
+        imitation_kernel<true><<<blocks, threads, 0, stream>>>(a);
+    else
+        imitation_kernel<false><<<blocks, threads, 0, stream>>>(a);
     return hipGetLastError();
 }
 

@@ -418,6 +418,8 @@ HE_DEV void zrow_bodies(float (&z)[NG], float (&bacc)[4], uint32_t lb, uint32_t 
         float nxt[15];
         if constexpr (B + 1 < NB) {
             if ((lb >> (B + 1)) & 1u) zrow_load(L, B + 1, nxt);
+            else
+                for (int x = 0; x < 15; ++x) regla::undef_reg(nxt[x]);  // never read: no zeros
         }
         constexpr int i0 = 6 + 3 * (B - 1);
         if ((lb >> B) & 1u) {
@@ -779,7 +781,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     float yl = L.rhs[lane], y2 = lane < NH ? L.rhs[64 + lane] : 0.f;
     {
         float Dl = 1.f, D2 = 1.f;
-        factor_lds_steps<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
+        factor_lds_groups<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
@@ -982,6 +984,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             {
                 float cur[15];
                 if ((lb >> 1) & 1u) zrow_load(L, 1, cur);
+                else
+                    for (int x = 0; x < 15; ++x) regla::undef_reg(cur[x]);
                 zrow_bodies<1>(z, bacc, lb, anc0, anc1, cx, dd, L, cur);
             }
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);

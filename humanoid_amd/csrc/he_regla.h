@@ -207,6 +207,16 @@ __device__ __forceinline__ typename RowOf<K>::T load_row_if(const float* Lp, int
     if constexpr (K >= 1) return load_row<K>(Lp, off + kPackStart[K]);
     else return typename RowOf<K>::T{};
 }
+// registers whose content does not matter (a row that is not loaded because its body is not live
+// is never read): defined by an empty asm, so the compiler does not materialise zeros for them
+__device__ __forceinline__ void undef_reg(float& x) { asm volatile("" : "=v"(x)); }
+template <int D>
+__device__ __forceinline__ void undef_row(Row<D>& r) {
+#pragma unroll
+    for (int q = 0; q < (D + 3) / 4 || q < 1; ++q) {
+        undef_reg(r.v[q].x); undef_reg(r.v[q].y); undef_reg(r.v[q].z); undef_reg(r.v[q].w);
+    }
+}
 template <int K>
 __device__ __forceinline__ void zbs_pipe(const float* Lp, float (&z)[NG], uint32_t lb, const typename RowOf<K>::T& rk) {
     if constexpr (K >= 1) {
@@ -216,6 +226,8 @@ __device__ __forceinline__ void zbs_pipe(const float* Lp, float (&z)[NG], uint32
                 int off = 0;
                 asm volatile("" : "+v"(off));
                 nx = load_row_if<K - 1>(Lp, off);
+            } else {
+                undef_row(nx);
             }
         }
         if (body_live<K>(lb)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z, z[K]);
@@ -383,4 +395,111 @@ __device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2
     }
 }
 
+// ---------------------------------------------------------------- grouped elimination
+// Consecutive steps of kElimOrder whose dofs are mutually independent (neither is an ancestor of
+// the other: different branches) touch disjoint pivots and rows, so a group of them runs as one
+// step: all pivots and reciprocals, then all packed-row stores and right-hand-side updates, then
+// all row broadcasts (one LDS round trip), then the ancestor updates in the original order. Every
+// register sees its updates in the same order as in the one-at-a-time elimination, so the factor
+// is bit-identical to factor_lds_steps; the dependent latency chain is paid once per group.
+constexpr bool dof_is_anc(int a, int b) {  // b in chain(a), a itself included
+    return b < 64 ? ((kAncLo[a] >> b) & 1ull) != 0 : ((kAncHi[a] >> (b - 64)) & 1u) != 0;
+}
+template <int GMAX>
+struct ElimGroups {
+    int start[NG + 1];
+    int count;
+    constexpr ElimGroups() : start(), count(0) {
+        int i = 0;
+        while (i < NG) {
+            start[count++] = i;
+            int j = i + 1;
+            while (j < NG && j - i < GMAX) {
+                bool ok = true;
+                for (int x = i; x < j; ++x)
+                    if (dof_is_anc(kElimOrder[j], kElimOrder[x]) || dof_is_anc(kElimOrder[x], kElimOrder[j])) ok = false;
+                if (!ok) break;
+                ++j;
+            }
+            i = j;
+        }
+        start[count] = NG;
+    }
+};
+constexpr int kElimGroupMax = 2;
+constexpr ElimGroups<kElimGroupMax> kElimGroups{};
+
+template <int K>
+struct PivotStep {
+    float dk, t, t2;
+    Row<kDofNanc[K] - 1> row;
+};
+// A: pivot, reciprocal, row K of L on lanes j < K
+template <int K>
+__device__ __forceinline__ void grp_pivot(RegMat& M, PivotStep<K>& st) {
+    st.dk = get<K, K>(M);
+    const float inv = uniform(__builtin_amdgcn_rcpf(st.dk));
+    st.t = M.c[K];
+    st.t2 = K >= 64 ? M.c2[K >= 64 ? K - 64 : 0] : 0.f;
+    M.c[K] = st.t * inv;
+    if constexpr (K >= 64) M.c2[K - 64] = st.t2 * inv;
+}
+// B: packed-row store and the fused forward substitution of the right-hand side
+template <int K>
+__device__ __forceinline__ void grp_store(const RegMat& M, float* Lp, int dj, int dj2, float& yl, float& y2) {
+    if constexpr (kDofNanc[K] - 1 > 0) {
+        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
+        if (lanes<lo>()) {
+            Lp[kPackStart[K] + dj] = M.c[K];
+            yl = yl - M.c[K] * yk;
+        }
+        if constexpr (K > 64) {
+            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+            if (lanes<hi>()) {
+                Lp[kPackStart[K] + dj2] = M.c2[K - 64];
+                y2 = y2 - M.c2[K - 64] * yk;
+            }
+        }
+    }
+}
+// C + D: row broadcast (in-order LDS: sees the stores of B) and the ancestor updates
+template <int K>
+__device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st) {
+    if constexpr (kDofNanc[K] - 1 > 0) st.row = load_row<K>(Lp, kPackStart[K]);
+}
+template <int K>
+__device__ __forceinline__ void grp_update(RegMat& M, float& Dl, float& D2, const PivotStep<K>& st) {
+    if constexpr (kDofNanc[K] - 1 > 0) fac_anc_row<K, 0, kDofNanc[K] - 1>(M, st.row, st.t, st.t2);
+    if constexpr (K < 64) Dl = wrlane<K>(st.dk, Dl);
+    else D2 = wrlane<K - 64>(st.dk, D2);
+}
+template <int GI>
+__device__ __forceinline__ void factor_lds_groups(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2,
+                                                  float& yl, float& y2) {
+    if constexpr (GI < kElimGroups.count) {
+        constexpr int S0 = kElimGroups.start[GI], n = kElimGroups.start[GI + 1] - S0;
+        static_assert(n >= 1 && n <= 3, "group size");
+        constexpr int K0 = kElimOrder[S0];
+        constexpr int K1 = kElimOrder[n > 1 ? S0 + 1 : S0];
+        constexpr int K2 = kElimOrder[n > 2 ? S0 + 2 : S0];
+        PivotStep<K0> a;
+        PivotStep<K1> b;
+        PivotStep<K2> c;
+        grp_pivot<K0>(M, a);
+        if constexpr (n > 1) grp_pivot<K1>(M, b);
+        if constexpr (n > 2) grp_pivot<K2>(M, c);
+        grp_store<K0>(M, Lp, dj, dj2, yl, y2);
+        if constexpr (n > 1) grp_store<K1>(M, Lp, dj, dj2, yl, y2);
+        if constexpr (n > 2) grp_store<K2>(M, Lp, dj, dj2, yl, y2);
+        grp_load<K0>(Lp, a);
+        if constexpr (n > 1) grp_load<K1>(Lp, b);
+        if constexpr (n > 2) grp_load<K2>(Lp, c);
+        grp_update<K0>(M, Dl, D2, a);
+        if constexpr (n > 1) grp_update<K1>(M, Dl, D2, b);
+        if constexpr (n > 2) grp_update<K2>(M, Dl, D2, c);
+        __builtin_amdgcn_sched_barrier(0);
+        factor_lds_groups<GI + 1>(M, Dl, D2, Lp, dj, dj2, yl, y2);
+    }
+}
 }  // namespace regla
