@@ -47,6 +47,7 @@ struct BodyTopo {
     uint32_t anc_mask[NB];
     uint32_t sub_mask[NB];
     float local_pos[NB][3];  // joint offsets (model), read along every FK chain walk
+    uint32_t jump4[NB];      // byte k: 2^k-th ancestor of body b (0xFF: none), for pointer jumping
     int16_t pack_start[NG];  // packed-row offset of dof i (smpl::kPackStart)
     int8_t dof_depth[NG];    // depth of dof i in the dof tree (smpl::kDofNanc - 1)
 };
@@ -551,12 +552,17 @@ struct JumpTable {
 constexpr JumpTable kJumpT{};
 static_assert(smpl::kNumBodyLevels <= 16, "four pointer-jumping rounds cover chains of 16 bodies");
 
+struct Jump4 {  // the four jump targets of each body packed as bytes (LDS table BodyTopo::jump4)
+    uint32_t v[NB];
+    constexpr Jump4() : v() {
+        for (int b = 0; b < NB; ++b)
+            for (int k = 0; k < 4; ++k) v[b] |= (uint32_t)(kJumpT.j[k][b] & 0xFF) << (8 * k);
+    }
+};
+constexpr Jump4 kJump4{};
 template <int K>
-HE_DEV int jump_of(int b) {  // kJumpT.j[K][b] as a select chain (no runtime-indexed constant memory)
-    int r = -1;
-#pragma unroll
-    for (int x = 0; x < NB; ++x) r = b == x ? kJumpT.j[K][x] : r;
-    return r;
+HE_DEV int jump_of(uint32_t jp) {  // byte K of the lane's packed entry, sign-extended (v_bfe_i32)
+    return (int)(int8_t)(jp >> (8 * K));
 }
 
 // World poses and spatial velocities, lane = body, by pointer jumping: X_b <- X_{J_k(b)} o X_b and
@@ -569,6 +575,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     const bool act = lane < NB;
     const int b = act ? lane : 0;
     const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
+    const uint32_t jp = act ? T.jump4[b] : 0xFFFFFFFFu;
     f4 q;
     f3 p;
     float u[3];
@@ -584,7 +591,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     }
     auto jump = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        const int j = act ? jump_of<K>(b) : -1;
+        const int j = jump_of<K>(jp);
         const int src = j < 0 ? lane : j;
         const f4 qa = f4{__shfl(q.x, src, W), __shfl(q.y, src, W), __shfl(q.z, src, W), __shfl(q.w, src, W)};
         const f3 pa = f3{__shfl(p.x, src, W), __shfl(p.y, src, W), __shfl(p.z, src, W)};
@@ -611,7 +618,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     for (int x = 0; x < 6; ++x) vj[x] = V[x];
     auto vjump = [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        const int j = act ? jump_of<K>(b) : -1;
+        const int j = jump_of<K>(jp);
         const int src = j < 0 ? lane : j;
         float Va[6];
 #pragma unroll
@@ -643,7 +650,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         }
         auto ajump = [&](auto kc) {
             constexpr int K = decltype(kc)::value;
-            const int j = act ? jump_of<K>(b) : -1;
+            const int j = jump_of<K>(jp);
             const int src = j < 0 ? lane : j;
             float Aa[6];
 #pragma unroll
@@ -1121,6 +1128,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         L.T.dof0[lane] = T.body_dof0[lane];
         L.T.anc_mask[lane] = T.anc_mask[lane];
         L.T.sub_mask[lane] = T.sub_mask[lane];
+        L.T.jump4[lane] = kJump4.v[lane < NB ? lane : 0];
         for (int c = 0; c < 3; ++c) L.T.local_pos[lane][c] = m.local_pos[lane][c];
     }
     for (int i = lane; i < NG; i += W) {  // per-dof tree tables (constant memory -> LDS once)
