@@ -14,7 +14,9 @@ ARCH = os.environ.get("HE_OFFLOAD_ARCH", "gfx950")
 # reference's torch ops do (no FMA contraction); the physics kernel may contract.
 SOURCES = [
     ("he_imitation.hip", ["-ffp-contract=off"]),
-    ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]),
+    # no SLP vectorisation: the compiler's own packed-FP32 pairing costs more moves than it saves;
+    # the elimination issues its v_pk_fma_f32 explicitly (he_regla.h)
+    ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]),
     ("he_ingest.hip", []),
     ("he_rollout.hip", ["-ffp-contract=off"]),  # GAE: the Cython module's float32 rounding
     ("he_engine.cpp", ["-x", "hip"]),

@@ -454,12 +454,12 @@ HE_DEV void crba_row(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[
     float h = lanes<smpl::kAncLo[I]>() ? dot6(Sj, IS) : 0.f;
     if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
     asm volatile("" : "+v"(h));
-    M.c[I] = h;
+    mc_set<I>(M, h);
     if constexpr (I >= 64) {
         float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? dot6(Sj2, IS) : 0.f;
         h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
         asm volatile("" : "+v"(h2));
-        M.c2[I - 64] = h2;
+        mc2_set<I - 64>(M, h2);
     }
 }
 
@@ -483,26 +483,6 @@ HE_DEV void crba_groups(regla::RegMat& M, const float (&Sj)[6], const float (&Sj
         if constexpr (4 * G + 3 < NG) crba_row<4 * G + 3>(M, Sj, Sj2, dadd, dadd2, cur[3]);
         crba_groups<G + 1>(M, Sj, Sj2, dadd, dadd2, L, nxt);
     }
-}
-
-// y <- L^-1 D^-1 L^-T y for a distributed right-hand side (lane i: y[i], lanes < 11: y[64+i])
-template <class LdsT>
-HE_DEV void joint_space_solve(const LdsT& L, float& yl, float& y2, int lane) {
-    using namespace regla;
-    const int dj = L.T.dof_depth[lane], dj2 = lane < NH ? L.T.dof_depth[64 + lane] : 0;
-    solve_LT_cols<smpl::kNumLevels - 1>(L.Lp, dj, dj2, yl, y2, lane);
-    yl *= L.Dinv[lane];
-    if (lane < NH) y2 *= L.Dinv[64 + lane];
-    float r1[kRowRegs], r2[kRowRegs];
-    const float4* p1 = reinterpret_cast<const float4*>(L.Lp + L.T.pack_start[lane]);
-    const float4* p2 = reinterpret_cast<const float4*>(L.Lp + L.T.pack_start[lane < NH ? 64 + lane : 0]);
-#pragma unroll
-    for (int q = 0; q < kRowRegs / 4; ++q) {
-        const float4 v1 = p1[q], v2 = p2[q];
-        r1[4 * q] = v1.x; r1[4 * q + 1] = v1.y; r1[4 * q + 2] = v1.z; r1[4 * q + 3] = v1.w;
-        r2[4 * q] = v2.x; r2[4 * q + 1] = v2.y; r2[4 * q + 2] = v2.z; r2[4 * q + 3] = v2.w;
-    }
-    solve_L_rows<0>(r1, r2, yl, y2);
 }
 
 // In-place subtree sums X[b] += sum over children of X[c], parents of the deepest level first: at

@@ -19,10 +19,23 @@ constexpr int W = 64;
 constexpr int NG = kNG;
 constexpr int NH = NG - 64;  // columns held in the second register set
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// c[i] = cp[i >> 1][i & 1], c2[i] = cp2[i >> 1][i & 1]: dofs (2k, 2k+1) share an aligned VGPR pair,
+// so two updates with a common multiplier are one v_pk_fma_f32
 struct RegMat {
-    float c[NG];
-    float c2[NH];
+    f2v cp[(NG + 1) / 2];
+    f2v cp2[(NH + 1) / 2];
 };
+template <int I>
+__device__ __forceinline__ float mc(const RegMat& M) { return M.cp[I >> 1][I & 1]; }
+template <int I>
+__device__ __forceinline__ void mc_set(RegMat& M, float v) { M.cp[I >> 1][I & 1] = v; }
+template <int I>
+__device__ __forceinline__ float mc2(const RegMat& M) { return M.cp2[I >> 1][I & 1]; }
+template <int I>
+__device__ __forceinline__ void mc2_set(RegMat& M, float v) { M.cp2[I >> 1][I & 1] = v; }
 
 __device__ __forceinline__ float rdlane(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
@@ -39,8 +52,8 @@ __device__ __forceinline__ float wrlane(float v, float old) {
 template <int ROW, int COL>
 __device__ __forceinline__ float get(const RegMat& M) {
     static_assert(ROW >= COL, "lower triangle only");
-    if constexpr (COL < 64) return rdlane(M.c[ROW], COL);
-    else return rdlane(M.c2[ROW - 64], COL - 64);
+    if constexpr (COL < 64) return rdlane(mc<ROW>(M), COL);
+    else return rdlane(mc2<ROW - 64>(M), COL - 64);
 }
 
 // lanes whose bit is set in the compile-time mask C (v_cndmask on an SGPR-pair constant; no
@@ -66,99 +79,6 @@ __device__ __forceinline__ float uniform(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
-// H[I][j] -= H[K][I] * L[K][j] for every column j (c[K] already scaled to row K of L)
-template <int K, int X, int D>
-__device__ __forceinline__ void fac_anc(RegMat& M, const float (&hk)[kMaxChain]) {
-    if constexpr (X < D) {
-        constexpr int I = kChain[K][X];
-        M.c[I] -= hk[X] * M.c[K];
-        if constexpr (I >= 64) M.c2[I - 64] -= hk[X] * M.c2[K - 64];
-        fac_anc<K, X + 1, D>(M, hk);
-    }
-}
-template <int K, int X, int D>
-__device__ __forceinline__ void read_row(const RegMat& M, float (&hk)[kMaxChain]) {
-    if constexpr (X < D) {
-        hk[X] = get<K, kChain[K][X]>(M);
-        read_row<K, X + 1, D>(M, hk);
-    }
-}
-
-// elimination step S eliminates dof kElimOrder[S] (deepest first, so consecutive steps mostly lie
-// on independent branches and can overlap; a scheduling barrier every two steps bounds the live
-// SGPR/VGPR ranges). The pivot D_K is kept on its owning lane (Dl / D2); the pivot reciprocal and
-// the row entries H[K][I] are wave-uniform (SGPRs), so each update is one FMA.
-template <int S>
-__device__ __forceinline__ void factor_steps(RegMat& M, float& Dl, float& D2) {
-    if constexpr (S < NG) {
-        constexpr int K = kElimOrder[S];
-        constexpr int D = kDofNanc[K] - 1;
-        const float dk = get<K, K>(M);
-        const float inv = uniform(__builtin_amdgcn_rcpf(dk));  // v_rcp_f32 (1 ulp): short pivot chain
-        float hk[kMaxChain];
-        read_row<K, 0, D>(M, hk);
-        M.c[K] *= inv;  // row K -> L[K][.] on lanes j < K
-        if constexpr (K >= 64) M.c2[K - 64] *= inv;
-        fac_anc<K, 0, D>(M, hk);
-        if constexpr (K < 64) Dl = wrlane<K>(dk, Dl);
-        else D2 = wrlane<K - 64>(dk, D2);
-        if constexpr (S % 2 == 1) __builtin_amdgcn_sched_barrier(0);
-        factor_steps<S + 1>(M, Dl, D2);
-    }
-}
-template <int K>
-__device__ __forceinline__ void factor(RegMat& M, float& Dl, float& D2, int) {
-    factor_steps<0>(M, Dl, D2);
-}
-
-// ---------------------------------------------------------------- y <- L^-T y (y distributed: lane i holds y[i], y2 = y[64+i])
-template <int K>
-__device__ __forceinline__ void solve_LT(const RegMat& M, float& yl, float& y2, int lane) {
-    if constexpr (K >= 1) {
-        const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-        yl = lanes<lo>() ? yl - M.c[K] * yk : yl;
-        if constexpr (K > 64) {
-            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-            y2 = lanes<hi>() ? y2 - M.c2[K - 64] * yk : y2;
-        }
-        solve_LT<K - 1>(M, yl, y2, lane);
-    }
-}
-
-// ---------------------------------------------------------------- y <- L^-1 y
-template <int K>
-__device__ __forceinline__ void solve_L(const RegMat& M, float& yl, float& y2, int lane) {
-    if constexpr (K < NG) {
-        float p = lane < K ? M.c[K] * yl : 0.0f;
-        if constexpr (K > 64) p += lane < K - 64 ? M.c2[K - 64] * y2 : 0.0f;
-        const float s = wave_sum(p);
-        if constexpr (K < 64) {
-            if (lane == K) yl -= s;
-        } else {
-            if (lane == K - 64) y2 -= s;
-        }
-        solve_L<K + 1>(M, yl, y2, lane);
-    }
-}
-
-// ---------------------------------------------------------------- packed copy of L for broadcast reads
-// Lp[kPackStart[K] + x] = L[K][kChain[K][x]] for x < depth(K) (rows padded to 4 floats): lane j
-// writes the entries of its column j; pad slots are loaded but never used
-template <int K>
-__device__ __forceinline__ void store_packed(const RegMat& M, float* Lp, int lane, int lane_depth,
-                                             int lane_depth2) {
-    if constexpr (K >= 1) {
-        constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-        if (lanes<lo>()) Lp[kPackStart[K] + lane_depth] = M.c[K];
-        if constexpr (K > 64) {
-            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-            if (lanes<hi>()) Lp[kPackStart[K] + lane_depth2] = M.c2[K - 64];
-        }
-        store_packed<K - 1>(M, Lp, lane, lane_depth, lane_depth2);
-    }
-}
-
 // z -= a * b as an ordered instruction: the DAG linearisation would otherwise sink the whole
 // unrolled sweep's FMAs below its LDS reads and spill the loaded rows
 __device__ __forceinline__ void fnma(float& z, float a, float b) {
@@ -169,19 +89,19 @@ __device__ __forceinline__ void fnma(float& z, float a, float b) {
 // the packed row K (D entries) as registers: ceil(D/4) 16-byte LDS broadcasts
 template <int D>
 struct Row {
-    float4 v[(D + 3) / 4 > 0 ? (D + 3) / 4 : 1];
+    f4v v[(D + 3) / 4 > 0 ? (D + 3) / 4 : 1];
 };
 template <int K>
 __device__ __forceinline__ Row<kDofNanc[K] - 1> load_row(const float* Lp, int off) {
     Row<kDofNanc[K] - 1> r;
 #pragma unroll
-    for (int q = 0; q < (kDofNanc[K] - 1 + 3) / 4; ++q) r.v[q] = *reinterpret_cast<const float4*>(Lp + off + 4 * q);
+    for (int q = 0; q < (kDofNanc[K] - 1 + 3) / 4; ++q) r.v[q] = *reinterpret_cast<const f4v*>(Lp + off + 4 * q);
     return r;
 }
 template <int K, int X, int D>
 __device__ __forceinline__ void zbs_anc(const Row<D>& row, float (&z)[NG], float zk) {
     if constexpr (X < D) {
-        const float4 v = row.v[X / 4];
+        const f4v v = row.v[X / 4];
         fnma(z[kChain[K][X]], v.x, zk);
         if constexpr (X + 1 < D) fnma(z[kChain[K][X + 1]], v.y, zk);
         if constexpr (X + 2 < D) fnma(z[kChain[K][X + 2]], v.z, zk);
@@ -214,7 +134,7 @@ template <int D>
 __device__ __forceinline__ void undef_row(Row<D>& r) {
 #pragma unroll
     for (int q = 0; q < (D + 3) / 4 || q < 1; ++q) {
-        undef_reg(r.v[q].x); undef_reg(r.v[q].y); undef_reg(r.v[q].z); undef_reg(r.v[q].w);
+        asm volatile("" : "=v"(r.v[q]));
     }
 }
 template <int K>
@@ -291,110 +211,6 @@ __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const 
     }
 }
 
-// ---------------------------------------------------------------- y <- L^-T y, column-distributed
-// by depth levels, deepest first. Lane j first gathers its whole column of L (g1[K] = L[K][j] =
-// Lp[kPackStart[K] + depth(j)], 75 independent LDS reads issued back to back; entries of non-
-// descendants are never selected), then each level is n readlanes of the final y_K plus n masked
-// FMAs into an accumulator and one subtraction.
-template <int K>
-__device__ __forceinline__ void gather_cols(const float* Lp, int dj, int dj2, float (&g1)[NG], float (&g2)[NG - 64]) {
-    if constexpr (K < NG) {
-        if constexpr (K >= 1) g1[K] = Lp[kPackStart[K] + dj];
-        if constexpr (K > 64) g2[K - 64] = Lp[kPackStart[K] + dj2];
-        gather_cols<K + 1>(Lp, dj, dj2, g1, g2);
-    }
-}
-template <int D, int J>
-__device__ __forceinline__ void level_push(const float (&g1)[NG], const float (&g2)[NG - 64], float yl, float y2,
-                                           float& t1, float& t2) {
-    if constexpr (J < kLevelStart[D + 1]) {
-        constexpr int K = kLevelDofs[J];
-        if constexpr (K >= 1) {
-            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-            t1 = lanes<lo>() ? fmaf(g1[K], yk, t1) : t1;
-            if constexpr (K > 64) {
-                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-                t2 = lanes<hi>() ? fmaf(g2[K - 64], yk, t2) : t2;
-            }
-        }
-        level_push<D, J + 1>(g1, g2, yl, y2, t1, t2);
-    }
-}
-template <int D>
-__device__ __forceinline__ void solve_LT_levels(const float (&g1)[NG], const float (&g2)[NG - 64], float& yl,
-                                                float& y2) {
-    if constexpr (D >= 1) {
-        float t1 = 0.f, t2 = 0.f;
-        level_push<D, kLevelStart[D]>(g1, g2, yl, y2, t1, t2);
-        yl -= t1;
-        y2 -= t2;
-        solve_LT_levels<D - 1>(g1, g2, yl, y2);
-    }
-}
-template <int D>
-__device__ __forceinline__ void solve_LT_cols(const float* Lp, int dj, int dj2, float& yl, float& y2, int) {
-    float g1[NG], g2[NG - 64];
-    g1[0] = 0.f;
-    g2[0] = 0.f;
-    gather_cols<0>(Lp, dj, dj2, g1, g2);
-    solve_LT_levels<D>(g1, g2, yl, y2);
-}
-
-// ---------------------------------------------------------------- LTDL with LDS row broadcasts
-// As factor_steps, but row K of L leaves through LDS as soon as it is final (the packed store of
-// the factor, lanes in chain(K) write their entry) and comes back as 16-byte broadcasts: the
-// updates H[I][j] -= L[K][I] * H[K][j] then take both operands from VGPRs (one FMA, no v_readlane),
-// halving the VALU work of the elimination. Leaves Lp complete (no separate store_packed).
-template <int K, int X, int D>
-__device__ __forceinline__ void fac_anc_row(RegMat& M, const Row<D>& row, float t, float t2) {
-    if constexpr (X < D) {
-        constexpr int I = kChain[K][X];
-        const float4 v = row.v[X / 4];
-        const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
-        fnma(M.c[I], l, t);  // ordered: keeps the row's registers short-lived
-        if constexpr (I >= 64) fnma(M.c2[I - 64], l, t2);
-        fac_anc_row<K, X + 1, D>(M, row, t, t2);
-    }
-}
-template <int S>
-__device__ __forceinline__ void factor_lds_steps(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2,
-                                                 float& yl, float& y2) {
-    if constexpr (S < NG) {
-        constexpr int K = kElimOrder[S];
-        constexpr int D = kDofNanc[K] - 1;
-        const float dk = get<K, K>(M);
-        const float inv = uniform(__builtin_amdgcn_rcpf(dk));
-        const float t = M.c[K];                        // H[K][j], unscaled
-        const float t2 = K >= 64 ? M.c2[K >= 64 ? K - 64 : 0] : 0.f;
-        M.c[K] = t * inv;                              // L[K][j] on lanes j < K
-        if constexpr (K >= 64) M.c2[K - 64] = t2 * inv;
-        if constexpr (D > 0) {
-            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-            // forward substitution of the right-hand side fused in (y = L^-T rhs, the same
-            // deepest-first order): y[K] is final once K's descendants are eliminated
-            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
-            if (lanes<lo>()) {
-                Lp[kPackStart[K] + dj] = M.c[K];
-                yl = yl - M.c[K] * yk;
-            }
-            if constexpr (K > 64) {
-                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-                if (lanes<hi>()) {
-                    Lp[kPackStart[K] + dj2] = M.c2[K - 64];
-                    y2 = y2 - M.c2[K - 64] * yk;
-                }
-            }
-            const auto row = load_row<K>(Lp, kPackStart[K]);  // in-order LDS: sees the writes above
-            fac_anc_row<K, 0, D>(M, row, t, t2);
-        }
-        if constexpr (K < 64) Dl = wrlane<K>(dk, Dl);
-        else D2 = wrlane<K - 64>(dk, D2);
-        __builtin_amdgcn_sched_barrier(0);
-        factor_lds_steps<S + 1>(M, Dl, D2, Lp, dj, dj2, yl, y2);
-    }
-}
-
 // ---------------------------------------------------------------- grouped elimination
 // Consecutive steps of kElimOrder whose dofs are mutually independent (neither is an ancestor of
 // the other: different branches) touch disjoint pivots and rows, so a group of them runs as one
@@ -431,46 +247,86 @@ constexpr ElimGroups<kElimGroupMax> kElimGroups{};
 
 template <int K>
 struct PivotStep {
-    float dk, t, t2;
+    float dk, l, l2;  // pivot, row K of L on this lane (scaled) and its second-set entry
     Row<kDofNanc[K] - 1> row;
 };
-// A: pivot, reciprocal, row K of L on lanes j < K
+// A: pivot and reciprocal; the scaled entry L[K][j] goes to a fresh register, M keeps the unscaled
+// H[K][j] as the broadcast operand of the updates until grp_update
 template <int K>
-__device__ __forceinline__ void grp_pivot(RegMat& M, PivotStep<K>& st) {
+__device__ __forceinline__ void grp_pivot(const RegMat& M, PivotStep<K>& st) {
     st.dk = get<K, K>(M);
     const float inv = uniform(__builtin_amdgcn_rcpf(st.dk));
-    st.t = M.c[K];
-    st.t2 = K >= 64 ? M.c2[K >= 64 ? K - 64 : 0] : 0.f;
-    M.c[K] = st.t * inv;
-    if constexpr (K >= 64) M.c2[K - 64] = st.t2 * inv;
+    st.l = mc<K>(M) * inv;
+    if constexpr (K >= 64) st.l2 = mc2<K >= 64 ? K - 64 : 0>(M) * inv;
 }
 // B: packed-row store and the fused forward substitution of the right-hand side
 template <int K>
-__device__ __forceinline__ void grp_store(const RegMat& M, float* Lp, int dj, int dj2, float& yl, float& y2) {
+__device__ __forceinline__ void grp_store(const PivotStep<K>& st, float* Lp, int dj, int dj2, float& yl, float& y2) {
     if constexpr (kDofNanc[K] - 1 > 0) {
         constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
         const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
         if (lanes<lo>()) {
-            Lp[kPackStart[K] + dj] = M.c[K];
-            yl = yl - M.c[K] * yk;
+            Lp[kPackStart[K] + dj] = st.l;
+            yl = yl - st.l * yk;
         }
         if constexpr (K > 64) {
             constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
             if (lanes<hi>()) {
-                Lp[kPackStart[K] + dj2] = M.c2[K - 64];
-                y2 = y2 - M.c2[K - 64] * yk;
+                Lp[kPackStart[K] + dj2] = st.l2;
+                y2 = y2 - st.l2 * yk;
             }
         }
     }
 }
-// C + D: row broadcast (in-order LDS: sees the stores of B) and the ancestor updates
+// C + D: row broadcast (in-order LDS: sees the stores of B), the ancestor updates, then row K of M
+// becomes L[K][.]
 template <int K>
 __device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st) {
     if constexpr (kDofNanc[K] - 1 > 0) st.row = load_row<K>(Lp, kPackStart[K]);
 }
+// H[I][j] -= L[K][I] * H[K][j] over I in chain(K) (row entries from the LDS broadcast, H[K][j]
+// unscaled on lane j, read in place from M). Chain positions X, X+1 holding dofs I, I+1 with X and
+// I even share both a row register pair and a column register pair: one v_pk_fma_f32, with H[K][j]
+// taken from half (K & 1) of K's column pair for both products.
+template <int HALF>
+__device__ __forceinline__ void pk_fnma(f2v& z, f2v a, f2v b) {
+    if constexpr (HALF == 0)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+                     : "+v"(z) : "v"(a), "v"(b));
+    else
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+                     : "+v"(z) : "v"(a), "v"(b));
+}
+template <int K, int X, int D>
+__device__ __forceinline__ void fac_anc_pk(RegMat& M, const Row<D>& row) {
+    if constexpr (X < D) {
+        constexpr int I = kChain[K][X];
+        constexpr bool PAIR = X % 2 == 0 && X + 1 < D && I % 2 == 0 && I + 1 < 64 &&
+                              kChain[K][X + 1 < kMaxChain ? X + 1 : 0] == I + 1;
+        const f4v v = row.v[X / 4];
+        if constexpr (PAIR) {
+            const f2v l = X % 4 == 0 ? __builtin_shufflevector(v, v, 0, 1) : __builtin_shufflevector(v, v, 2, 3);
+            pk_fnma<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
+            fac_anc_pk<K, X + 2, D>(M, row);
+        } else {
+            const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
+            float c = mc<I>(M);
+            fnma(c, l, mc<K>(M));  // ordered: keeps the row's registers short-lived
+            mc_set<I>(M, c);
+            if constexpr (I >= 64) {
+                float c2 = mc2<I - 64>(M);
+                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                mc2_set<I - 64>(M, c2);
+            }
+            fac_anc_pk<K, X + 1, D>(M, row);
+        }
+    }
+}
 template <int K>
 __device__ __forceinline__ void grp_update(RegMat& M, float& Dl, float& D2, const PivotStep<K>& st) {
-    if constexpr (kDofNanc[K] - 1 > 0) fac_anc_row<K, 0, kDofNanc[K] - 1>(M, st.row, st.t, st.t2);
+    if constexpr (kDofNanc[K] - 1 > 0) fac_anc_pk<K, 0, kDofNanc[K] - 1>(M, st.row);
+    mc_set<K>(M, st.l);  // row K -> L[K][.] on lanes j < K
+    if constexpr (K >= 64) mc2_set<K - 64>(M, st.l2);
     if constexpr (K < 64) Dl = wrlane<K>(st.dk, Dl);
     else D2 = wrlane<K - 64>(st.dk, D2);
 }
@@ -489,9 +345,9 @@ __device__ __forceinline__ void factor_lds_groups(RegMat& M, float& Dl, float& D
         grp_pivot<K0>(M, a);
         if constexpr (n > 1) grp_pivot<K1>(M, b);
         if constexpr (n > 2) grp_pivot<K2>(M, c);
-        grp_store<K0>(M, Lp, dj, dj2, yl, y2);
-        if constexpr (n > 1) grp_store<K1>(M, Lp, dj, dj2, yl, y2);
-        if constexpr (n > 2) grp_store<K2>(M, Lp, dj, dj2, yl, y2);
+        grp_store<K0>(a, Lp, dj, dj2, yl, y2);
+        if constexpr (n > 1) grp_store<K1>(b, Lp, dj, dj2, yl, y2);
+        if constexpr (n > 2) grp_store<K2>(c, Lp, dj, dj2, yl, y2);
         grp_load<K0>(Lp, a);
         if constexpr (n > 1) grp_load<K1>(Lp, b);
         if constexpr (n > 2) grp_load<K2>(Lp, c);
