@@ -284,7 +284,7 @@ HE_DEV float reduce_scatter(float (&v)[N]) {
     }
     return v[0];
 }
-HE_DEV void delassus_mfma(const float (&z)[NG], float (&acol)[MAXR], uint32_t live) {
+HE_DEV void delassus_mfma(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
     f32x16 t00 = {}, t01 = {}, t10 = {}, t11 = {};
 #pragma unroll
     for (int g = 0; g < NGRP; ++g) {
@@ -293,7 +293,7 @@ HE_DEV void delassus_mfma(const float (&z)[NG], float (&acol)[MAXR], uint32_t li
             for (int h = 0; h < 4; h += 2) {
                 const int k0 = 4 * g + h;
                 if (k0 < NG) {
-                    float p0 = z[k0], p1 = k0 + 1 < NG ? z[k0 + 1 < NG ? k0 + 1 : 0] : 0.f;
+                    float p0 = ZV(z, k0), p1 = k0 + 1 < NG ? ZV(z, k0 + 1 < NG ? k0 + 1 : 0) : 0.f;
                     swap32(p0, p1);
                     t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(p0, p0, t00, 0, 0, 0);
                     t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(p0, p1, t01, 0, 0, 0);
@@ -319,7 +319,7 @@ HE_DEV void delassus_mfma(const float (&z)[NG], float (&acol)[MAXR], uint32_t li
 // Delassus column entries A[RR][lane] for RR < nr, one row per step (constant register indices);
 // dof groups without a nonzero entry in any row are skipped
 template <int RR>
-HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uint32_t live) {
+HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uint32_t live) {
     // four rows at a time: four independent accumulation chains, and each v_readlane has three
     // other instructions before its SGPR is consumed (no hazard s_nop)
     if constexpr (RR < MAXR) {
@@ -336,7 +336,7 @@ HE_DEV void delassus_rows(const float (&z)[NG], float (&acol)[MAXR], int nr, uin
                     const int i = 4 * g + k < NG ? 4 * g + k : 0;
                     if (4 * g + k < NG) {
 #pragma unroll
-                        for (int q = 0; q < NQ; ++q) acc[q] = fmaf(regla::rdlane(z[i], RR + q), z[i], acc[q]);
+                        for (int q = 0; q < NQ; ++q) acc[q] = fmaf(regla::rdlane(ZV(z, i), RR + q), ZV(z, i), acc[q]);
                     }
                 }
             }
@@ -413,7 +413,7 @@ HE_DEV void zrow_load(const Lds& L, int b, float (&d)[15]) {
 // z_i = S_i . (rho, dd) = a_i . ((x - p_b) x dd) for joint b's three dofs, bodies in order with
 // the next live body's data read while this one is computed
 template <int B>
-HE_DEV void zrow_bodies(float (&z)[NG], float (&bacc)[4], uint32_t lb, uint32_t anc0, uint32_t anc1, f3 cx, f3 dd,
+HE_DEV void zrow_bodies(regla::ZVec& z, float (&bacc)[4], uint32_t lb, uint32_t anc0, uint32_t anc1, f3 cx, f3 dd,
                         const Lds& L, const float (&cur)[15]) {
     if constexpr (B < NB) {
         float nxt[15];
@@ -428,20 +428,20 @@ HE_DEV void zrow_bodies(float (&z)[NG], float (&bacc)[4], uint32_t lb, uint32_t 
             const f3 v = cross3(cx - f3{cur[0], cur[1], cur[2]}, dd) * sgn;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                z[i0 + c] = cur[3 + 3 * c] * v.x + cur[4 + 3 * c] * v.y + cur[5 + 3 * c] * v.z;
-                bacc[c] = fmaf(z[i0 + c], cur[12 + c], bacc[c]);
+                ZV(z, i0 + c) = cur[3 + 3 * c] * v.x + cur[4 + 3 * c] * v.y + cur[5 + 3 * c] * v.z;
+                bacc[c] = fmaf(ZV(z, i0 + c), cur[12 + c], bacc[c]);
             }
         } else {
-            z[i0] = 0.f; z[i0 + 1] = 0.f; z[i0 + 2] = 0.f;
+            ZV(z, i0) = 0.f; ZV(z, i0 + 1) = 0.f; ZV(z, i0 + 2) = 0.f;
         }
-        asm volatile("" : "+v"(z[i0]), "+v"(z[i0 + 1]), "+v"(z[i0 + 2]), "+v"(bacc[0]), "+v"(bacc[1]), "+v"(bacc[2]));
+        asm volatile("" : "+v"(z.p[i0 >> 1]), "+v"(z.p[(i0 + 2) >> 1]), "+v"(bacc[0]), "+v"(bacc[1]), "+v"(bacc[2]));
         zrow_bodies<B + 1>(z, bacc, lb, anc0, anc1, cx, dd, L, nxt);
     }
 }
 template <int I>
-HE_DEV void scale_rows(float (&z)[NG], float sdl, float sdl2) {
+HE_DEV void scale_rows(regla::ZVec& z, float sdl, float sdl2) {
     if constexpr (I < NG) {
-        z[I] *= I < 64 ? regla::rdlane(sdl, I < 64 ? I : 0) : regla::rdlane(sdl2, I >= 64 ? I - 64 : 0);
+        ZV(z, I) *= I < 64 ? regla::rdlane(sdl, I < 64 ? I : 0) : regla::rdlane(sdl2, I >= 64 ? I - 64 : 0);
         scale_rows<I + 1>(z, sdl, sdl2);
     }
 }
@@ -943,7 +943,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         const int nr = 3 * nc;
         float brow = 0.f, diag = 0.f, lamv = 0.f;
         float acol[MAXR];  // lane c: A[r][c]
-        float z[NG];       // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
+        regla::ZVec z;     // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
         {
             const int r = lane < nr ? lane : 0;
             const int ci = r / 3, kind = r - 3 * ci;
@@ -963,10 +963,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             {
                 // root: S = unit axes, so z = sgn0 * (rho, dd)
                 const float s0 = (float)(anc0 & 1u) - (float)(anc1 & 1u);
-                z[0] = s0 * rho.x; z[1] = s0 * rho.y; z[2] = s0 * rho.z;
-                z[3] = s0 * dd.x; z[4] = s0 * dd.y; z[5] = s0 * dd.z;
+                ZV(z, 0) = s0 * rho.x; ZV(z, 1) = s0 * rho.y; ZV(z, 2) = s0 * rho.z;
+                ZV(z, 3) = s0 * dd.x; ZV(z, 4) = s0 * dd.y; ZV(z, 5) = s0 * dd.z;
             }
-            for (int i = 0; i < 6; ++i) bacc[i & 3] = fmaf(z[i], L.uf[i], bacc[i & 3]);
+            for (int i = 0; i < 6; ++i) bacc[i & 3] = fmaf(ZV(z, i), L.uf[i], bacc[i & 3]);
             const f3 cx = f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]};
             {
                 float cur[15];
@@ -986,7 +986,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             scale_rows<0>(z, sdl, sdl2);
             float dacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(z[i], z[i], dacc[i & 3]);
+            for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(ZV(z, i), ZV(z, i), dacc[i & 3]);
             diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
@@ -1014,9 +1014,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         {
             float v64[64], v16[16];
 #pragma unroll
-            for (int i = 0; i < 64; ++i) v64[i] = z[i] * lamv;
+            for (int i = 0; i < 64; ++i) v64[i] = ZV(z, i) * lamv;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? z[64 + i] * lamv : 0.f;
+            for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? ZV(z, 64 + i < NG ? 64 + i : 0) * lamv : 0.f;
             float yl = reduce_scatter<64>(v64);
             float y2 = __shfl(reduce_scatter<16>(v16), 4 * (lane & 15), W);
             yl *= L.sDinv[lane];

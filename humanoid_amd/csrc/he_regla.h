@@ -85,6 +85,17 @@ __device__ __forceinline__ void fnma(float& z, float a, float b) {
     asm volatile("v_fma_f32 %0, -%1, %2, %0" : "+v"(z) : "v"(a), "v"(b));
 }
 
+// z, z' -= a * b, a' * b as one v_pk_fma_f32, b taken from half HALF of its register pair
+template <int HALF>
+__device__ __forceinline__ void pk_fnma(f2v& z, f2v a, f2v b) {
+    if constexpr (HALF == 0)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+                     : "+v"(z) : "v"(a), "v"(b));
+    else
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+                     : "+v"(z) : "v"(a), "v"(b));
+}
+
 // ---------------------------------------------------------------- per-lane z <- L^-T z (each lane its own rhs)
 // the packed row K (D entries) as registers: ceil(D/4) 16-byte LDS broadcasts
 template <int D>
@@ -98,15 +109,29 @@ __device__ __forceinline__ Row<kDofNanc[K] - 1> load_row(const float* Lp, int of
     for (int q = 0; q < (kDofNanc[K] - 1 + 3) / 4; ++q) r.v[q] = *reinterpret_cast<const f4v*>(Lp + off + 4 * q);
     return r;
 }
+// a contact row's dof vector, dofs (2k, 2k+1) in one aligned register pair
+struct ZVec {
+    f2v p[(NG + 1) / 2];
+};
+#define ZV(z, i) (z).p[(i) >> 1][(i) & 1]
+
 template <int K, int X, int D>
-__device__ __forceinline__ void zbs_anc(const Row<D>& row, float (&z)[NG], float zk) {
+__device__ __forceinline__ void zbs_anc(const Row<D>& row, ZVec& z) {
     if constexpr (X < D) {
+        constexpr int I = kChain[K][X];
+        constexpr bool PAIR = X % 2 == 0 && X + 1 < D && I % 2 == 0 && kChain[K][X + 1 < kMaxChain ? X + 1 : 0] == I + 1;
         const f4v v = row.v[X / 4];
-        fnma(z[kChain[K][X]], v.x, zk);
-        if constexpr (X + 1 < D) fnma(z[kChain[K][X + 1]], v.y, zk);
-        if constexpr (X + 2 < D) fnma(z[kChain[K][X + 2]], v.z, zk);
-        if constexpr (X + 3 < D) fnma(z[kChain[K][X + 3]], v.w, zk);
-        zbs_anc<K, X + 4, D>(row, z, zk);
+        if constexpr (PAIR) {  // z[I], z[I+1] -= L[K][I], L[K][I+1] * z[K]: one v_pk_fma_f32
+            const f2v l = X % 4 == 0 ? __builtin_shufflevector(v, v, 0, 1) : __builtin_shufflevector(v, v, 2, 3);
+            pk_fnma<K & 1>(z.p[I >> 1], l, z.p[K >> 1]);
+            zbs_anc<K, X + 2, D>(row, z);
+        } else {
+            const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
+            float t = ZV(z, I);
+            fnma(t, l, ZV(z, K));
+            ZV(z, I) = t;
+            zbs_anc<K, X + 1, D>(row, z);
+        }
     }
 }
 // z <- L^-T z, one dof per step, software-pipelined: the next row is read (16-byte LDS
@@ -138,7 +163,7 @@ __device__ __forceinline__ void undef_row(Row<D>& r) {
     }
 }
 template <int K>
-__device__ __forceinline__ void zbs_pipe(const float* Lp, float (&z)[NG], uint32_t lb, const typename RowOf<K>::T& rk) {
+__device__ __forceinline__ void zbs_pipe(const float* Lp, ZVec& z, uint32_t lb, const typename RowOf<K>::T& rk) {
     if constexpr (K >= 1) {
         typename RowOf<K - 1>::T nx;
         if constexpr (K - 1 >= 1) {
@@ -150,13 +175,13 @@ __device__ __forceinline__ void zbs_pipe(const float* Lp, float (&z)[NG], uint32
                 undef_row(nx);
             }
         }
-        if (body_live<K>(lb)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z, z[K]);
+        if (body_live<K>(lb)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z);
         __builtin_amdgcn_sched_barrier(0);
         zbs_pipe<K - 1>(Lp, z, lb, nx);
     }
 }
 template <int K>
-__device__ __forceinline__ void zbs(const float* Lp, float (&z)[NG], uint32_t lb) {
+__device__ __forceinline__ void zbs(const float* Lp, ZVec& z, uint32_t lb) {
     int off = 0;
     asm volatile("" : "+v"(off));
     const auto r0 = load_row_if<K>(Lp, off);
@@ -288,15 +313,6 @@ __device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st) {
 // unscaled on lane j, read in place from M). Chain positions X, X+1 holding dofs I, I+1 with X and
 // I even share both a row register pair and a column register pair: one v_pk_fma_f32, with H[K][j]
 // taken from half (K & 1) of K's column pair for both products.
-template <int HALF>
-__device__ __forceinline__ void pk_fnma(f2v& z, f2v a, f2v b) {
-    if constexpr (HALF == 0)
-        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
-                     : "+v"(z) : "v"(a), "v"(b));
-    else
-        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
-                     : "+v"(z) : "v"(a), "v"(b));
-}
 template <int K, int X, int D>
 __device__ __forceinline__ void fac_anc_pk(RegMat& M, const Row<D>& row) {
     if constexpr (X < D) {
