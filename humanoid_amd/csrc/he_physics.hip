@@ -80,7 +80,7 @@ HE_DEV void sync() {
 HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
 
 // optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
-// s_memtime deltas per phase into stamps[block * 16 + phase]
+// s_memtime deltas per phase into stamps[block * HE_STAMP_SLOTS + phase]
 #define STAMP(id)                                                             \
     do {                                                                      \
         if (stamps && lane == 0) {                                            \
@@ -139,56 +139,27 @@ HE_DEV float terrain_dist(const he_sim_params& p, int kind, f3 x, f3& n) {
     return x.z;
 }
 
-HE_DEV void body_segment(const he_model& m, const Lds& L, int b, f3& a, f3& c, float& r) {
-    const float* g = m.geom_params[b];
-    int gt = m.geom_type[b];
-    if (gt == HE_GEOM_SPHERE) {
-        a = body_point(L, b, f3{g[0], g[1], g[2]});
-        c = a;
-        r = g[3];
-    } else if (gt == HE_GEOM_CAPSULE) {
-        a = body_point(L, b, f3{g[0], g[1], g[2]});
-        c = body_point(L, b, f3{g[3], g[4], g[5]});
-        r = g[6];
-    } else {  // box -> capsule proxy along its longest axis
-        float e0 = g[3], e1 = g[4], e2 = g[5];
-        int ax = 0;
-        float emax = e0;
-        if (e1 > emax) { ax = 1; emax = e1; }
-        if (e2 > emax) { ax = 2; emax = e2; }
-        float rp = m.geom_radius[b];
-        float half = fmaxf(emax - rp, 0.f);
-        f4 bq = f4{g[6], g[7], g[8], g[9]};
-        f3 unit = ax == 0 ? f3{1.f, 0.f, 0.f} : (ax == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
-        f3 dir = qapply(bq, unit) * half;
-        f3 ctr = f3{g[0], g[1], g[2]};
-        a = body_point(L, b, ctr - dir);
-        c = body_point(L, b, ctr + dir);
-        r = rp;
-    }
-}
-
-// closest points between segments p1q1 and p2q2 (Ericson, RTCD 5.1.9)
+// closest points between segments p1q1 and p2q2 (Ericson, RTCD 5.1.9), branch-free: every case
+// (both degenerate, one degenerate, general with its two t-clamps) is formed and selected, so a
+// wave of mixed sphere / capsule pairs runs one path
 HE_DEV void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3& c1, f3& c2) {
-    f3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
-    float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
-    float s, t;
+    const f3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
+    const float a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
     const float eps = 1e-12f;
     // divisions as v_rcp_f32 products (1 ulp; the fp64 oracle's tolerance covers it)
     const float ia = __builtin_amdgcn_rcpf(a), ie = __builtin_amdgcn_rcpf(e);
-    if (a <= eps && e <= eps) { s = t = 0.f; }
-    else if (a <= eps) { s = 0.f; t = __builtin_amdgcn_fmed3f(f * ie, 0.f, 1.f); }
-    else {
-        float c = dot3(d1, r);
-        if (e <= eps) { t = 0.f; s = __builtin_amdgcn_fmed3f(-c * ia, 0.f, 1.f); }
-        else {
-            float b = dot3(d1, d2), den = a * e - b * b;
-            s = den > eps ? __builtin_amdgcn_fmed3f((b * f - c * e) * __builtin_amdgcn_rcpf(den), 0.f, 1.f) : 0.f;
-            t = (b * s + f) * ie;
-            if (t < 0.f) { t = 0.f; s = __builtin_amdgcn_fmed3f(-c * ia, 0.f, 1.f); }
-            else if (t > 1.f) { t = 1.f; s = __builtin_amdgcn_fmed3f((b - c) * ia, 0.f, 1.f); }
-        }
-    }
+    const float c = dot3(d1, r), b = dot3(d1, d2), den = a * e - b * b;
+    const float sg = den > eps ? __builtin_amdgcn_fmed3f((b * f - c * e) * __builtin_amdgcn_rcpf(den), 0.f, 1.f) : 0.f;
+    const float tg = (b * sg + f) * ie;
+    const float s_lo = __builtin_amdgcn_fmed3f(-c * ia, 0.f, 1.f);       // t clamped to 0 (and e degenerate)
+    const float s_hi = __builtin_amdgcn_fmed3f((b - c) * ia, 0.f, 1.f);  // t clamped to 1
+    float s = tg < 0.f ? s_lo : (tg > 1.f ? s_hi : sg);
+    float t = tg < 0.f ? 0.f : (tg > 1.f ? 1.f : tg);
+    const bool adeg = a <= eps, edeg = e <= eps;
+    s = edeg ? s_lo : s;
+    t = edeg ? 0.f : t;
+    s = adeg ? 0.f : s;
+    t = adeg ? (edeg ? 0.f : __builtin_amdgcn_fmed3f(f * ie, 0.f, 1.f)) : t;
     c1 = p1 + d1 * s;
     c2 = p2 + d2 * t;
 }
@@ -349,37 +320,34 @@ HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uin
 }
 
 // one Gauss-Seidel sweep over the contacts: normal row clamped at 0, friction rows to the pyramid
-// |lambda_t| <= mu lambda_n. Lane r holds w_r, lambda_r and 1/A[r][r], so each row's candidate
-// impulse is computed lane-parallel from VGPRs (only lane r's result is used); one v_readlane
-// carries the impulse change d to the column update w += A[.][r] * d of every lane. muL: lane r
-// holds the friction coefficient of row r's contact (the bound is formed beside the candidate).
-template <int R, bool NORMAL>
-HE_DEV void pgs_row(float& w, float& lamv, const float (&acol)[MAXR], float invd, float muL, float& ln) {
-    const float c = fmaf(-w, invd, lamv);
-    float nt;
-    if constexpr (NORMAL) {
-        nt = fmaxf(c, 0.f);
-    } else {
-        const float bnd = muL * ln;
-        nt = __builtin_amdgcn_fmed3f(c, -bnd, bnd);
-    }
-    const float d = regla::rdlane(nt - lamv, R);
-    const float s = regla::rdlane(nt, R);
-    if constexpr (NORMAL) ln = s;
-    lamv = regla::wrlane<R>(s, lamv);  // lane R only, no lane mask
-    w = fmaf(acol[R], d, w);
-}
-
+// |lambda_t| <= mu lambda_n, in delta form. Lane r holds cd_r = -w_r / A[r][r] (the unconstrained
+// impulse change of row r), lambda_r as of the sweep's start and the negated scaled Delassus
+// column acolp[R] = -A[R][r] / A[r][r]. Row R's change is the clamp of cd_R against the bounds
+// shifted by lambda_R (max(cd, -lambda) for a normal row), so the dependent chain per row is
+// clamp -> v_readlane -> fma: the change d goes to every lane's cd += acolp[R] * d and into lane
+// R of dvec; lambda += dvec once per sweep. The friction bounds mu (lambda_n + d_n) -+ lambda
+// are two fmas on the normal row's d from bases formed at the sweep's start (off the chain).
 template <int CI>
-HE_DEV void pgs_sweep(float& w, float& lamv, const float (&acol)[MAXR], float invd, float muL, int nc) {
+HE_DEV void pgs_sweep(float& cd, float& dvec, const float& lamv, const float (&acolp)[MAXR], float muL, int nc) {
     if constexpr (CI < MAXC) {
         if (CI >= nc) return;
         constexpr int R0 = 3 * CI;
-        float ln = 0.f;
-        pgs_row<R0, true>(w, lamv, acol, invd, muL, ln);
-        pgs_row<R0 + 1, false>(w, lamv, acol, invd, muL, ln);
-        pgs_row<R0 + 2, false>(w, lamv, acol, invd, muL, ln);
-        pgs_sweep<CI + 1>(w, lamv, acol, invd, muL, nc);
+        // bounds of this contact's friction rows: mu lambda_n(start) -+ lambda_row, per lane
+        const float lnold = regla::rdlane(lamv, R0);
+        const float hb = fmaf(muL, lnold, -lamv), lbs = fmaf(-muL, lnold, -lamv);
+        // normal row
+        const float dn = regla::rdlane(__builtin_amdgcn_fmed3f(cd, -lamv, __builtin_inff()), R0);  // max, one op
+        dvec = regla::wrlane<R0>(dn, dvec);
+        cd = fmaf(acolp[R0], dn, cd);
+        const float hi = fmaf(muL, dn, hb), lo = fmaf(-muL, dn, lbs);
+        // friction rows
+        const float d1 = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R0 + 1);
+        dvec = regla::wrlane<R0 + 1>(d1, dvec);
+        cd = fmaf(acolp[R0 + 1], d1, cd);
+        const float d2 = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R0 + 2);
+        dvec = regla::wrlane<R0 + 2>(d2, dvec);
+        cd = fmaf(acolp[R0 + 2], d2, cd);
+        pgs_sweep<CI + 1>(cd, dvec, lamv, acolp, muL, nc);
     }
 }
 
@@ -798,53 +766,75 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
     const int maxc = p.max_contacts < MAXC ? p.max_contacts : MAXC;
     const float off = p.contact_offset;
     int nc = 0;
+    // self-collision pair indices of the four rounds (independent of the state: issued first)
+    constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
+    int2 prs[ROUNDS];
+    const int npairs = m.num_pairs;
+#pragma unroll
+    for (int rd = 0; rd < ROUNDS; ++rd) {
+        const int pi = rd * W + lane;
+        prs[rd] = *reinterpret_cast<const int2*>(m.pairs[pi < npairs ? pi : 0]);
+        if (pi >= npairs) prs[rd].x = -1;
+    }
     {
-        // per body: sphere 1, capsule 2 (end spheres), box up to 4 deepest corners (ranked by depth,
-        // ties by corner index -- the oracle's selection order); fully unrolled, no scratch arrays
-        int b = lane < NB ? lane : 0;
+        // per-body collision geometry (lane = body), one path for every geometry type:
+        //  self segment P0-P1, radius rs: sphere P0 = P1 = centre; capsule from / to; box the
+        //    capsule proxy along its longest axis (radius geom_radius)
+        //  terrain candidates, radius rt: sphere the centre; capsule from, to; box the 8 corners
+        //    around its centre Pc (world centre +- the world half-axes, which are 0 for the others)
+        const int b = lane < NB ? lane : 0;
         const float* g = m.geom_params[b];
-        int gt = m.geom_type[b];
+        float gv[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) gv[i] = g[i];
+        const int gt = m.geom_type[b];
+        const float grad = m.geom_radius[b];
+        const bool isS = gt == HE_GEOM_SPHERE, isC = gt == HE_GEOM_CAPSULE, isB = !isS && !isC;
+        const f4 bq = isB ? f4{gv[6], gv[7], gv[8], gv[9]} : f4{0.f, 0.f, 0.f, 1.f};
+        int ax = 0;
+        float emax = gv[3];
+        if (gv[4] > emax) { ax = 1; emax = gv[4]; }
+        if (gv[5] > emax) { ax = 2; emax = gv[5]; }
+        const float half = fmaxf(emax - grad, 0.f);
+        const f3 unit = ax == 0 ? f3{1.f, 0.f, 0.f} : (ax == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
+        const f3 dir = qapply(bq, unit) * half;
+        const f3 ctr = f3{gv[0], gv[1], gv[2]};
+        const f3 l0 = isB ? ctr - dir : ctr;
+        const f3 l1 = isB ? ctr + dir : (isC ? f3{gv[3], gv[4], gv[5]} : ctr);
+        const float rs = isS ? gv[3] : (isC ? gv[6] : grad);
+        const float rt = isS ? gv[3] : (isC ? gv[6] : 0.f);
+        const f3 P0 = body_point(L, b, l0), P1 = body_point(L, b, l1), Pc = body_point(L, b, ctr);
+        if (p.self_collision && lane < NB) {
+            // world segments (the Ib scratch is dead after the subtree sums) with the bounding
+            // radius about the segment midpoint for the pair cull
+            float* sg = L.Ib[lane];
+            sg[0] = P0.x; sg[1] = P0.y; sg[2] = P0.z; sg[3] = P1.x; sg[4] = P1.y; sg[5] = P1.z; sg[6] = rs;
+            sg[7] = 0.5f * norm3(P1 - P0) + rs;
+        }
+        const f4 qb = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
+        const f3 ex = qapply(qb, qapply(bq, f3{isB ? gv[3] : 0.f, 0.f, 0.f}));
+        const f3 ey = qapply(qb, qapply(bq, f3{0.f, isB ? gv[4] : 0.f, 0.f}));
+        const f3 ez = qapply(qb, qapply(bq, f3{0.f, 0.f, isB ? gv[5] : 0.f}));
+        const f3 base0 = isB ? Pc : P0;
+        const int ncand = lane < NB ? (isS ? 1 : (isC ? 2 : 8)) : 0;
         float cd[8];
         f3 cxs[8], cns[8];
         bool cand[8];
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) { cand[ci] = false; cd[ci] = 0.f; }
-        if (lane < NB) {
-            if (gt == HE_GEOM_SPHERE) {
-                f3 c = body_point(L, b, f3{g[0], g[1], g[2]});
-                cd[0] = terrain_dist(p, tkind, c, cns[0]) - g[3];
-                cxs[0] = c - cns[0] * g[3];
-                cand[0] = cd[0] < off;
-            } else if (gt == HE_GEOM_CAPSULE) {
-#pragma unroll
-                for (int e2 = 0; e2 < 2; ++e2) {
-                    f3 c = body_point(L, b, f3{g[3 * e2], g[3 * e2 + 1], g[3 * e2 + 2]});
-                    cd[e2] = terrain_dist(p, tkind, c, cns[e2]) - g[6];
-                    cxs[e2] = c - cns[e2] * g[6];
-                    cand[e2] = cd[e2] < off;
-                }
-            } else {
-                // corners = world centre +- the three world half-axes (4 rotations, not 16)
-                const f4 bq = f4{g[6], g[7], g[8], g[9]};
-                const f4 qb = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
-                const f3 ctr = body_point(L, b, f3{g[0], g[1], g[2]});
-                const f3 ex = qapply(qb, qapply(bq, f3{g[3], 0.f, 0.f}));
-                const f3 ey = qapply(qb, qapply(bq, f3{0.f, g[4], 0.f}));
-                const f3 ez = qapply(qb, qapply(bq, f3{0.f, 0.f, g[5]}));
-#pragma unroll
-                for (int ci = 0; ci < 8; ++ci) {
-                    cxs[ci] = ((ctr + ((ci & 1) ? ex : ex * -1.f)) + ((ci & 2) ? ey : ey * -1.f)) + ((ci & 4) ? ez : ez * -1.f);
-                    cd[ci] = terrain_dist(p, tkind, cxs[ci], cns[ci]);
-                    cand[ci] = cd[ci] < off;
-                }
-            }
+        for (int ci = 0; ci < 8; ++ci) {
+            const f3 bs = (ci == 1 && isC) ? P1 : base0;
+            const f3 x = ((bs + ((ci & 1) ? ex : ex * -1.f)) + ((ci & 2) ? ey : ey * -1.f)) + ((ci & 4) ? ez : ez * -1.f);
+            cd[ci] = terrain_dist(p, tkind, x, cns[ci]) - rt;
+            cxs[ci] = x - cns[ci] * rt;
+            cand[ci] = ci < ncand && cd[ci] < off;
         }
+        STAMP(14);
         // rank among this body's candidates: box corners by depth, ties (and sphere / capsule end
         // points, keyed 0) by index; one comparison per unordered pair serves both ranks
         int rank[8];
         float key[8];
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) { rank[ci] = 0; key[ci] = gt == HE_GEOM_BOX ? cd[ci] : 0.f; }
+        for (int ci = 0; ci < 8; ++ci) { rank[ci] = 0; key[ci] = isB ? cd[ci] : 0.f; }
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci)
 #pragma unroll
@@ -857,74 +847,100 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci)
             if (cand[ci] && rank[ci] < 4) ++myn;
-        int incl = myn;
-        for (int s2 = 1; s2 < W; s2 <<= 1) {
-            int v = __shfl_up(incl, s2, W);
-            if (lane >= s2) incl += v;
+        // exclusive prefix of myn (0..4) over the lanes: three bit ballots, v_mbcnt per bit
+        int base = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint64_t bm = __ballot((myn >> k) & 1);
+            base += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << k;
+            total += __popcll(bm) << k;
         }
-        int total = __shfl(incl, W - 1, W);
-        int base = incl - myn;
+        STAMP(16);
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci)
             if (cand[ci] && rank[ci] < 4 && base + rank[ci] < maxc)
                 store_contact(L, base + rank[ci], b, -1, cxs[ci], cns[ci], cd[ci], mu);
         nc = total < maxc ? total : maxc;
     }
+    STAMP(17);
     if (p.self_collision && nc < maxc) {
-        // world-space collision segments once per body (lane = body) into the Ib scratch
-        // (dead after the subtree sums), so each pair lane only gathers two of them
-        float (*seg)[10] = L.Ib;
-        if (lane < NB) {
-            f3 a, c;
-            float r;
-            body_segment(m, L, lane, a, c, r);
-            seg[lane][0] = a.x; seg[lane][1] = a.y; seg[lane][2] = a.z;
-            seg[lane][3] = c.x; seg[lane][4] = c.y; seg[lane][5] = c.z; seg[lane][6] = r;
+        sync();
+        STAMP(18);
+        // broad phase: a pair whose bounding spheres (segment midpoint, half length + radius) are
+        // apart by more than the contact offset plus a 1 mm guard cannot reach gap < offset; the
+        // survivors are compacted in pair order into the lam scratch (dead until the solver)
+        int* list = reinterpret_cast<int*>(L.lam);
+        int nsurv = 0;
+#pragma unroll
+        for (int rd = 0; rd < ROUNDS; ++rd) {
+            const int i = prs[rd].x, j = prs[rd].y;
+            bool need = false;
+            if (i >= 0) {
+                const float* si = L.Ib[i];
+                const float* sj = L.Ib[j];
+                const f3 d = (f3{si[0], si[1], si[2]} + f3{si[3], si[4], si[5]}) - (f3{sj[0], sj[1], sj[2]} + f3{sj[3], sj[4], sj[5]});
+                const float lim = 2.f * (si[7] + sj[7] + off + 1e-3f);  // d is twice the midpoint offset
+                need = dot3(d, d) < lim * lim;
+            }
+            const uint64_t bm = __ballot(need);
+            const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+            if (need && slot < W) list[slot] = (rd * W + lane) | (i << 16) | (j << 24);
+            nsurv += __popcll(bm);
         }
         sync();
-        // every round's segment test first: four independent dependency chains per lane
-        constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
-        bool hit[ROUNDS];
-        f3 px[ROUNDS], pn[ROUNDS];
-        float pgap[ROUNDS];
-        int pi0[ROUNDS], pj0[ROUNDS];
-#pragma unroll
-        for (int rd = 0; rd < ROUNDS; ++rd) {
-            const int pi = rd * W + lane;
-            hit[rd] = false;
-            pgap[rd] = 0.f;
-            pi0[rd] = 0;
-            pj0[rd] = 0;
-            px[rd] = pn[rd] = f3{0.f, 0.f, 0.f};
-            if (pi < m.num_pairs) {
-                const int i = m.pairs[pi][0], j = m.pairs[pi][1];
-                pi0[rd] = i;
-                pj0[rd] = j;
-                const float* si = seg[i];
-                const float* sj = seg[j];
-                const f3 a0 = f3{si[0], si[1], si[2]}, a1 = f3{si[3], si[4], si[5]};
-                const f3 b0 = f3{sj[0], sj[1], sj[2]}, b1 = f3{sj[3], sj[4], sj[5]};
+        STAMP(19);
+        // narrow phase on the survivors, W per pass, in pair order
+        for (int s0 = 0; s0 < nsurv && nc < maxc; s0 += W) {
+            bool hit = false;
+            f3 px = f3{0.f, 0.f, 0.f}, pn = f3{0.f, 0.f, 0.f};
+            float pgap = 0.f;
+            int i = 0, j = 0;
+            if (s0 + lane < nsurv) {
+                const int e = list[lane];
+                i = (e >> 16) & 0xFF;
+                j = (e >> 24) & 0xFF;
+                const float* si = L.Ib[i];
+                const float* sj = L.Ib[j];
                 const float ri = si[6], rj = sj[6];
                 f3 ci, cj;
-                seg_seg(a0, a1, b0, b1, ci, cj);
+                seg_seg(f3{si[0], si[1], si[2]}, f3{si[3], si[4], si[5]}, f3{sj[0], sj[1], sj[2]}, f3{sj[3], sj[4], sj[5]}, ci, cj);
                 const f3 dv = ci - cj;
                 const float len = norm3(dv);
-                pgap[rd] = len - ri - rj;
-                if (pgap[rd] < off) {
-                    hit[rd] = true;
-                    pn[rd] = len > 1e-9f ? dv * __builtin_amdgcn_rcpf(len) : f3{0.f, 0.f, 1.f};
-                    px[rd] = cj + pn[rd] * (rj + 0.5f * pgap[rd]);
+                pgap = len - ri - rj;
+                if (pgap < off) {
+                    hit = true;
+                    pn = len > 1e-9f ? dv * __builtin_amdgcn_rcpf(len) : f3{0.f, 0.f, 1.f};
+                    px = cj + pn * (rj + 0.5f * pgap);
                 }
             }
-        }
-#pragma unroll
-        for (int rd = 0; rd < ROUNDS; ++rd) {
             int total;
-            const int pre = wave_prefix(hit[rd], lane, total);
-            if (hit[rd] && nc + pre < maxc) store_contact(L, nc + pre, pi0[rd], pj0[rd], px[rd], pn[rd], pgap[rd], mu);
+            const int pre = wave_prefix(hit, lane, total);
+            if (hit && nc + pre < maxc) store_contact(L, nc + pre, i, j, px, pn, pgap, mu);
             nc = nc + total < maxc ? nc + total : maxc;
+            if (s0 + W < nsurv) {  // more than W survivors: compact the next pass (rare)
+                sync();
+                // recompute the next W survivors into the list
+                int k = 0;
+                for (int rd = 0; rd < ROUNDS; ++rd) {
+                    const int ii = prs[rd].x, jj = prs[rd].y;
+                    bool need = false;
+                    if (ii >= 0) {
+                        const float* si = L.Ib[ii];
+                        const float* sj = L.Ib[jj];
+                        const f3 d = (f3{si[0], si[1], si[2]} + f3{si[3], si[4], si[5]}) - (f3{sj[0], sj[1], sj[2]} + f3{sj[3], sj[4], sj[5]});
+                        const float lim = 2.f * (si[7] + sj[7] + off + 1e-3f);
+                        need = dot3(d, d) < lim * lim;
+                    }
+                    const uint64_t bm = __ballot(need);
+                    const int slot = k + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) - (s0 + W);
+                    if (need && slot >= 0 && slot < W) list[slot] = (rd * W + lane) | (ii << 16) | (jj << 24);
+                    k += __popcll(bm);
+                }
+                sync();
+            }
         }
     }
+    STAMP(15);
     if (lane == 0) L.nc = nc;
     if (lane < NB) { L.cf[lane][0] = 0.f; L.cf[lane][1] = 0.f; L.cf[lane][2] = 0.f; }
     sync();
@@ -1000,11 +1016,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
         STAMP(9);
         // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
         {
-            float w = lane < nr ? brow : 0.f;
             const float invd = 1.0f / (lane < nr ? diag + 1e-12f : 1.f);
+            float cd = lane < nr ? -brow * invd : 0.f;
+            const float ninvd = -invd;
+#pragma unroll
+            for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
             const float muL = lane < nr ? L.cmu[lane / 3] : 0.f;
             const int ncu = __builtin_amdgcn_readfirstlane(nc);
-            for (int it = 0; it < p.solver_iterations; ++it) pgs_sweep<0>(w, lamv, acol, invd, muL, ncu);
+            for (int it = 0; it < p.solver_iterations; ++it) {
+                float dvec = 0.f;
+                pgs_sweep<0>(cd, dvec, lamv, acol, muL, ncu);
+                lamv += dvec;
+            }
         }
         L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();
@@ -1137,7 +1160,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     const float* ms = a.mass_scale ? a.mass_scale + (size_t)e * NB : nullptr;
     float mu = a.friction ? a.friction[e] : a.p.friction;
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;
-    unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * 16 : nullptr;
+    unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * HE_STAMP_SLOTS : nullptr;
     unsigned long long t_prev = __builtin_readcyclecounter();
     for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev);
     // ---- outputs: generalized state, FK rigid-body state, forces

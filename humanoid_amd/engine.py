@@ -384,7 +384,7 @@ class Engine:
         _check(self.lib.he_set_amp(self.h, C.byref(b)))
 
     def set_debug_stamps(self, buf=None):
-        """Diagnostics: int64 [num_envs, 16] device tensor receiving per-phase cycles, or None."""
+        """Diagnostics: int64 [num_envs, 32] (HE_STAMP_SLOTS) device tensor receiving per-phase cycles, or None."""
         import torch
         if buf is not None:
             self._contig(buf, torch.int64)

@@ -27,6 +27,7 @@ extern "C" {
 #define HE_NUM_DOF 69
 #define HE_NUM_GEN 75          /* 6 root + 69 joint generalized velocities */
 #define HE_MAX_PAIRS 256
+#define HE_STAMP_SLOTS 32 /* diagnostic per-phase cycle slots per env (he_set_debug_stamps) */
 #define HE_MAX_CONTACTS 21       /* 3 rows each: all contact rows of an env fit one 64-lane wave */
 #define HE_OBS_SELF 358
 #define HE_OBS_TASK 576
@@ -283,7 +284,7 @@ int he_amp_observations(int k, const float* root_pos, const float* root_rot, con
                         const float* key_body_pos, float* out, void* stream);
 
 /* Diagnostics: when non-NULL, the physics kernel accumulates per-phase shader cycles into
- * device_buffer [N][16] (u64; phases listed in DESIGN.md §4). NULL disables (default). */
+ * device_buffer [N][HE_STAMP_SLOTS] (u64; phases listed in DESIGN.md §4). NULL disables (default). */
 int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer);
 
 /* hash-based uniform used by he_env_step (exposed for parity tests): out[k] for env ids[k]. */

@@ -13,7 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba", "ltdl factor", "free solve",
-          "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write"]
+          "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write",
+          "terrain: geometry", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
+          "self: segments", "self: segment tests"]  # slots 14-19 are carved out of "contact gen"
 
 
 def main():
@@ -34,7 +36,7 @@ def main():
     ro = bench.Rollout(bargs, model, 0, 0)
     for _ in range(args.warmup):
         ro.step()
-    buf = torch.zeros(args.num_envs, 16, dtype=torch.int64, device=ro.eng.device)
+    buf = torch.zeros(args.num_envs, 32, dtype=torch.int64, device=ro.eng.device)
     ro.eng.set_debug_stamps(buf)
     nc = []
     for _ in range(args.steps):
@@ -47,9 +49,6 @@ def main():
     total = mean[:len(PHASES)].sum()
     rows = {PHASES[i]: {"cycles": round(float(mean[i])), "share": round(float(mean[i] / total), 4)}
             for i in range(len(PHASES))}
-    # sub-phase slots 14/15 (when a diagnostic build stamps them) are carved out of their phase
-    extra = {f"slot{i}": round(float(mean[i])) for i in range(len(PHASES), 16) if mean[i] != 0}
-    rows.update(extra)
     print(json.dumps({"config": args.config, "num_envs": args.num_envs, "mean_contacts": float(np.mean(nc)),
                       "cycles_per_env_step": round(float(total)), "phases": rows}, indent=1))
 
