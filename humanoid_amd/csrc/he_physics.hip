@@ -172,6 +172,20 @@ HE_DEV void friction_basis(f3 n, f3& t1, f3& t2) {
     t2 = cross3(n, t1);
 }
 
+// OR over the wave as a wave-uniform value: quad and row DPP mirrors, then the 16- and 32-lane
+// permlane swaps (no LDS crossbar round trips)
+HE_DEV uint32_t wave_or(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    const auto r16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    x = r16[0] | r16[1];
+    const auto r32 = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    x = r32[0] | r32[1];
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+
 // wave-wide exclusive prefix count of `flag` (uint64 ballot)
 HE_DEV int wave_prefix(bool flag, int lane, int& total) {
     uint64_t m = __ballot(flag);
@@ -969,10 +983,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
             const f3 dd = f3{dir[0], dir[1], dir[2]};
             const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o, dd);
             // bodies on some row's support (wave-uniform): the only ones whose dofs can be nonzero
-            uint32_t lb = anc0 | anc1;
-#pragma unroll
-            for (int sh = 32; sh > 0; sh >>= 1) lb |= (uint32_t)__shfl_xor((int)lb, sh, W);
-            lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)lb);
+            const uint32_t lb = wave_or(anc0 | anc1);
             // z = J_r^T and brow = J_r uf, four dofs per pinned group (their LDS reads overlap; the
             // results are fixed in place so the loads cannot all be hoisted ahead of the math)
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -996,7 +1007,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
                 const float g = L.cgap[ci];
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
+            STAMP(20);
             zbs<NG - 1>(L.Lp, z, lb);
+            STAMP(21);
             // z <- D^-1/2 z: the scale of dof i is broadcast from lane i's register (no LDS)
             const float sdl = L.sDinv[lane], sdl2 = lane < NH ? L.sDinv[64 + lane] : 0.f;
             scale_rows<0>(z, sdl, sdl2);
