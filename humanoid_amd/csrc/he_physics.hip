@@ -646,10 +646,15 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
 }
 
 // ---------------------------------------------------------------------------------- one substep
-HE_DEV void substep(Lds& L0, const PhysArgs& a, const he_model* mp, int lane,
+HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
                     unsigned long long& t_prev) {
     using namespace regla;
+    // the launch arguments through an opaque offset too: their fields are re-read (scalar loads
+    // from the kernarg segment) where used instead of being held in SGPRs across the substep loop
+    int ao = 0;
+    asm volatile("" : "+s"(ao));
+    const PhysArgs& a = *reinterpret_cast<const PhysArgs*>(reinterpret_cast<const char*>(&a0) + ao);
     // opaque per substep: keeps the compiler from hoisting ~1k uniform model loads out of the
     // substep loop into SGPRs (which then spill into VGPR lanes)
     // (an opaque byte offset rather than an opaque pointer: the pointer keeps its global address
