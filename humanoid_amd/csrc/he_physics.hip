@@ -125,15 +125,24 @@ HE_DEV f3 body_point(const Lds& L, int b, f3 local) {
     return f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} + qapply(q, local);
 }
 
-HE_DEV float terrain_dist(const he_sim_params& p, int kind, f3 x, f3& n) {
-    if (kind == 1) {
-        float s = sinf(p.terrain_slope), c = cosf(p.terrain_slope);
-        n = f3{-s, 0.f, c};
+// terrain constants of the env, read once per contact phase (slope normal, step field)
+struct Terrain {
+    int kind;
+    float sn, cs, step_h, step_l;
+};
+HE_DEV Terrain terrain_of(const he_sim_params& p, int kind) {
+    Terrain t{kind, 0.f, 1.f, p.step_height, p.step_length};
+    if (kind == 1) { t.sn = sinf(p.terrain_slope); t.cs = cosf(p.terrain_slope); }
+    return t;
+}
+HE_DEV float terrain_dist(const Terrain& t, f3 x, f3& n) {
+    if (t.kind == 1) {
+        n = f3{-t.sn, 0.f, t.cs};
         return dot3(n, x);
     }
     n = f3{0.f, 0.f, 1.f};
-    if (kind == 2) {
-        float h = x.x > 0.f ? p.step_height * floorf(x.x / p.step_length) : 0.f;
+    if (t.kind == 2) {
+        float h = x.x > 0.f ? t.step_h * floorf(x.x / t.step_l) : 0.f;
         return x.z - h;
     }
     return x.z;
@@ -764,6 +773,28 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     sync();
     STAMP(5);
+    // the contact phase's model reads (geometry of the lane's body, self-collision pair indices)
+    // depend on nothing computed here: issued now, they land behind the free-velocity sweep
+    constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
+    float gv[10];
+    int gt;
+    float grad;
+    int2 prs[ROUNDS];
+    const int npairs = m.num_pairs;
+    {
+        const int b = lane < NB ? lane : 0;
+        const float* g = m.geom_params[b];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) gv[i] = g[i];
+        gt = m.geom_type[b];
+        grad = m.geom_radius[b];
+#pragma unroll
+        for (int rd = 0; rd < ROUNDS; ++rd) {
+            const int pi = rd * W + lane;
+            prs[rd] = *reinterpret_cast<const int2*>(m.pairs[pi < npairs ? pi : 0]);
+            if (pi >= npairs) prs[rd].x = -1;
+        }
+    }
     // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs): the L^-1 sweep
     {
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
@@ -784,17 +815,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     // ---- contacts: terrain (bodies in order, box corners deepest-first), then self pairs
     const int maxc = p.max_contacts < MAXC ? p.max_contacts : MAXC;
     const float off = p.contact_offset;
+    const Terrain ter = terrain_of(p, tkind);
+    const bool self_col = p.self_collision;
     int nc = 0;
-    // self-collision pair indices of the four rounds (independent of the state: issued first)
-    constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
-    int2 prs[ROUNDS];
-    const int npairs = m.num_pairs;
-#pragma unroll
-    for (int rd = 0; rd < ROUNDS; ++rd) {
-        const int pi = rd * W + lane;
-        prs[rd] = *reinterpret_cast<const int2*>(m.pairs[pi < npairs ? pi : 0]);
-        if (pi >= npairs) prs[rd].x = -1;
-    }
     {
         // per-body collision geometry (lane = body), one path for every geometry type:
         //  self segment P0-P1, radius rs: sphere P0 = P1 = centre; capsule from / to; box the
@@ -802,12 +825,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         //  terrain candidates, radius rt: sphere the centre; capsule from, to; box the 8 corners
         //    around its centre Pc (world centre +- the world half-axes, which are 0 for the others)
         const int b = lane < NB ? lane : 0;
-        const float* g = m.geom_params[b];
-        float gv[10];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) gv[i] = g[i];
-        const int gt = m.geom_type[b];
-        const float grad = m.geom_radius[b];
         const bool isS = gt == HE_GEOM_SPHERE, isC = gt == HE_GEOM_CAPSULE, isB = !isS && !isC;
         const f4 bq = isB ? f4{gv[6], gv[7], gv[8], gv[9]} : f4{0.f, 0.f, 0.f, 1.f};
         int ax = 0;
@@ -823,7 +840,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const float rs = isS ? gv[3] : (isC ? gv[6] : grad);
         const float rt = isS ? gv[3] : (isC ? gv[6] : 0.f);
         const f3 P0 = body_point(L, b, l0), P1 = body_point(L, b, l1), Pc = body_point(L, b, ctr);
-        if (p.self_collision && lane < NB) {
+        if (self_col && lane < NB) {
             // world segments (the Ib scratch is dead after the subtree sums) with the bounding
             // radius about the segment midpoint for the pair cull
             float* sg = L.Ib[lane];
@@ -843,7 +860,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         for (int ci = 0; ci < 8; ++ci) {
             const f3 bs = (ci == 1 && isC) ? P1 : base0;
             const f3 x = ((bs + ((ci & 1) ? ex : ex * -1.f)) + ((ci & 2) ? ey : ey * -1.f)) + ((ci & 4) ? ez : ez * -1.f);
-            cd[ci] = terrain_dist(p, tkind, x, cns[ci]) - rt;
+            cd[ci] = terrain_dist(ter, x, cns[ci]) - rt;
             cxs[ci] = x - cns[ci] * rt;
             cand[ci] = ci < ncand && cd[ci] < off;
         }
@@ -882,7 +899,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         nc = total < maxc ? total : maxc;
     }
     STAMP(17);
-    if (p.self_collision && nc < maxc) {
+    if (self_col && nc < maxc) {
         sync();
         STAMP(18);
         // broad phase: a pair whose bounding spheres (segment midpoint, half length + radius) are
