@@ -125,6 +125,25 @@ HE_DEV f3 body_point(const Lds& L, int b, f3 local) {
     return f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} + qapply(q, local);
 }
 
+// rotation-vector exponential / logarithm for the physics kernel: one sincos range reduction and
+// v_rcp_f32 quotients (1 ulp; the fp64 oracle's tolerance covers it). The imitation kernel keeps
+// he_math.h's forms, which follow torch's rounding.
+HE_DEV f4 pqexp(f3 v) {
+    const float th = norm3(v);
+    if (th < 1e-8f) return qnormalize(f4{0.5f * v.x, 0.5f * v.y, 0.5f * v.z, 1.f});
+    float sh, ch;
+    sincosf(0.5f * th, &sh, &ch);
+    const float s = sh * __builtin_amdgcn_rcpf(th);
+    return f4{v.x * s, v.y * s, v.z * s, ch};
+}
+HE_DEV f3 pqlog(f4 q) {
+    if (q.w < 0.f) q = qneg(q);
+    const float s = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+    if (s < 1e-8f) return f3{2.f * q.x, 2.f * q.y, 2.f * q.z};
+    const float k = 2.f * atan2f(s, q.w) * __builtin_amdgcn_rcpf(s);
+    return f3{q.x * k, q.y * k, q.z * k};
+}
+
 // terrain constants of the env, read once per contact phase (slope normal, step field)
 struct Terrain {
     int kind;
@@ -556,7 +575,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         u[0] = L.u0[0]; u[1] = L.u0[1]; u[2] = L.u0[2];
     } else {
         const int d = 3 * (b - 1);
-        q = qexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
+        q = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
         p = f3{T.local_pos[b][0], T.local_pos[b][1], T.local_pos[b][2]};
         u[0] = L.u0[6 + d]; u[1] = L.u0[7 + d]; u[2] = L.u0[8 + d];
     }
@@ -866,18 +885,20 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         }
         STAMP(14);
         // rank among this body's candidates: box corners by depth, ties (and sphere / capsule end
-        // points, keyed 0) by index; one comparison per unordered pair serves both ranks
+        // points, keyed 0) by index; non-candidates keyed +inf never go first. With rank[k]
+        // starting at k, one comparison per unordered pair i < j moves both ranks:
+        // rank[k] = #{i < k : key_i <= key_k} + #{j > k : key_j < key_k} (vector ops only)
         int rank[8];
         float key[8];
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) { rank[ci] = 0; key[ci] = isB ? cd[ci] : 0.f; }
+        for (int ci = 0; ci < 8; ++ci) { rank[ci] = ci; key[ci] = cand[ci] ? (isB ? cd[ci] : 0.f) : __builtin_inff(); }
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci)
 #pragma unroll
             for (int cj = ci + 1; cj < 8; ++cj) {
-                const bool j_first = key[cj] < key[ci];  // else i goes first (i < j breaks ties)
-                rank[ci] += (cand[cj] && j_first) ? 1 : 0;
-                rank[cj] += (cand[ci] && !j_first) ? 1 : 0;
+                const int c = key[cj] < key[ci] ? 1 : 0;  // j goes first
+                rank[ci] += c;
+                rank[cj] -= c;
             }
         int myn = 0;
 #pragma unroll
@@ -1137,14 +1158,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     if (lane < NB) {
         if (lane == 0) {
             for (int c = 0; c < 3; ++c) L.root_pos[c] += dt * L.u0[3 + c];
-            f4 dq = qexp(f3{dt * L.u0[0], dt * L.u0[1], dt * L.u0[2]});
+            f4 dq = pqexp(f3{dt * L.u0[0], dt * L.u0[1], dt * L.u0[2]});
             f4 nq = qnormalize(qmul(dq, f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]}));
             L.root_q[0] = nq.x; L.root_q[1] = nq.y; L.root_q[2] = nq.z; L.root_q[3] = nq.w;
         } else {
             int d = 3 * (lane - 1), g = 6 + d;
-            f4 ql = qexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
-            f4 dq = qexp(f3{dt * L.u0[g], dt * L.u0[g + 1], dt * L.u0[g + 2]});
-            f3 nv = qlog(qnormalize(qmul(ql, dq)));
+            f4 ql = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
+            f4 dq = pqexp(f3{dt * L.u0[g], dt * L.u0[g + 1], dt * L.u0[g + 2]});
+            f3 nv = pqlog(qnormalize(qmul(ql, dq)));
             L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
         }
     }
