@@ -70,6 +70,21 @@ struct Lds {
     BodyTopo T;
 };
 
+// wave priority over the serial chains (PGS rows, the elimination, the L^-T sweep) against the
+// partner wave's throughput phases (diagnostic knobs, s_setprio 0..3)
+#ifndef HE_PRIO_PGS
+#define HE_PRIO_PGS 3
+#endif
+#ifndef HE_PRIO_FACTOR
+#define HE_PRIO_FACTOR 3
+#endif
+#ifndef HE_PRIO_SOLVE
+#define HE_PRIO_SOLVE 0
+#endif
+#ifndef HE_PRIO_KIN
+#define HE_PRIO_KIN 0
+#endif
+
 // wave-level ordering point: one wave per workgroup, LDS executes its instructions in order, so
 // only the compiler must not move memory operations across phase boundaries
 HE_DEV void sync() {
@@ -701,7 +716,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     const BodyTopo& T = L.T;
     const he_sim_params& p = a.p;
     const float dt = p.dt;
+    __builtin_amdgcn_s_setprio(HE_PRIO_KIN);
     kinematics<true>(L, m, lane, a.p);
+    __builtin_amdgcn_s_setprio(0);
     STAMP(0);
     const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
     // ---- body spatial inertias about o + RNEA body forces (gravity as base acceleration)
@@ -739,7 +756,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     sync();
     STAMP(1);
     // ---- subtree sums: F_b (forces) and composite inertias, in place by body levels
+    __builtin_amdgcn_s_setprio(HE_PRIO_KIN);
     subtree_levels<16, smpl::kNumBodyLevels - 2>(&L.F[0][0], &L.Ic[0][0], lane);
+    __builtin_amdgcn_s_setprio(0);
     STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
     for (int i = lane; i < NG; i += W) {
@@ -783,7 +802,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     float yl = L.rhs[lane], y2 = lane < NH ? L.rhs[64 + lane] : 0.f;
     {
         float Dl = 1.f, D2 = 1.f;
+        __builtin_amdgcn_s_setprio(HE_PRIO_FACTOR);
         factor_lds_groups<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
+        __builtin_amdgcn_s_setprio(0);
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
@@ -825,7 +846,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             r1[4 * q] = a1.x; r1[4 * q + 1] = a1.y; r1[4 * q + 2] = a1.z; r1[4 * q + 3] = a1.w;
             r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
         }
+        __builtin_amdgcn_s_setprio(HE_PRIO_SOLVE);
         regla::solve_L_rows<0>(r1, r2, yl, y2);
+        __builtin_amdgcn_s_setprio(0);
         L.uf[lane] = L.u0[lane] + yl;
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
     }
@@ -1051,7 +1074,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             STAMP(20);
+            __builtin_amdgcn_s_setprio(HE_PRIO_FACTOR);
             zbs<NG - 1>(L.Lp, z, lb);
+            __builtin_amdgcn_s_setprio(0);
             STAMP(21);
             // z <- D^-1/2 z: the scale of dof i is broadcast from lane i's register (no LDS)
             const float sdl = L.sDinv[lane], sdl2 = lane < NH ? L.sDinv[64 + lane] : 0.f;
@@ -1079,11 +1104,13 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
             const float muL = lane < nr ? L.cmu[lane / 3] : 0.f;
             const int ncu = __builtin_amdgcn_readfirstlane(nc);
+            __builtin_amdgcn_s_setprio(HE_PRIO_PGS);
             for (int it = 0; it < p.solver_iterations; ++it) {
                 float dvec = 0.f;
                 pgs_sweep<0>(cd, dvec, lamv, acol, muL, ncu);
                 lamv += dvec;
             }
+            __builtin_amdgcn_s_setprio(0);
         }
         L.lam[lane] = lane < nr ? lamv : 0.f;
         sync();
@@ -1091,6 +1118,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
         // a wave reduce-scatter sums the 75 columns into lane = dof, then one L^-1 sweep
         {
+            __builtin_amdgcn_s_setprio(HE_PRIO_SOLVE);
             float v64[64], v16[16];
 #pragma unroll
             for (int i = 0; i < 64; ++i) v64[i] = ZV(z, i) * lamv;
@@ -1110,6 +1138,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
             }
             regla::solve_L_rows<0>(r1, r2, yl, y2);
+            __builtin_amdgcn_s_setprio(0);
             L.uf[lane] += yl;
             if (lane < NH) L.uf[64 + lane] += y2;
         }

@@ -42,7 +42,8 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = path or LIB_PATH
+    # HE_ENGINE_LIB: diagnostics only (A/B timing of a variant build, tools/build_variant.py)
+    p = path or os.environ.get("HE_ENGINE_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise EngineError(f"{p} not found: build it with `python -m humanoid_amd.build` (hipcc, gfx950)")
     lib = C.CDLL(p)
