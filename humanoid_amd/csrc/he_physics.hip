@@ -393,17 +393,20 @@ HE_DEV void pgs_sweep(float& cd, float& dvec, const float& lamv, const float (&a
         const float lnold = regla::rdlane(lamv, R0);
         const float hb = fmaf(muL, lnold, -lamv), lbs = fmaf(-muL, lnold, -lamv);
         // normal row
-        const float dn = regla::rdlane(__builtin_amdgcn_fmed3f(cd, -lamv, __builtin_inff()), R0);  // max, one op
-        dvec = regla::wrlane<R0>(dn, dvec);
+        // (each change's v_writelane into dvec is issued after the fma that the next row waits on)
+        float cn;  // max(cd, -lambda): one v_max (no NaN-quieting canonicalize pair)
+        asm("v_max_f32 %0, %1, %2" : "=v"(cn) : "v"(cd), "v"(-lamv));
+        const float dn = regla::rdlane(cn, R0);
         cd = fmaf(acolp[R0], dn, cd);
         const float hi = fmaf(muL, dn, hb), lo = fmaf(-muL, dn, lbs);
+        dvec = regla::wrlane<R0>(dn, dvec);
         // friction rows
         const float d1 = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R0 + 1);
-        dvec = regla::wrlane<R0 + 1>(d1, dvec);
         cd = fmaf(acolp[R0 + 1], d1, cd);
+        dvec = regla::wrlane<R0 + 1>(d1, dvec);
         const float d2 = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R0 + 2);
-        dvec = regla::wrlane<R0 + 2>(d2, dvec);
         cd = fmaf(acolp[R0 + 2], d2, cd);
+        dvec = regla::wrlane<R0 + 2>(d2, dvec);
         pgs_sweep<CI + 1>(cd, dvec, lamv, acolp, muL, nc);
     }
 }
