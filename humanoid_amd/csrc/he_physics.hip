@@ -66,7 +66,8 @@ struct Lds {
     float cf[NB][3];
     float dforce[ND];
     float root_pos[3], root_q[4];
-    int nc;
+    int nc, nterr;                 // contacts, of which terrain (slots [0, nterr), grouped by body)
+    int8_t tbase[NB], tcnt[NB];    // body b's terrain contacts: slots tbase[b] .. + tcnt[b]
     BodyTopo T;
 };
 
@@ -944,6 +945,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             if (cand[ci] && rank[ci] < 4 && base + rank[ci] < maxc)
                 store_contact(L, base + rank[ci], b, -1, cxs[ci], cns[ci], cd[ci], mu);
         nc = total < maxc ? total : maxc;
+        if (lane < NB) {  // the body's slot range, for the per-body force sums
+            L.tbase[lane] = (int8_t)(base < maxc ? base : maxc);
+            L.tcnt[lane] = (int8_t)(base + myn < maxc ? myn : (base < maxc ? maxc - base : 0));
+        }
+        if (lane == 0) L.nterr = nc;
     }
     STAMP(17);
     if (self_col && nc < maxc) {
@@ -1156,13 +1162,21 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         }
         sync();
         if (lane < NB) {
+            // the body's own terrain contacts (a contiguous slot range, in slot order), then the
+            // self-pair contacts with their sign; the same summation order as over all slots
             float F3[3] = {0.f, 0.f, 0.f};
+            const int tb = L.tbase[lane], tn = L.tcnt[lane];
 #pragma unroll
-            for (int c = 0; c < MAXC; ++c) {
-                if (c < nc) {
-                    const float sg = (L.cb0[c] == lane ? 1.f : 0.f) - (L.cb1[c] == lane ? 1.f : 0.f);
-                    for (int x = 0; x < 3; ++x) F3[x] += sg * fc[c][x];
+            for (int k = 0; k < 4; ++k) {
+                if (k < tn) {
+                    const int c = tb + k;
+                    for (int x = 0; x < 3; ++x) F3[x] += fc[c][x];
                 }
+            }
+            const int nterr = __builtin_amdgcn_readfirstlane(L.nterr);
+            for (int c = nterr; c < nc; ++c) {  // wave-uniform bounds
+                const float sg = (L.cb0[c] == lane ? 1.f : 0.f) - (L.cb1[c] == lane ? 1.f : 0.f);
+                for (int x = 0; x < 3; ++x) F3[x] += sg * fc[c][x];
             }
             L.cf[lane][0] = F3[0] / dt; L.cf[lane][1] = F3[1] / dt; L.cf[lane][2] = F3[2] / dt;
         }
