@@ -68,6 +68,7 @@ struct Lds {
     float root_pos[3], root_q[4];
     int nc, nterr;                 // contacts, of which terrain (slots [0, nterr), grouped by body)
     int8_t tbase[NB], tcnt[NB];    // body b's terrain contacts: slots tbase[b] .. + tcnt[b]
+    float4 bsph[NB];               // per-body bounding sphere of the collision segment (cull)
     BodyTopo T;
 };
 
@@ -879,24 +880,31 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         if (gv[5] > emax) { ax = 2; emax = gv[5]; }
         const float half = fmaxf(emax - grad, 0.f);
         const f3 unit = ax == 0 ? f3{1.f, 0.f, 0.f} : (ax == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
-        const f3 dir = qapply(bq, unit) * half;
+        // rotations as matrices (the box's local frame and the body's world rotation): six
+        // mat-vecs instead of ten quaternion applications
+        f3 bc0, bc1, bc2, wc0, wc1, wc2;
+        qcols(bq, bc0, bc1, bc2);
+        qcols(f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]}, wc0, wc1, wc2);
+        const f3 pwb = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]};
+        const f3 dir = (ax == 0 ? bc0 : (ax == 1 ? bc1 : bc2)) * half;
         const f3 ctr = f3{gv[0], gv[1], gv[2]};
         const f3 l0 = isB ? ctr - dir : ctr;
         const f3 l1 = isB ? ctr + dir : (isC ? f3{gv[3], gv[4], gv[5]} : ctr);
         const float rs = isS ? gv[3] : (isC ? gv[6] : grad);
         const float rt = isS ? gv[3] : (isC ? gv[6] : 0.f);
-        const f3 P0 = body_point(L, b, l0), P1 = body_point(L, b, l1), Pc = body_point(L, b, ctr);
+        auto rot = [&](f3 v) { return (wc0 * v.x + wc1 * v.y) + wc2 * v.z; };
+        const f3 P0 = pwb + rot(l0), P1 = pwb + rot(l1), Pc = pwb + rot(ctr);
         if (self_col && lane < NB) {
-            // world segments (the Ib scratch is dead after the subtree sums) with the bounding
-            // radius about the segment midpoint for the pair cull
+            // world segments (the Ib scratch is dead after the subtree sums), and the bounding
+            // sphere about the segment midpoint for the pair cull as one 16-byte record
             float* sg = L.Ib[lane];
             sg[0] = P0.x; sg[1] = P0.y; sg[2] = P0.z; sg[3] = P1.x; sg[4] = P1.y; sg[5] = P1.z; sg[6] = rs;
-            sg[7] = 0.5f * norm3(P1 - P0) + rs;
+            const f3 mid = (P0 + P1) * 0.5f;
+            L.bsph[lane] = make_float4(mid.x, mid.y, mid.z, 0.5f * norm3(P1 - P0) + rs);
         }
-        const f4 qb = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
-        const f3 ex = qapply(qb, qapply(bq, f3{isB ? gv[3] : 0.f, 0.f, 0.f}));
-        const f3 ey = qapply(qb, qapply(bq, f3{0.f, isB ? gv[4] : 0.f, 0.f}));
-        const f3 ez = qapply(qb, qapply(bq, f3{0.f, 0.f, isB ? gv[5] : 0.f}));
+        const f3 ex = rot(bc0 * (isB ? gv[3] : 0.f));
+        const f3 ey = rot(bc1 * (isB ? gv[4] : 0.f));
+        const f3 ez = rot(bc2 * (isB ? gv[5] : 0.f));
         const f3 base0 = isB ? Pc : P0;
         const int ncand = lane < NB ? (isS ? 1 : (isC ? 2 : 8)) : 0;
         float cd[8];
@@ -965,10 +973,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const int i = prs[rd].x, j = prs[rd].y;
             bool need = false;
             if (i >= 0) {
-                const float* si = L.Ib[i];
-                const float* sj = L.Ib[j];
-                const f3 d = (f3{si[0], si[1], si[2]} + f3{si[3], si[4], si[5]}) - (f3{sj[0], sj[1], sj[2]} + f3{sj[3], sj[4], sj[5]});
-                const float lim = 2.f * (si[7] + sj[7] + off + 1e-3f);  // d is twice the midpoint offset
+                const float4 bi = L.bsph[i], bj = L.bsph[j];
+                const f3 d = f3{bi.x - bj.x, bi.y - bj.y, bi.z - bj.z};
+                const float lim = bi.w + bj.w + off + 1e-3f;
                 need = dot3(d, d) < lim * lim;
             }
             const uint64_t bm = __ballot(need);
@@ -1014,10 +1021,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const int ii = prs[rd].x, jj = prs[rd].y;
                     bool need = false;
                     if (ii >= 0) {
-                        const float* si = L.Ib[ii];
-                        const float* sj = L.Ib[jj];
-                        const f3 d = (f3{si[0], si[1], si[2]} + f3{si[3], si[4], si[5]}) - (f3{sj[0], sj[1], sj[2]} + f3{sj[3], sj[4], sj[5]});
-                        const float lim = 2.f * (si[7] + sj[7] + off + 1e-3f);
+                        const float4 bi = L.bsph[ii], bj = L.bsph[jj];
+                        const f3 d = f3{bi.x - bj.x, bi.y - bj.y, bi.z - bj.z};
+                        const float lim = bi.w + bj.w + off + 1e-3f;
                         need = dot3(d, d) < lim * lim;
                     }
                     const uint64_t bm = __ballot(need);
