@@ -80,6 +80,9 @@ struct Lds {
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
 #endif
+#ifndef HE_CRBA_MFMA
+#define HE_CRBA_MFMA 1
+#endif
 #ifndef HE_PRIO_SOLVE
 #define HE_PRIO_SOLVE 0
 #endif
@@ -515,6 +518,90 @@ HE_DEV void crba_groups(regla::RegMat& M, const float (&Sj)[6], const float (&Sj
     }
 }
 
+// CRBA on the matrix cores: H = IS^T S as v_mfma_f32_32x32x2_f32 tiles (rows i, columns j, K = the
+// six spatial components in three steps), lower block triangle only: 6 tiles, 18 MFMAs. Operands
+// come straight from LDS (lane l: IS_{32R + l%32}[2s + l/32] and S_{32C + l%32}[2s + l/32]). One
+// v_permlane32_swap per register pair of a row block's column-tile pair lands "lane j holds column
+// j" (RegMat), then the ancestor masks and the diagonal addends as in crba_row.
+template <int RB>
+HE_DEV void crba_tile_rows(regla::RegMat& M, const f32x16& ta, const f32x16& tb) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int r = RB + (v & 3) + 8 * (v >> 2);
+        float a = ta[v], b = tb[v];
+        swap32(a, b);  // a: row r of columns (lane), b: row r + 4
+        if (r < NG) M.cp[r >> 1][r & 1] = a;
+        if (r + 4 < NG) M.cp[(r + 4 < NG ? r + 4 : 0) >> 1][(r + 4) & 1] = b;
+    }
+}
+template <int I>
+HE_DEV void crba_mask_rows(regla::RegMat& M, float dadd, float dadd2) {
+    using namespace regla;
+    if constexpr (I < NG) {
+        float h = lanes<smpl::kAncLo[I]>() ? mc<I>(M) : 0.f;
+        if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
+        asm volatile("" : "+v"(h));
+        mc_set<I>(M, h);
+        if constexpr (I >= 64) {
+            float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? mc2<I - 64>(M) : 0.f;
+            h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
+            asm volatile("" : "+v"(h2));
+            mc2_set<I - 64>(M, h2);
+        }
+        crba_mask_rows<I + 1>(M, dadd, dadd2);
+    }
+}
+HE_DEV void crba_mfma(regla::RegMat& M, const Lds& L, int lane, float dadd, float dadd2) {
+    const int l31 = lane & 31, kh = lane >> 5;
+    float bS[3][3], aI[3][3];  // [block][k step]
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int j = 32 * c + l31;
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            bS[c][st] = j < NG ? L.S[j < NG ? j : 0][2 * st + kh] : 0.f;
+            aI[c][st] = j < NG ? L.IS[j < NG ? j : 0][2 * st + kh] : 0.f;
+        }
+    }
+    const f32x16 zero = {};
+    {
+        f32x16 t0 = {};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aI[0][st], bS[0][st], t0, 0, 0, 0);
+        crba_tile_rows<0>(M, t0, zero);  // rows 0-31 are above the diagonal for columns 32-63
+    }
+    {
+        f32x16 t0 = {}, t1 = {};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aI[1][st], bS[0][st], t0, 0, 0, 0);
+            t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(aI[1][st], bS[1][st], t1, 0, 0, 0);
+        }
+        crba_tile_rows<32>(M, t0, t1);
+    }
+    {
+        f32x16 t0 = {}, t1 = {}, t2 = {};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aI[2][st], bS[0][st], t0, 0, 0, 0);
+            t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(aI[2][st], bS[1][st], t1, 0, 0, 0);
+            t2 = __builtin_amdgcn_mfma_f32_32x32x2f32(aI[2][st], bS[2][st], t2, 0, 0, 0);
+        }
+        crba_tile_rows<64>(M, t0, t1);
+        // columns 64-74 (second register set, lanes 0-10): rows r from the low half, r + 4 from
+        // the high half of the same tile
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int r = 64 + (v & 3) + 8 * (v >> 2);
+            float a = t2[v], b = t2[v];
+            swap32(a, b);
+            if (r < NG) M.cp2[(r - 64) >> 1][(r - 64) & 1] = a;
+            if (r + 4 < NG) M.cp2[(r + 4 < NG ? r - 60 : 0) >> 1][(r - 60) & 1] = b;
+        }
+    }
+    crba_mask_rows<0>(M, dadd, dadd2);
+}
+
 // In-place subtree sums X[b] += sum over children of X[c], parents of the deepest level first: at
 // each level, lane (parent, component) pulls its (at most three) children's finished sums. The
 // levels are unrolled at compile time, so parents and children are immediates selected by lane
@@ -796,10 +883,15 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // per-lane diagonal addend (dof = lane, and 64 + lane on lanes < 11), loaded once
         const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + dt * L.coef[lane] : 0.f;
         const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + dt * L.coef[64 + lane] : 0.f;
+#if HE_CRBA_MFMA
+        (void)Sj; (void)Sj2;
+        crba_mfma(M, L, lane, dadd, dadd2);
+#else
         float first[4][6];
         for (int k = 0; k < 4; ++k)
             for (int x = 0; x < 6; ++x) first[k][x] = L.IS[k][x];
         crba_groups<0>(M, Sj, Sj2, dadd, dadd2, L, first);
+#endif
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
