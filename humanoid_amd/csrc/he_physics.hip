@@ -80,6 +80,9 @@ struct Lds {
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
 #endif
+#ifndef HE_JT_MFMA
+#define HE_JT_MFMA 1
+#endif
 #ifndef HE_CRBA_MFMA
 #define HE_CRBA_MFMA 1
 #endif
@@ -443,6 +446,68 @@ HE_DEV void zrow_load(const Lds& L, int b, float (&d)[15]) {
         d[12 + c] = Lg.uf[i];
     }
 }
+// z = J_r^T on the matrix cores: C[i][r] = S_i . u_r with u_r = (rho, dd) of row r (lane r), as
+// v_mfma_f32_32x32x2_f32 tiles over the dof blocks of 32 that hold a live body (A = S from LDS, B =
+// the rows' 6-vectors redistributed by one permlane32 swap per k step). The two row tiles of a
+// block are paired by v_permlane32_swap into "lane r holds z[r][i]" (ZVec); then each dof takes its
+// body's sign for the row (+1 on the first contact body's chain, -1 on the second's, 0 elsewhere).
+constexpr uint32_t block_bodies(int D) {
+    uint32_t m = 0;
+    for (int i = 32 * D; i < 32 * D + 32 && i < NG; ++i) m |= 1u << (i < 6 ? 0 : (i - 6) / 3 + 1);
+    return m;
+}
+template <int D>
+HE_DEV void zrows_block(regla::ZVec& z, uint32_t lb, const float (&b0)[3], const float (&b1)[3], const Lds& L, int l31,
+                        int kh) {
+    if constexpr (32 * D < NG) {
+        if (lb & block_bodies(D)) {
+            float aS[3];
+            const int j = 32 * D + l31;
+#pragma unroll
+            for (int st = 0; st < 3; ++st) aS[st] = j < NG ? L.S[j < NG ? j : 0][2 * st + kh] : 0.f;
+            f32x16 t0 = {}, t1 = {};
+#pragma unroll
+            for (int st = 0; st < 3; ++st) {
+                t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aS[st], b0[st], t0, 0, 0, 0);
+                t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(aS[st], b1[st], t1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int i = 32 * D + (v & 3) + 8 * (v >> 2);
+                float a = t0[v], b = t1[v];
+                swap32(a, b);  // a: z[lane][i], b: z[lane][i + 4]
+                if (i < NG) ZV(z, i < NG ? i : 0) = a;
+                if (i + 4 < NG) ZV(z, i + 4 < NG ? i + 4 : 0) = b;
+            }
+        } else {
+#pragma unroll
+            for (int i = 32 * D; i < 32 * D + 32 && i < NG; ++i) ZV(z, i) = 0.f;
+        }
+        zrows_block<D + 1>(z, lb, b0, b1, L, l31, kh);
+    }
+}
+HE_DEV void zrows_mfma(regla::ZVec& z, uint32_t lb, uint32_t anc0, uint32_t anc1, f3 rho, f3 dd, const Lds& L,
+                       int lane) {
+    const int l31 = lane & 31, kh = lane >> 5;
+    float b0[3], b1[3];
+    {
+        const float u[6] = {rho.x, rho.y, rho.z, dd.x, dd.y, dd.z};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            float x = u[2 * st], y = u[2 * st + 1];
+            swap32(x, y);  // x: B operand of rows 0-31, y: of rows 32-63
+            b0[st] = x;
+            b1[st] = y;
+        }
+    }
+    zrows_block<0>(z, lb, b0, b1, L, l31, kh);
+    float sg[NB];
+#pragma unroll
+    for (int B = 0; B < NB; ++B) sg[B] = (float)((anc0 >> B) & 1u) - (float)((anc1 >> B) & 1u);
+#pragma unroll
+    for (int i = 0; i < NG; ++i) ZV(z, i) *= sg[i < 6 ? 0 : (i - 6) / 3 + 1];
+}
+
 // z_i = S_i . (rho, dd) = a_i . ((x - p_b) x dd) for joint b's three dofs, bodies in order with
 // the next live body's data read while this one is computed
 template <int B>
@@ -1160,6 +1225,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             // z = J_r^T and brow = J_r uf, four dofs per pinned group (their LDS reads overlap; the
             // results are fixed in place so the loads cannot all be hoisted ahead of the math)
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+#if HE_JT_MFMA
+            zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane);
+#pragma unroll
+            for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), L.uf[i], bacc[i & 3]);  // J_r uf
+#else
             {
                 // root: S = unit axes, so z = sgn0 * (rho, dd)
                 const float s0 = (float)(anc0 & 1u) - (float)(anc1 & 1u);
@@ -1175,6 +1245,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     for (int x = 0; x < 15; ++x) regla::undef_reg(cur[x]);
                 zrow_bodies<1>(z, bacc, lb, anc0, anc1, cx, dd, L, cur);
             }
+#endif
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
             if (lane < nr && kind == 0) {
                 const float g = L.cgap[ci];
