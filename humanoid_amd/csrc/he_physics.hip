@@ -80,6 +80,9 @@ struct Lds {
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
 #endif
+#ifndef HE_FAC_PIPE
+#define HE_FAC_PIPE 1
+#endif
 #ifndef HE_JT_MFMA
 #define HE_JT_MFMA 1
 #endif
@@ -965,7 +968,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     {
         float Dl = 1.f, D2 = 1.f;
         __builtin_amdgcn_s_setprio(HE_PRIO_FACTOR);
+#if HE_FAC_PIPE
+        factor_pipelined(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
+#else
         factor_lds_groups<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
+#endif
         __builtin_amdgcn_s_setprio(0);
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);

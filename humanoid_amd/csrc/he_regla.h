@@ -400,6 +400,126 @@ __device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st) {
     if constexpr (kDofNanc[K] - 1 > 0) st.row = load_row<K>(Lp, kPackStart[K]);
 #endif
 }
+// ---------------------------------------------------------------- software-pipelined groups
+// The next group's pivots only wait for the updates of their own rows. Those rows (I in chain(K)
+// and a pivot of group GI+1) take L[K][I] straight from lane I (one v_readlane) as soon as row K
+// is scaled; group GI+1 is then pivoted, stored and its LDS broadcast issued before group GI's
+// remaining updates wait for theirs. Every register still sees its updates in elimination order,
+// so the factor is bit-identical.
+template <int G>
+constexpr bool in_group(int I) {
+    if (G >= kElimGroups.count) return false;
+    for (int x = kElimGroups.start[G]; x < kElimGroups.start[G + 1]; ++x)
+        if (kElimOrder[x] == I) return true;
+    return false;
+}
+template <int K, int X, int D, int GN>
+__device__ __forceinline__ void fac_anc_fast(RegMat& M, const PivotStep<K>& st) {
+    if constexpr (X < D) {
+        constexpr int I = kChain[K][X];
+        if constexpr (in_group<GN>(I)) {
+            const float l = lrow<K, I>(st);
+            float c = mc<I>(M);
+            fnma(c, l, mc<K>(M));
+            mc_set<I>(M, c);
+            if constexpr (I >= 64) {
+                float c2 = mc2<I - 64>(M);
+                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                mc2_set<I - 64>(M, c2);
+            }
+        }
+        fac_anc_fast<K, X + 1, D, GN>(M, st);
+    }
+}
+template <int K, int X, int D, int GN>
+__device__ __forceinline__ void fac_anc_slow(RegMat& M, const Row<D>& row) {
+    if constexpr (X < D) {
+        constexpr int I = kChain[K][X];
+        constexpr bool FAST = in_group<GN>(I);
+        constexpr bool PAIR = !FAST && X % 2 == 0 && X + 1 < D && I % 2 == 0 && I + 1 < 64 &&
+                              kChain[K][X + 1 < kMaxChain ? X + 1 : 0] == I + 1 && !in_group<GN>(I + 1);
+        const f4v v = row.v[X / 4];
+        if constexpr (FAST) {
+            fac_anc_slow<K, X + 1, D, GN>(M, row);
+        } else if constexpr (PAIR) {
+            const f2v l = X % 4 == 0 ? __builtin_shufflevector(v, v, 0, 1) : __builtin_shufflevector(v, v, 2, 3);
+            pk_fnma<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
+            fac_anc_slow<K, X + 2, D, GN>(M, row);
+        } else {
+            const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
+            float c = mc<I>(M);
+            fnma(c, l, mc<K>(M));
+            mc_set<I>(M, c);
+            if constexpr (I >= 64) {
+                float c2 = mc2<I - 64>(M);
+                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                mc2_set<I - 64>(M, c2);
+            }
+            fac_anc_slow<K, X + 1, D, GN>(M, row);
+        }
+    }
+}
+template <int GI>
+struct GSteps {
+    static constexpr int S0 = kElimGroups.start[GI < kElimGroups.count ? GI : 0];
+    static constexpr int n = GI < kElimGroups.count ? kElimGroups.start[GI + 1] - S0 : 1;
+    static constexpr int K0 = kElimOrder[S0];
+    static constexpr int K1 = kElimOrder[n > 1 ? S0 + 1 : S0];
+    static constexpr int K2 = kElimOrder[n > 2 ? S0 + 2 : S0];
+    PivotStep<K0> a;
+    PivotStep<K1> b;
+    PivotStep<K2> c;
+};
+template <int K>
+__device__ __forceinline__ void grp_load_always(const float* Lp, PivotStep<K>& st) {
+    if constexpr (kDofNanc[K] - 1 > 0) st.row = load_row<K>(Lp, kPackStart[K]);
+}
+template <int GI>
+__device__ __forceinline__ void group_front(RegMat& M, GSteps<GI>& g, float* Lp, int dj, int dj2, float& yl, float& y2) {
+    using G = GSteps<GI>;
+    grp_pivot<G::K0>(M, g.a);
+    if constexpr (G::n > 1) grp_pivot<G::K1>(M, g.b);
+    if constexpr (G::n > 2) grp_pivot<G::K2>(M, g.c);
+    grp_store<G::K0>(g.a, Lp, dj, dj2, yl, y2);
+    if constexpr (G::n > 1) grp_store<G::K1>(g.b, Lp, dj, dj2, yl, y2);
+    if constexpr (G::n > 2) grp_store<G::K2>(g.c, Lp, dj, dj2, yl, y2);
+    grp_load_always<G::K0>(Lp, g.a);
+    if constexpr (G::n > 1) grp_load_always<G::K1>(Lp, g.b);
+    if constexpr (G::n > 2) grp_load_always<G::K2>(Lp, g.c);
+}
+template <int K, int GN>
+__device__ __forceinline__ void grp_finish(RegMat& M, float& Dl, float& D2, const PivotStep<K>& st) {
+    if constexpr (kDofNanc[K] - 1 > 0) fac_anc_slow<K, 0, kDofNanc[K] - 1, GN>(M, st.row);
+    mc_set<K>(M, st.l);  // row K -> L[K][.] on lanes j < K
+    if constexpr (K >= 64) mc2_set<K - 64>(M, st.l2);
+    if constexpr (K < 64) Dl = wrlane<K>(st.dk, Dl);
+    else D2 = wrlane<K - 64>(st.dk, D2);
+}
+template <int GI>
+__device__ __forceinline__ void factor_pipe(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2, float& yl,
+                                            float& y2, GSteps<GI>& g) {
+    if constexpr (GI < kElimGroups.count) {
+        using G = GSteps<GI>;
+        constexpr int GN = GI + 1;
+        if constexpr (kDofNanc[G::K0] - 1 > 0) fac_anc_fast<G::K0, 0, kDofNanc[G::K0] - 1, GN>(M, g.a);
+        if constexpr (G::n > 1 && kDofNanc[G::K1] - 1 > 0) fac_anc_fast<G::K1, 0, kDofNanc[G::K1] - 1, GN>(M, g.b);
+        if constexpr (G::n > 2 && kDofNanc[G::K2] - 1 > 0) fac_anc_fast<G::K2, 0, kDofNanc[G::K2] - 1, GN>(M, g.c);
+        GSteps<GN> gn;
+        if constexpr (GN < kElimGroups.count) group_front<GN>(M, gn, Lp, dj, dj2, yl, y2);
+        grp_finish<G::K0, GN>(M, Dl, D2, g.a);
+        if constexpr (G::n > 1) grp_finish<G::K1, GN>(M, Dl, D2, g.b);
+        if constexpr (G::n > 2) grp_finish<G::K2, GN>(M, Dl, D2, g.c);
+        __builtin_amdgcn_sched_barrier(0);
+        factor_pipe<GN>(M, Dl, D2, Lp, dj, dj2, yl, y2, gn);
+    }
+}
+__device__ __forceinline__ void factor_pipelined(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2, float& yl,
+                                                 float& y2) {
+    GSteps<0> g;
+    group_front<0>(M, g, Lp, dj, dj2, yl, y2);
+    factor_pipe<0>(M, Dl, D2, Lp, dj, dj2, yl, y2, g);
+}
+
 template <int GI>
 __device__ __forceinline__ void factor_lds_groups(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2,
                                                   float& yl, float& y2) {
