@@ -85,6 +85,30 @@ __device__ __forceinline__ void fnma(float& z, float a, float b) {
     asm volatile("v_fma_f32 %0, -%1, %2, %0" : "+v"(z) : "v"(a), "v"(b));
 }
 
+// the same without volatile: the scheduler may interleave them with independent work (data
+// dependences still order them)
+__device__ __forceinline__ void fnma_nv(float& z, float a, float b) {
+    asm("v_fma_f32 %0, -%1, %2, %0" : "+v"(z) : "v"(a), "v"(b));
+}
+template <int HALF>
+__device__ __forceinline__ void pk_fnma_nv(f2v& z, f2v a, f2v b) {
+    if constexpr (HALF == 0)
+        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "+v"(z) : "v"(a), "v"(b));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+            : "+v"(z) : "v"(a), "v"(b));
+}
+#ifndef HE_FAC_NV
+#define HE_FAC_NV 0
+#endif
+#if HE_FAC_NV
+#define FAC_FNMA fnma_nv
+#define FAC_PK_FNMA pk_fnma_nv
+#else
+#define FAC_FNMA fnma
+#define FAC_PK_FNMA pk_fnma
+#endif
+
 // z, z' -= a * b, a' * b as one v_pk_fma_f32, b taken from half HALF of its register pair
 template <int HALF>
 __device__ __forceinline__ void pk_fnma(f2v& z, f2v a, f2v b) {
@@ -267,7 +291,10 @@ struct ElimGroups {
         start[count] = NG;
     }
 };
-constexpr int kElimGroupMax = 2;
+#ifndef HE_ELIM_GMAX
+#define HE_ELIM_GMAX 2
+#endif
+constexpr int kElimGroupMax = HE_ELIM_GMAX;
 constexpr ElimGroups<kElimGroupMax> kElimGroups{};
 
 template <int K>
@@ -420,11 +447,11 @@ __device__ __forceinline__ void fac_anc_fast(RegMat& M, const PivotStep<K>& st) 
         if constexpr (in_group<GN>(I)) {
             const float l = lrow<K, I>(st);
             float c = mc<I>(M);
-            fnma(c, l, mc<K>(M));
+            FAC_FNMA(c, l, mc<K>(M));
             mc_set<I>(M, c);
             if constexpr (I >= 64) {
                 float c2 = mc2<I - 64>(M);
-                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                FAC_FNMA(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
                 mc2_set<I - 64>(M, c2);
             }
         }
@@ -443,16 +470,16 @@ __device__ __forceinline__ void fac_anc_slow(RegMat& M, const Row<D>& row) {
             fac_anc_slow<K, X + 1, D, GN>(M, row);
         } else if constexpr (PAIR) {
             const f2v l = X % 4 == 0 ? __builtin_shufflevector(v, v, 0, 1) : __builtin_shufflevector(v, v, 2, 3);
-            pk_fnma<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
+            FAC_PK_FNMA<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
             fac_anc_slow<K, X + 2, D, GN>(M, row);
         } else {
             const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
             float c = mc<I>(M);
-            fnma(c, l, mc<K>(M));
+            FAC_FNMA(c, l, mc<K>(M));
             mc_set<I>(M, c);
             if constexpr (I >= 64) {
                 float c2 = mc2<I - 64>(M);
-                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                FAC_FNMA(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
                 mc2_set<I - 64>(M, c2);
             }
             fac_anc_slow<K, X + 1, D, GN>(M, row);
