@@ -848,6 +848,20 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     sync();
 }
 
+// lane i's packed row of L (dof i) and the row of dof 64 + i (lanes >= NH read row 64 and never
+// use it: an exec-masked second load measured slower than the unmasked one, A/B r01)
+HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[regla::kRowRegs],
+                      float (&r2)[regla::kRowRegs]) {
+    const float4* p1 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane]);
+    const float4* p2 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane < regla::NH ? 64 + lane : 0]);
+#pragma unroll
+    for (int q = 0; q < regla::kRowRegs / 4; ++q) {
+        const float4 a1 = p1[q], a2 = p2[q];
+        r1[4 * q] = a1.x; r1[4 * q + 1] = a1.y; r1[4 * q + 2] = a1.z; r1[4 * q + 3] = a1.w;
+        r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
+    }
+}
+
 // ---------------------------------------------------------------------------------- one substep
 HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
@@ -1007,17 +1021,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs): the L^-1 sweep
     {
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
-        const float4* p1 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane]);
-        const float4* p2 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane < NH ? 64 + lane : 0]);
-#pragma unroll
-        for (int q = 0; q < regla::kRowRegs / 4; ++q) {
-            const float4 a1 = p1[q], a2 = p2[q];
-            r1[4 * q] = a1.x; r1[4 * q + 1] = a1.y; r1[4 * q + 2] = a1.z; r1[4 * q + 3] = a1.w;
-            r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
-        }
+        load_rows(L, T, lane, r1, r2);
+        STAMP(22);
         __builtin_amdgcn_s_setprio(HE_PRIO_SOLVE);
         regla::solve_L_rows<0>(r1, r2, yl, y2);
         __builtin_amdgcn_s_setprio(0);
+        STAMP(23);
         L.uf[lane] = L.u0[lane] + yl;
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
     }
@@ -1043,7 +1052,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         if (gv[4] > emax) { ax = 1; emax = gv[4]; }
         if (gv[5] > emax) { ax = 2; emax = gv[5]; }
         const float half = fmaxf(emax - grad, 0.f);
-        const f3 unit = ax == 0 ? f3{1.f, 0.f, 0.f} : (ax == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
         // rotations as matrices (the box's local frame and the body's world rotation): six
         // mat-vecs instead of ten quaternion applications
         f3 bc0, bc1, bc2, wc0, wc1, wc2;
@@ -1314,14 +1322,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             yl *= L.sDinv[lane];
             y2 = lane < NH ? y2 * L.sDinv[64 + lane] : 0.f;
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
-            const float4* p1 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane]);
-            const float4* p2 = reinterpret_cast<const float4*>(L.Lp + T.pack_start[lane < NH ? 64 + lane : 0]);
-#pragma unroll
-            for (int q = 0; q < regla::kRowRegs / 4; ++q) {
-                const float4 a1 = p1[q], a2 = p2[q];
-                r1[4 * q] = a1.x; r1[4 * q + 1] = a1.y; r1[4 * q + 2] = a1.z; r1[4 * q + 3] = a1.w;
-                r2[4 * q] = a2.x; r2[4 * q + 1] = a2.y; r2[4 * q + 2] = a2.z; r2[4 * q + 3] = a2.w;
-            }
+            load_rows(L, T, lane, r1, r2);
             regla::solve_L_rows<0>(r1, r2, yl, y2);
             __builtin_amdgcn_s_setprio(0);
             L.uf[lane] += yl;

@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba", "ltdl factor", "free solve",
           "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write",
           "terrain: geometry", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
-          "self: segments", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep"]  # slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows"
+          "self: segments", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
+          "free: prefetch + row loads", "free: L^-1 levels"]  # slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
 
 
 def main():
