@@ -483,3 +483,80 @@ extern "C" int he_gae_minibatch(const float* dones, const float* values, const f
               num_minibatches, minibatch_rows, bptt_horizon, b_advantages, b_returns};
     return launch_gae(a, static_cast<hipStream_t>(stream));
 }
+
+// ---------------------------------------------------------------- PHCPufferEnv.step bookkeeping
+namespace {
+constexpr int EB_THREADS = 256;  // 10 x 256 doubles of LDS for the tree
+struct EpisodeArgs {
+    int n;
+    const float* rew;
+    const float* reward_raw;
+    const uint8_t* reset;
+    const uint8_t* terminate;
+    float* rew_out;
+    uint8_t* term_out;
+    uint8_t* terminals;
+    uint8_t* truncations;
+    uint8_t* masks;
+    float* episode_returns;
+    int32_t* episode_lengths;
+    float* raw_rewards;
+    double* acc;
+};
+// one workgroup: per-thread strided partial sums, then a fixed-order tree in LDS (deterministic)
+__global__ void __launch_bounds__(EB_THREADS) episode_step_kernel(EpisodeArgs a) {
+    __shared__ double red[10][EB_THREADS];
+    const int tid = threadIdx.x;
+    double s[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = tid; i < a.n; i += EB_THREADS) {
+        const bool r = a.reset[i] != 0, t = a.terminate[i] != 0;
+        const bool term = t && r, trunc = r && !t;
+        a.terminals[i] = term;
+        a.truncations[i] = trunc;
+        a.masks[i] = !trunc;
+        const float rw = a.rew[i];
+        a.rew_out[i] = rw;
+        a.term_out[i] = t;
+        const float ret = a.episode_returns[i];
+        const int32_t len = a.episode_lengths[i];
+        if (r) {
+            s[0] += (double)ret;
+            s[1] += (double)len;
+            s[2] += 1.0;
+        }
+        s[3] += trunc ? 1.0 : 0.0;
+        s[4] += term ? 1.0 : 0.0;
+        a.episode_returns[i] = r ? 0.0f : ret + rw;
+        a.episode_lengths[i] = r ? 0 : len + 1;
+        const float* rr = a.reward_raw + (size_t)i * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s[5 + k] += (double)rr[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) red[k][tid] = s[k];
+    __syncthreads();
+    for (int w = EB_THREADS / 2; w > 0; w >>= 1) {
+        if (tid < w)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) red[k][tid] += red[k][tid + w];
+        __syncthreads();
+    }
+    if (tid < 5) a.acc[tid] += red[tid][0];
+    if (tid >= 5 && tid < 10 && a.n > 0) a.raw_rewards[tid - 5] += (float)(red[tid][0] / (double)a.n);
+}
+}  // namespace
+
+extern "C" int he_episode_step(int32_t num_envs, const float* rew, const float* reward_raw, const uint8_t* reset,
+                               const uint8_t* terminate, float* rew_out, uint8_t* term_out, uint8_t* terminals,
+                               uint8_t* truncations, uint8_t* masks, float* episode_returns, int32_t* episode_lengths,
+                               float* raw_rewards, double* acc, void* stream) {
+    if (num_envs < 0) return he_fail_text("he_episode_step: negative num_envs");
+    if (num_envs > 0 && (!rew || !reward_raw || !reset || !terminate || !rew_out || !term_out || !terminals ||
+                         !truncations || !masks || !episode_returns || !episode_lengths || !raw_rewards || !acc))
+        return he_fail_text("he_episode_step: null argument");
+    if (num_envs == 0) return 0;
+    EpisodeArgs a{num_envs, rew, reward_raw, reset, terminate, rew_out, term_out, terminals, truncations, masks,
+                  episode_returns, episode_lengths, raw_rewards, acc};
+    episode_step_kernel<<<1, EB_THREADS, 0, static_cast<hipStream_t>(stream)>>>(a);
+    return check_launch("he_episode_step");
+}

@@ -33,7 +33,7 @@ HE_SYMBOLS = (
     "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips", "he_set_eval",
     "he_set_amp", "he_amp_observations",
     # include/humanoid_rollout.h
-    "he_rollout_store", "he_rollout_order", "he_rollout_gather", "he_gae", "he_gae_minibatch",
+    "he_rollout_store", "he_rollout_order", "he_rollout_gather", "he_gae", "he_gae_minibatch", "he_episode_step",
 )
 
 
@@ -75,6 +75,7 @@ def load_library(path: Optional[str] = None):
         "he_rollout_gather": [V, I, V, C.c_int64, C.c_int32, C.c_int32, C.c_int32, V],
         "he_gae": [V, V, V, C.c_int64, F, F, V, V],
         "he_gae_minibatch": [V, V, V, V, V, C.c_int64, F, F, C.c_int32, C.c_int32, C.c_int32, V, V, V],
+        "he_episode_step": [C.c_int32] + [V] * 14,
     }
     for name, args in sigs.items():
         fn = getattr(lib, name)

@@ -388,6 +388,11 @@ class PHCPufferEnv:
         # device-side accumulators of the reference's per-episode info lists (env.py:80-84)
         self._acc = torch.zeros(5, dtype=torch.float64, device=dev)  # sum_ret, sum_len, n_ep, n_trunc, n_term
         self.tick = 0
+        # numpy actions go through two pinned host buffers (alternating, each reused only after its
+        # previous host-to-device copy has completed), so the copy is asynchronous and the host runs
+        # ahead of the device instead of blocking on a pageable transfer every step
+        self._pinned = [torch.empty(n, NUM_ACTIONS, dtype=torch.float32).pin_memory() for _ in range(2)]
+        self._pinned_done = [None, None]
 
     @property
     def num_agents(self):
@@ -409,9 +414,17 @@ class PHCPufferEnv:
         """``actions``: numpy [N,69] (copied to the device, as env.py:112) or a device tensor."""
         import torch
         if isinstance(actions, np.ndarray):
-            if self.cfg.clip_actions:
-                actions = np.clip(actions, -1, 1)
-            self.actions[:] = torch.from_numpy(np.ascontiguousarray(actions, np.float32))
+            k = self.tick & 1
+            if self._pinned_done[k] is not None:
+                self._pinned_done[k].synchronize()
+            buf = self._pinned[k]
+            buf.numpy()[...] = actions
+            self.actions.copy_(buf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pinned_done[k] = ev
+            if self.cfg.clip_actions:  # env.py:110-111, on the device
+                self.actions.clamp_(-1, 1)
         else:
             self.actions[:] = actions.clamp(-1, 1) if self.cfg.clip_actions else actions
         e = self.env
@@ -419,27 +432,22 @@ class PHCPufferEnv:
         e._attach_eval()
         e.engine.imitation_reset_step(e._params, e._em, e.obs_buf, e.rew_buf, e.reward_raw, e._reset_u8, e._term_u8,
                                       seed=self.cfg.seed, step_index=self.tick)
-        e.extras["terminate"] = e._terminate_buf.clone()
+        # the step's returned copies and the episode bookkeeping (env.py:120-160) in one launch
+        rew = torch.empty_like(self.rewards)
+        term_copy = torch.empty_like(e._term_u8)
+        stream = torch.cuda.current_stream(self.actions.device).cuda_stream
+        rc = e.engine.lib.he_episode_step(
+            int(self.cfg.num_envs), self.rewards.data_ptr(), e.reward_raw.data_ptr(), e._reset_u8.data_ptr(),
+            e._term_u8.data_ptr(), rew.data_ptr(), term_copy.data_ptr(), self.terminals.data_ptr(),
+            self.truncations.data_ptr(), self.masks.data_ptr(), self.episode_returns.data_ptr(),
+            self.episode_lengths.data_ptr(), self.raw_rewards.data_ptr(), self._acc.data_ptr(), stream)
+        if rc != 0:
+            from humanoid_amd.engine import EngineError
+            raise EngineError(e.engine.lib.he_last_error().decode())
+        e.extras["terminate"] = term_copy.view(torch.bool)
         e.extras["reward_raw"] = e.reward_raw.detach()
         if self.cfg.use_amp_obs:
             e.extras["amp_obs"] = e.amp_obs
-        rew = self.rewards.clone()
-        self.raw_rewards += e.reward_raw.mean(dim=0)
-        reset = e.reset_buf
-        term = e._terminate_buf & reset
-        trunc = reset & ~term
-        self.terminals.copy_(term)
-        self.truncations.copy_(trunc)
-        torch.logical_not(trunc, out=self.masks)
-        r = reset.to(torch.float64)
-        self._acc[0] += (self.episode_returns.double() * r).sum()
-        self._acc[1] += (self.episode_lengths.double() * r).sum()
-        self._acc[2] += r.sum()
-        self._acc[3] += trunc.double().sum()
-        self._acc[4] += term.double().sum()
-        keep = ~reset
-        self.episode_returns.mul_(keep).add_(self.rewards * keep)
-        self.episode_lengths.mul_(keep).add_(keep.to(torch.int32))
         info = []
         self.tick += 1
         if self.tick % self.cfg.log_interval == 0:

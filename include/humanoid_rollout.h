@@ -94,6 +94,21 @@ int he_gae_minibatch(const float* dones, const float* values, const float* rewar
                      int32_t minibatch_rows, int32_t bptt_horizon, float* b_advantages, float* b_returns,
                      void* stream);
 
+/* PHCPufferEnv.step episode bookkeeping in one launch (clean_pufferl/env.py:120-160, replacing its
+ * nonzero / tolist / isin host round trips and the per-step torch ops of the device mirror). For
+ * env i with r = reset[i], t = terminate[i] (0/1 bytes): terminals[i] = t & r, truncations[i] =
+ * r & !t, masks[i] = !truncations[i]; rew_out[i] = rew[i] and term_out[i] = t (the step's returned
+ * copies, env.py:121); acc[0..4] += the sums over reset envs of episode_returns, episode_lengths,
+ * 1, truncation, termination (double, env.py:137-148's info lists reduced on the device); then
+ * episode_returns[i] = r ? 0 : episode_returns[i] + rew[i], episode_lengths[i] = r ? 0 :
+ * episode_lengths[i] + 1 (env.py:140-141, 159-160), and raw_rewards[k] += mean_i reward_raw[i][k]
+ * for k < 5 (env.py:124). One workgroup, fixed-order sums: the result is deterministic. Device
+ * pointers; num_envs >= 0. */
+int he_episode_step(int32_t num_envs, const float* rew, const float* reward_raw, const uint8_t* reset,
+                    const uint8_t* terminate, float* rew_out, uint8_t* term_out, uint8_t* terminals,
+                    uint8_t* truncations, uint8_t* masks, float* episode_returns, int32_t* episode_lengths,
+                    float* raw_rewards, double* acc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

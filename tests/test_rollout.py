@@ -222,3 +222,46 @@ def test_gpu_order_full_size_properties():
     e.flatten_batch()
     assert torch.equal(e.b_obs, e.obs[e.b_idxs_obs])
     assert torch.equal(e.b_values, e.values[e.b_idxs_flat])
+
+
+@pytest.mark.gpu
+def test_episode_step_kernel_edges():
+    """he_episode_step (PHCPufferEnv.step bookkeeping, clean_pufferl/env.py:120-160) against the
+    torch restatement on random flags, including the all-reset and no-reset steps."""
+    import torch
+    from humanoid_amd.engine import load_library
+    lib = load_library()
+    rng = np.random.default_rng(7)
+    n = 3000
+    dev = "cuda:0"
+    for mode in ("random", "all", "none"):
+        reset = rng.random(n) < 0.3 if mode == "random" else np.full(n, mode == "all")
+        term = reset & (rng.random(n) < 0.5)
+        rew = torch.as_tensor(rng.standard_normal(n).astype(np.float32), device=dev)
+        raw = torch.as_tensor(rng.random((n, 5)).astype(np.float32), device=dev)
+        r8 = torch.as_tensor(reset.astype(np.uint8), device=dev)
+        t8 = torch.as_tensor(term.astype(np.uint8), device=dev)
+        ret = torch.as_tensor(rng.standard_normal(n).astype(np.float32), device=dev)
+        ln = torch.as_tensor(rng.integers(0, 300, n).astype(np.int32), device=dev)
+        ret0, ln0 = ret.clone(), ln.clone()
+        raw_acc = torch.zeros(5, device=dev)
+        acc = torch.zeros(5, dtype=torch.float64, device=dev)
+        rew_out = torch.empty_like(rew)
+        t_out, terminals, truncs, masks = (torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(4))
+        rc = lib.he_episode_step(n, rew.data_ptr(), raw.data_ptr(), r8.data_ptr(), t8.data_ptr(), rew_out.data_ptr(),
+                                 t_out.data_ptr(), terminals.data_ptr(), truncs.data_ptr(), masks.data_ptr(),
+                                 ret.data_ptr(), ln.data_ptr(), raw_acc.data_ptr(), acc.data_ptr(), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        rb, tb = r8.bool(), t8.bool()
+        assert torch.equal(rew_out, rew) and torch.equal(t_out, t8)
+        assert torch.equal(terminals.bool(), tb & rb) and torch.equal(truncs.bool(), rb & ~tb)
+        assert torch.equal(masks.bool(), ~(rb & ~tb))
+        assert torch.equal(ret, torch.where(rb, torch.zeros_like(ret0), ret0 + rew))
+        assert torch.equal(ln, torch.where(rb, torch.zeros_like(ln0), ln0 + 1))
+        want = [(ret0.double() * rb).sum(), (ln0.double() * rb).sum(), rb.double().sum(),
+                (rb & ~tb).double().sum(), (tb & rb).double().sum()]
+        np.testing.assert_allclose(acc.cpu().numpy(), [float(w) for w in want], rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(raw_acc.cpu().numpy(), raw.mean(0).cpu().numpy(), rtol=1e-6)
+    assert lib.he_episode_step(0, *([None] * 13), None) == 0
+    assert lib.he_episode_step(-1, *([None] * 13), None) != 0
