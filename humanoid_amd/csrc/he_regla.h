@@ -297,6 +297,9 @@ struct ElimGroups {
 constexpr int kElimGroupMax = HE_ELIM_GMAX;
 constexpr ElimGroups<kElimGroupMax> kElimGroups{};
 
+#ifndef HE_FAC_VINV  // +0.4% (A/B r01)
+#define HE_FAC_VINV 1
+#endif
 template <int K>
 struct PivotStep {
     float dk, l, l2;  // pivot, row K of L on this lane (scaled) and its second-set entry
@@ -307,7 +310,11 @@ struct PivotStep {
 template <int K>
 __device__ __forceinline__ void grp_pivot(const RegMat& M, PivotStep<K>& st) {
     st.dk = get<K, K>(M);
+#if HE_FAC_VINV  // the reciprocal stays a (wave-uniform) VGPR: no readfirstlane on the pivot chain
+    const float inv = __builtin_amdgcn_rcpf(st.dk);
+#else
     const float inv = uniform(__builtin_amdgcn_rcpf(st.dk));
+#endif
     st.l = mc<K>(M) * inv;
     if constexpr (K >= 64) st.l2 = mc2<K >= 64 ? K - 64 : 0>(M) * inv;
 }
