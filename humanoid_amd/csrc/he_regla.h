@@ -204,8 +204,62 @@ __device__ __forceinline__ void zbs_pipe(const float* Lp, ZVec& z, uint32_t lb, 
         zbs_pipe<K - 1>(Lp, z, lb, nx);
     }
 }
+// body-level variant: one liveness branch per body (its 3 rows, or the root's 5, applied in a
+// row-prefetch chain inside it) instead of two per dof
+template <int K>
+constexpr int dof_first_of_body() { return K < 6 ? 0 : 6 + 3 * ((K - 6) / 3); }
+template <int K>
+__device__ __forceinline__ typename RowOf<K>::T row_if_live(const float* Lp, uint32_t lb) {
+    typename RowOf<K>::T r;
+    if constexpr (K >= 1) {
+        if (body_live<K>(lb)) {
+            int off = 0;
+            asm volatile("" : "+v"(off));
+            r = load_row_if<K>(Lp, off);
+        } else {
+            undef_row(r);
+        }
+    } else {
+        undef_row(r);
+    }
+    return r;
+}
+// rows K .. K0 of one live body: row K is in registers, row K-1 (same body) is requested first
+template <int K, int K0>
+__device__ __forceinline__ void zbs_in_body(const float* Lp, ZVec& z, const typename RowOf<K>::T& rk) {
+    if constexpr (K > K0 && K >= 1) {
+        int off = 0;
+        asm volatile("" : "+v"(off));
+        const typename RowOf<K - 1>::T nx = load_row_if<K - 1>(Lp, off);
+        zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z);
+        __builtin_amdgcn_sched_barrier(0);
+        zbs_in_body<K - 1, K0>(Lp, z, nx);
+    } else if constexpr (K >= 1) {
+        zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+template <int K>  // K: the last dof of a body (74, 71, ..., 8, then 5 for the root)
+__device__ __forceinline__ void zbs_bodies(const float* Lp, ZVec& z, uint32_t lb, const typename RowOf<K>::T& rk) {
+    if constexpr (K >= 1) {
+        constexpr int K0 = dof_first_of_body<K>();
+        if (body_live<K>(lb)) zbs_in_body<K, K0>(Lp, z, rk);
+        // the next body's last row (requested after this body's updates were issued)
+        const typename RowOf<K0 - 1>::T nx = row_if_live<K0 - 1>(Lp, lb);
+        __builtin_amdgcn_sched_barrier(0);
+        zbs_bodies<K0 - 1>(Lp, z, lb, nx);
+    }
+}
+#ifndef HE_ZBS_BODY
+#define HE_ZBS_BODY 1
+#endif
+
 template <int K>
 __device__ __forceinline__ void zbs(const float* Lp, ZVec& z, uint32_t lb) {
+#if HE_ZBS_BODY
+    zbs_bodies<K>(Lp, z, lb, row_if_live<K>(Lp, lb));
+    return;
+#endif
     int off = 0;
     asm volatile("" : "+v"(off));
     const auto r0 = load_row_if<K>(Lp, off);
