@@ -59,7 +59,8 @@ struct Lds {
     float S[NG][6], IS[NG][6];
     float V[NB][6], Acc[NB][6], F[NB][6];
     float Ib[NB][10], Ic[NB][10];  // m, h(3), I(xx yy zz xy xz yz)
-    alignas(16) float Lp[smpl::kNpack];  // packed unit-lower factor L (row K: ancestors in chain order)
+    alignas(16) float Lp[smpl::kNpack + 4];  // packed unit-lower factor L (row K: ancestors in chain
+                                             // order); Lp[kNpack] is the elimination's store sink
     float cx[MAXC][3], cn[MAXC][3], ct1[MAXC][3], ct2[MAXC][3], cgap[MAXC], cmu[MAXC];
     int cb0[MAXC], cb1[MAXC];
     float lam[W];

@@ -373,11 +373,31 @@ __device__ __forceinline__ void grp_pivot(const RegMat& M, PivotStep<K>& st) {
     if constexpr (K >= 64) st.l2 = mc2<K >= 64 ? K - 64 : 0>(M) * inv;
 }
 // B: packed-row store and the fused forward substitution of the right-hand side
+#ifndef HE_FAC_NOBRANCH  // sink-slot stores instead of exec-mask branches: no gain (A/B r01)
+#define HE_FAC_NOBRANCH 0
+#endif
 template <int K>
 __device__ __forceinline__ void grp_store(const PivotStep<K>& st, float* Lp, int dj, int dj2, float& yl, float& y2) {
     if constexpr (kDofNanc[K] - 1 > 0) {
         constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
         const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
+#if HE_FAC_NOBRANCH
+        // no exec-mask branch: lanes off the chain store into the sink slot Lp[kNpack], and the
+        // right-hand side update is a select
+        {
+            const bool on = lanes<lo>();
+            Lp[on ? kPackStart[K] + dj : kNpack] = st.l;
+            const float yn = yl - st.l * yk;
+            yl = on ? yn : yl;
+        }
+        if constexpr (K > 64) {
+            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+            const bool on2 = lanes<hi>();
+            Lp[on2 ? kPackStart[K] + dj2 : kNpack] = st.l2;
+            const float yn2 = y2 - st.l2 * yk;
+            y2 = on2 ? yn2 : y2;
+        }
+#else
         if (lanes<lo>()) {
             Lp[kPackStart[K] + dj] = st.l;
             yl = yl - st.l * yk;
@@ -389,6 +409,7 @@ __device__ __forceinline__ void grp_store(const PivotStep<K>& st, float* Lp, int
                 y2 = y2 - st.l2 * yk;
             }
         }
+#endif
     }
 }
 // C + D: row broadcast (in-order LDS: sees the stores of B), the ancestor updates, then row K of M
