@@ -693,12 +693,52 @@ HE_DEV void subtree_parent(float* F, float* I, int lane, int j0) {
         subtree_parent<NC, J + 1, END>(F, I, lane, j0);
     }
 }
+// one level with every parent at once: lane (group g = lane / NC, component x) takes its parent and
+// children from compile-time selects, reads them (a missing child reads the parent and adds 0:
+// the sum order of subtree_parent, bit-identical) and writes back; no exec-mask branch per parent
+template <int J, int JE>
+HE_DEV int pick_body(int g, int j0, int k) {  // k = -1: the parent, else child slot k (-1 = none)
+    if constexpr (J < JE) {
+        constexpr int p = smpl::kParentLevelBodies[J];
+        const int v = k < 0 ? p : (k == 0 ? smpl::kChildren[p][0] : (k == 1 ? smpl::kChildren[p][1] : smpl::kChildren[p][2]));
+        return g == J - j0 ? v : pick_body<J + 1, JE>(g, j0, k);
+    } else {
+        return -1;
+    }
+}
+template <int NC, int D>
+HE_DEV void subtree_level_flat(float* F, float* I, int lane) {
+    constexpr int j0 = smpl::kParentLevelStart[D], j1 = smpl::kParentLevelStart[D + 1];
+    static_assert((j1 - j0) * NC <= W, "one level's parents fit one wave");
+    const int g = lane / NC, x = lane - g * NC;
+    const int p = pick_body<j0, j1>(g, j0, -1);
+    const int c0 = pick_body<j0, j1>(g, j0, 0), c1 = pick_body<j0, j1>(g, j0, 1), c2 = pick_body<j0, j1>(g, j0, 2);
+    if (lane < (j1 - j0) * NC) {
+        float* X = x < 6 ? F : I;
+        const int st = x < 6 ? 6 : 10, xx = x < 6 ? x : x - 6;
+        float v = X[p * st + xx];
+        const float v0 = X[(c0 >= 0 ? c0 : p) * st + xx];
+        const float v1 = X[(c1 >= 0 ? c1 : p) * st + xx];
+        const float v2 = X[(c2 >= 0 ? c2 : p) * st + xx];
+        v += c0 >= 0 ? v0 : 0.f;
+        v += c1 >= 0 ? v1 : 0.f;
+        v += c2 >= 0 ? v2 : 0.f;
+        X[p * st + xx] = v;
+    }
+}
+#ifndef HE_SUBTREE_FLAT
+#define HE_SUBTREE_FLAT 1
+#endif
 template <int NC, int D>
 HE_DEV void subtree_levels(float* F, float* I, int lane) {
     if constexpr (D >= 0) {
         constexpr int j0 = smpl::kParentLevelStart[D], j1 = smpl::kParentLevelStart[D + 1];
         if constexpr (j1 > j0) {
+#if HE_SUBTREE_FLAT
+            subtree_level_flat<NC, D>(F, I, lane);
+#else
             subtree_parent<NC, j0, j1>(F, I, lane, j0);
+#endif
             sync();
         }
         subtree_levels<NC, D - 1>(F, I, lane);
