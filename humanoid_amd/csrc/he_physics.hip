@@ -1406,8 +1406,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     for (int i = lane; i < NG; i += W)
         if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
     sync();
+    // damping, the angular-velocity clamp and the semi-implicit position update in one pass per
+    // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
+    // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
     if (lane < NB) {
-        int d0 = lane == 0 ? 0 : 6 + 3 * (lane - 1);
+        const bool root = lane == 0;
+        const int d0 = root ? 0 : 6 + 3 * (lane - 1);
         float w[3] = {L.uf[d0] * damp, L.uf[d0 + 1] * damp, L.uf[d0 + 2] * damp};
         float nrm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         if (nrm > p.max_angular_velocity) {
@@ -1415,21 +1419,17 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             w[0] *= s; w[1] *= s; w[2] *= s;
         }
         L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
-        if (lane == 0) { L.u0[3] = L.uf[3]; L.u0[4] = L.uf[4]; L.u0[5] = L.uf[5]; }
-    }
-    sync();
-    // ---- semi-implicit position update
-    if (lane < NB) {
-        if (lane == 0) {
-            for (int c = 0; c < 3; ++c) L.root_pos[c] += dt * L.u0[3 + c];
-            f4 dq = pqexp(f3{dt * L.u0[0], dt * L.u0[1], dt * L.u0[2]});
-            f4 nq = qnormalize(qmul(dq, f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]}));
+        const int d = root ? 0 : 3 * (lane - 1);
+        const f3 dtw = f3{dt * w[0], dt * w[1], dt * w[2]};
+        const f4 e1 = pqexp(root ? dtw : f3{L.q[d], L.q[d + 1], L.q[d + 2]});
+        const f4 e2 = root ? f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]} : pqexp(dtw);
+        const f4 nq = qnormalize(qmul(e1, e2));
+        if (root) {
+            L.u0[3] = L.uf[3]; L.u0[4] = L.uf[4]; L.u0[5] = L.uf[5];
+            for (int c = 0; c < 3; ++c) L.root_pos[c] += dt * L.uf[3 + c];
             L.root_q[0] = nq.x; L.root_q[1] = nq.y; L.root_q[2] = nq.z; L.root_q[3] = nq.w;
         } else {
-            int d = 3 * (lane - 1), g = 6 + d;
-            f4 ql = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
-            f4 dq = pqexp(f3{dt * L.u0[g], dt * L.u0[g + 1], dt * L.u0[g + 2]});
-            f3 nv = pqlog(qnormalize(qmul(ql, dq)));
+            const f3 nv = pqlog(nq);
             L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
         }
     }
