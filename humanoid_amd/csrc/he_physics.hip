@@ -889,6 +889,30 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     sync();
 }
 
+__device__ const regla::ChainBytes kChainBytesDev{};
+#ifndef HE_LSOLVE_GATHER  // ds_bpermute gathers per level: no gain over the readlane picks (A/B r01)
+#define HE_LSOLVE_GATHER 0
+#endif
+// y <- L^-1 y for the lane's rows (see regla::solve_L_rows / solve_L_gather)
+HE_DEV void solve_L(const float (&r1)[regla::kRowRegs], const float (&r2)[regla::kRowRegs], int lane, float& yl,
+                    float& y2) {
+#if HE_LSOLVE_GATHER
+    uint32_t c1[8], c2[8];
+    const uint4* w1 = reinterpret_cast<const uint4*>(kChainBytesDev.w[lane]);
+    const uint4* w2 = reinterpret_cast<const uint4*>(kChainBytesDev.w[lane < regla::NH ? 64 + lane : 0]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint4 a = w1[q], b = w2[q];
+        c1[4 * q] = a.x; c1[4 * q + 1] = a.y; c1[4 * q + 2] = a.z; c1[4 * q + 3] = a.w;
+        c2[4 * q] = b.x; c2[4 * q + 1] = b.y; c2[4 * q + 2] = b.z; c2[4 * q + 3] = b.w;
+    }
+    regla::solve_L_gather<0>(r1, r2, c1, c2, yl, y2);
+#else
+    (void)lane;
+    regla::solve_L_rows<0>(r1, r2, yl, y2);
+#endif
+}
+
 // lane i's packed row of L (dof i) and the row of dof 64 + i (lanes >= NH read row 64 and never
 // use it: an exec-masked second load measured slower than the unmasked one, A/B r01)
 HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[regla::kRowRegs],
@@ -1065,7 +1089,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         load_rows(L, T, lane, r1, r2);
         STAMP(22);
         __builtin_amdgcn_s_setprio(HE_PRIO_SOLVE);
-        regla::solve_L_rows<0>(r1, r2, yl, y2);
+        solve_L(r1, r2, lane, yl, y2);
         __builtin_amdgcn_s_setprio(0);
         STAMP(23);
         L.uf[lane] = L.u0[lane] + yl;
@@ -1364,7 +1388,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             y2 = lane < NH ? y2 * L.sDinv[64 + lane] : 0.f;
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
             load_rows(L, T, lane, r1, r2);
-            regla::solve_L_rows<0>(r1, r2, yl, y2);
+            solve_L(r1, r2, lane, yl, y2);
             __builtin_amdgcn_s_setprio(0);
             L.uf[lane] += yl;
             if (lane < NH) L.uf[64 + lane] += y2;

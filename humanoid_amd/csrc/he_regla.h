@@ -314,6 +314,60 @@ __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const 
     }
 }
 
+// ---------------------------------------------------------------- y <- L^-1 y by gathers
+// The same level sweep with the ancestor value gathered by ds_bpermute from a per-lane chain table
+// (byte D of chain word D/4 = the dof at depth D of the lane's chain, 0xFF past its end) instead
+// of one v_readlane + v_cndmask per dof of the level: two gathers (first / second register set)
+// and one masked FMA per level; the FMA and its operands are those of solve_L_rows (bit-identical).
+struct ChainBytes {
+    uint32_t w[NG][8];
+    constexpr ChainBytes() : w() {
+        for (int i = 0; i < NG; ++i)
+            for (int d = 0; d < 32; ++d) {
+                const uint32_t v = (d < kMaxChain && kChain[i][d] >= 0) ? (uint32_t)kChain[i][d] : 0xFFu;
+                w[i][d >> 2] |= v << (8 * (d & 3));
+            }
+    }
+};
+__device__ __forceinline__ float gather_lane(float v, int src) {  // v on lane src (0..63)
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+template <int D>
+constexpr bool level_reads_hi() {  // some dof at depth D is >= 64 (its y lives in the second set)
+    bool r = false;
+    for (int i = 0; i < NG; ++i)
+        if (kDofNanc[i] - 1 > D && kChain[i][D] >= 64) r = true;
+    return r;
+}
+template <int D>
+__device__ __forceinline__ void solve_L_gather(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs],
+                                               const uint32_t (&c1)[8], const uint32_t (&c2)[8], float& yl,
+                                               float& y2) {
+    if constexpr (D < kNumLevels - 1) {
+        constexpr uint64_t ulo = level_desc_lo<D>();
+        constexpr uint64_t uhi = level_desc_hi<D>();
+        if constexpr (ulo != 0 || uhi != 0) {
+            const int s1 = (int)((c1[D >> 2] >> (8 * (D & 3))) & 0xFFu);
+            const int s2 = (int)((c2[D >> 2] >> (8 * (D & 3))) & 0xFFu);
+            float t1, t2 = 0.f;
+            if constexpr (level_reads_hi<D>()) {
+                const float a1 = gather_lane(yl, s1 & 63), b1 = gather_lane(y2, (s1 - 64) & 63);
+                t1 = s1 < 64 ? a1 : b1;
+                if constexpr (uhi != 0) {
+                    const float a2 = gather_lane(yl, s2 & 63), b2 = gather_lane(y2, (s2 - 64) & 63);
+                    t2 = s2 < 64 ? a2 : b2;
+                }
+            } else {
+                t1 = gather_lane(yl, s1 & 63);
+                if constexpr (uhi != 0) t2 = gather_lane(yl, s2 & 63);
+            }
+            if constexpr (ulo != 0) yl = lanes<ulo>() ? yl - r1[D] * t1 : yl;
+            if constexpr (uhi != 0) y2 = lanes<uhi>() ? y2 - r2[D] * t2 : y2;
+        }
+        solve_L_gather<D + 1>(r1, r2, c1, c2, yl, y2);
+    }
+}
+
 // ---------------------------------------------------------------- grouped elimination
 // Consecutive steps of kElimOrder whose dofs are mutually independent (neither is an ancestor of
 // the other: different branches) touch disjoint pivots and rows, so a group of them runs as one
