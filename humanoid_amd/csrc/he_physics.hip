@@ -55,6 +55,7 @@ struct BodyTopo {
 struct Lds {
     float q[ND], tgt[ND];
     float u0[NG], uf[NG], rhs[NG], coef[NG], Dinv[NG], sDinv[NG];
+    float yh[NG];  // D^-1/2 L^-T (dt rhs): the free motion's share of the one L^-1 sweep
     float ql[NB][4], qw[NB][4], pw[NB][3];
     float S[NG][6], IS[NG][6];
     float V[NB][6], Acc[NB][6], F[NB][6];
@@ -80,6 +81,9 @@ struct Lds {
 #endif
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
+#endif
+#ifndef HE_ONE_SWEEP
+#define HE_ONE_SWEEP 1
 #endif
 #ifndef HE_FAC_PIPE
 #define HE_FAC_PIPE 1
@@ -1056,8 +1060,15 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
+#if HE_ONE_SWEEP
+        // the free velocity is not formed here: the contact bias takes z.u0 + zh.yh, and one L^-1
+        // sweep after the solver gives uf = u0 + L^-1 D^-1/2 (yh + Zh^T lambda)
+        L.yh[lane] = yl * (1.0f / sqrtf(Dl));
+        if (lane < NH) L.yh[64 + lane] = y2 * (1.0f / sqrtf(D2));
+#else
         yl *= 1.0f / Dl;
         y2 = lane < NH ? y2 * (1.0f / D2) : 0.f;
+#endif
     }
     sync();
     STAMP(5);
@@ -1084,6 +1095,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         }
     }
     // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs): the L^-1 sweep
+#if !HE_ONE_SWEEP
     {
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
         load_rows(L, T, lane, r1, r2);
@@ -1095,6 +1107,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         L.uf[lane] = L.u0[lane] + yl;
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
     }
+#endif
     sync();
     STAMP(6);
     // ---- contacts: terrain (bodies in order, box corners deepest-first), then self pairs
@@ -1308,7 +1321,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #if HE_JT_MFMA
             zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane);
 #pragma unroll
-            for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), L.uf[i], bacc[i & 3]);  // J_r uf
+            for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), HE_ONE_SWEEP ? L.u0[i] : L.uf[i], bacc[i & 3]);  // J_r u
 #else
             {
                 // root: S = unit axes, so z = sgn0 * (rho, dd)
@@ -1343,6 +1356,17 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #pragma unroll
             for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(ZV(z, i), ZV(z, i), dacc[i & 3]);
             diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
+#if HE_ONE_SWEEP
+            {  // J_r (uf - u0) = zh_r . yh, yh_i broadcast from lane i (v_readlane: no LDS loads to
+               // hoist into registers at the phase's register peak)
+                const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
+                float yacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < NG; ++i)
+                    yacc[i & 3] = fmaf(ZV(z, i), regla::rdlane(i < 64 ? yhl : yh2, i & 63), yacc[i & 3]);
+                brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
+            }
+#endif
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
 #pragma unroll
@@ -1384,14 +1408,24 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? ZV(z, 64 + i < NG ? 64 + i : 0) * lamv : 0.f;
             float yl = reduce_scatter<64>(v64);
             float y2 = __shfl(reduce_scatter<16>(v16), 4 * (lane & 15), W);
+#if HE_ONE_SWEEP
+            yl = (yl + L.yh[lane]) * L.sDinv[lane];
+            y2 = lane < NH ? (y2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
+#else
             yl *= L.sDinv[lane];
             y2 = lane < NH ? y2 * L.sDinv[64 + lane] : 0.f;
+#endif
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
             load_rows(L, T, lane, r1, r2);
             solve_L(r1, r2, lane, yl, y2);
             __builtin_amdgcn_s_setprio(0);
+#if HE_ONE_SWEEP
+            L.uf[lane] = L.u0[lane] + yl;
+            if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
+#else
             L.uf[lane] += yl;
             if (lane < NH) L.uf[64 + lane] += y2;
+#endif
         }
         // ---- reported contact forces (net linear contact impulse per body / dt)
         float (*fc)[6] = L.Acc;  // per-contact scratch (Acc is dead in the contact phase)
@@ -1424,6 +1458,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         }
         sync();
     }
+#if HE_ONE_SWEEP
+    else {  // no contact: uf = u0 + L^-1 D^-1/2 yh
+        float yl = L.yh[lane] * L.sDinv[lane];
+        float y2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
+        float r1[regla::kRowRegs], r2[regla::kRowRegs];
+        load_rows(L, T, lane, r1, r2);
+        solve_L(r1, r2, lane, yl, y2);
+        L.uf[lane] = L.u0[lane] + yl;
+        if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
+        sync();
+    }
+#endif
     STAMP(11);
     // ---- drive force actually applied, damping, clamps, write velocities
     const float damp = 1.0f / (1.0f + dt * p.angular_damping);
