@@ -328,6 +328,36 @@ HE_DEV float reduce_scatter(float (&v)[N]) {
     }
     return v[0];
 }
+// at most 32 rows (<= 10 contacts): only the rows-0-31 x columns-0-31 tile is needed (one MFMA per
+// dof pair instead of four); rows >= 32 of acol are never read then
+HE_DEV void delassus_mfma32(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
+    f32x16 t00 = {};
+#pragma unroll
+    for (int g = 0; g < NGRP; ++g) {
+        if ((live >> g) & 1u) {
+#pragma unroll
+            for (int h = 0; h < 4; h += 2) {
+                const int k0 = 4 * g + h;
+                if (k0 < NG) {
+                    float p0 = ZV(z, k0), p1 = k0 + 1 < NG ? ZV(z, k0 + 1 < NG ? k0 + 1 : 0) : 0.f;
+                    swap32(p0, p1);
+                    t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(p0, p0, t00, 0, 0, 0);
+                }
+            }
+        }
+    }
+    const f32x16 zero = {};
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int r = (v & 3) + 8 * (v >> 2);
+        float a = t00[v], b = zero[v];
+        swap32(a, b);  // a: A[r][lane], b: A[r + 4][lane] (lanes >= 32: zero)
+        acol[r] = a;
+        acol[r + 4] = b;
+        if (32 + r < MAXR) acol[32 + r < MAXR ? 32 + r : 0] = 0.f;
+        if (36 + r < MAXR) acol[36 + r < MAXR ? 36 + r : 0] = 0.f;
+    }
+}
 HE_DEV void delassus_mfma(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
     f32x16 t00 = {}, t01 = {}, t10 = {}, t11 = {};
 #pragma unroll
@@ -1374,7 +1404,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 if (lb & kGroupBodies[g]) live |= 1u << g;
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
-            delassus_mfma(z, acol, live);
+            if (nr <= 32) delassus_mfma32(z, acol, live);  // wave-uniform
+            else delassus_mfma(z, acol, live);
         }
         STAMP(9);
         // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
