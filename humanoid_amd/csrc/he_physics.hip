@@ -496,7 +496,7 @@ constexpr uint32_t block_bodies(int D) {
 }
 template <int D>
 HE_DEV void zrows_block(regla::ZVec& z, uint32_t lb, const float (&b0)[3], const float (&b1)[3], const Lds& L, int l31,
-                        int kh) {
+                        int kh, bool rows32) {
     if constexpr (32 * D < NG) {
         if (lb & block_bodies(D)) {
             float aS[3];
@@ -505,9 +505,10 @@ HE_DEV void zrows_block(regla::ZVec& z, uint32_t lb, const float (&b0)[3], const
             for (int st = 0; st < 3; ++st) aS[st] = j < NG ? L.S[j < NG ? j : 0][2 * st + kh] : 0.f;
             f32x16 t0 = {}, t1 = {};
 #pragma unroll
-            for (int st = 0; st < 3; ++st) {
-                t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aS[st], b0[st], t0, 0, 0, 0);
-                t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(aS[st], b1[st], t1, 0, 0, 0);
+            for (int st = 0; st < 3; ++st) t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aS[st], b0[st], t0, 0, 0, 0);
+            if (!rows32) {  // rows 32-63 exist (wave-uniform)
+#pragma unroll
+                for (int st = 0; st < 3; ++st) t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(aS[st], b1[st], t1, 0, 0, 0);
             }
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -521,11 +522,11 @@ HE_DEV void zrows_block(regla::ZVec& z, uint32_t lb, const float (&b0)[3], const
 #pragma unroll
             for (int i = 32 * D; i < 32 * D + 32 && i < NG; ++i) ZV(z, i) = 0.f;
         }
-        zrows_block<D + 1>(z, lb, b0, b1, L, l31, kh);
+        zrows_block<D + 1>(z, lb, b0, b1, L, l31, kh, rows32);
     }
 }
 HE_DEV void zrows_mfma(regla::ZVec& z, uint32_t lb, uint32_t anc0, uint32_t anc1, f3 rho, f3 dd, const Lds& L,
-                       int lane) {
+                       int lane, bool rows32) {
     const int l31 = lane & 31, kh = lane >> 5;
     float b0[3], b1[3];
     {
@@ -538,7 +539,7 @@ HE_DEV void zrows_mfma(regla::ZVec& z, uint32_t lb, uint32_t anc0, uint32_t anc1
             b1[st] = y;
         }
     }
-    zrows_block<0>(z, lb, b0, b1, L, l31, kh);
+    zrows_block<0>(z, lb, b0, b1, L, l31, kh, rows32);
     float sg[NB];
 #pragma unroll
     for (int B = 0; B < NB; ++B) sg[B] = (float)((anc0 >> B) & 1u) - (float)((anc1 >> B) & 1u);
@@ -1349,7 +1350,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             // results are fixed in place so the loads cannot all be hoisted ahead of the math)
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
 #if HE_JT_MFMA
-            zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane);
+            zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane, nr <= 32);
 #pragma unroll
             for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), HE_ONE_SWEEP ? L.u0[i] : L.uf[i], bacc[i & 3]);  // J_r u
 #else
