@@ -1,0 +1,89 @@
+"""Full-size (BASELINE configs[1]/[2]: 4096 envs) checks of the bench workload on the GPU, through
+size-independent properties: determinism (the launch is bit-reproducible), finiteness, the
+stand-still invariant of configs[1], and oracle parity on a random sample of envs taken from the
+full-size run (one policy step from the GPU's own state, fp64 C oracle, the physics tolerances of
+test_gpu_parity)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _rollout(config, model):
+    import bench
+    if not torch.cuda.is_available():
+        pytest.skip("needs the GPU")
+    args = argparse.Namespace(config=config, num_envs=4096, clips=128, seed=0, max_contacts=20)
+    return bench.Rollout(args, model, 0, 0)
+
+
+def _state(ro):
+    return (ro.eng.root_states.clone(), ro.eng.dof_state.clone(), ro.obs.clone(), ro.rew.clone())
+
+
+@pytest.mark.parametrize("config", ["standstill", "imitation"])
+def test_full_size_deterministic_and_finite(model, config):
+    a, b = _rollout(config, model), _rollout(config, model)
+    for _ in range(10):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    for x, y in zip(_state(a), _state(b)):
+        assert torch.isfinite(x).all()
+        assert torch.equal(x, y), "the step must be bit-reproducible"
+
+
+def test_full_size_standstill_invariant(model):
+    ro = _rollout("standstill", model)
+    z0 = ro.eng.root_states[:, 2].clone()
+    for _ in range(30):
+        ro.step()
+        # PD stand-still on the zero pose: nobody falls (resets happen only when the clip's time
+        # runs out, which restarts the env at the same stand-still reference)
+        assert (ro.term == 0).all()
+    torch.cuda.synchronize()
+    z = ro.eng.root_states[:, 2]
+    assert (z - z0).abs().max().item() < 0.05
+    assert (ro.eng.num_contacts == 16).all()  # 4 foot/toe boxes x 4 corners
+
+
+@pytest.mark.parametrize("config", ["standstill", "imitation"])
+def test_full_size_sample_matches_oracle(model, he_model, config):
+    import cases  # noqa: F401  (tests/ on the path)
+    from humanoid_amd import _abi
+    ro = _rollout(config, model)
+    for _ in range(5):
+        ro.step()
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(4096, 48, replace=False))
+    root = ro.eng.root_states.cpu().numpy()[idx].copy()
+    dof = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy()
+    ro.eng.step_actions(ro.actions, 2)
+    torch.cuda.synchronize()
+    tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
+    from test_gpu_parity import _cond_close
+    sp = _abi.default_sim_params(max_contacts=20)
+    probes = []
+    for seed in (123, 124, 125):  # the oracle's own sensitivity (see _cond_close)
+        r_s, d_s = root.copy(), dof.copy()
+        d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
+        O.physics_step(he_model, sp, r_s, d_s, tgt, 2)
+        probes.append((r_s, d_s))
+    out = O.physics_step(he_model, sp, root, dof, tgt, 2)
+    same = ro.eng.num_contacts.cpu().numpy()[idx] == out["num_contacts"]
+    assert same.mean() >= 0.9
+    rg = ro.eng.root_states.cpu().numpy()[idx]
+    dg = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx]
+    _cond_close("root pos", rg[same, :3], root[same, :3], [r[same, :3] for r, _ in probes], 1e-4)
+    _cond_close("dof pos", dg[same, :, 0], dof[same, :, 0], [d[same, :, 0] for _, d in probes], 1e-4)
+    _cond_close("dof vel", dg[same, :, 1], dof[same, :, 1], [d[same, :, 1] for _, d in probes], 1e-2, 1e-3)
