@@ -82,6 +82,9 @@ struct Lds {
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
 #endif
+#ifndef HE_DELASSUS48
+#define HE_DELASSUS48 1
+#endif
 #ifndef HE_ONE_SWEEP
 #define HE_ONE_SWEEP 1
 #endif
@@ -357,6 +360,49 @@ HE_DEV void delassus_mfma32(const regla::ZVec& z, float (&acol)[MAXR], uint32_t 
         if (32 + r < MAXR) acol[32 + r < MAXR ? 32 + r : 0] = 0.f;
         if (36 + r < MAXR) acol[36 + r < MAXR ? 36 + r : 0] = 0.f;
     }
+}
+// 33-48 rows (11-16 contacts): 16x16x4 tiles over three row blocks instead of four 32x32 tiles
+// (9 x 32 cycles per four dofs instead of 8 x 64). Operands: a 4x4 transpose of (register,
+// 16-lane group) by two permlane32 and two permlane16 swaps turns z[k0..k0+3] into the A/B
+// operand of each row block; results: the same transpose moves each tile's 4 row quads into the
+// column's lane group (lane c holds A[r][c]).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+HE_DEV void xpose4(float (&r)[4]) {  // r[i] <- (group g: r[g] of group i)
+    swap32(r[0], r[2]);
+    swap32(r[1], r[3]);
+    swap16(r[0], r[1]);
+    swap16(r[2], r[3]);
+}
+HE_DEV void delassus_mfma48(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
+    f32x4 c[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < NGRP; ++g) {
+        if ((live >> g) & 1u) {
+            float r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = 4 * g + k < NG ? ZV(z, 4 * g + k < NG ? 4 * g + k : 0) : 0.f;
+            xpose4(r);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(r[i], r[j], c[i][j], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            float x[4] = {c[i][0][v], c[i][1][v], c[i][2][v], 0.f};
+            xpose4(x);  // x[g] on lane c: A[16 i + 4 g + v][c]
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acol[16 * i + 4 * g + v] = x[g];
+        }
+#pragma unroll
+    for (int r = 48; r < MAXR; ++r) acol[r] = 0.f;
 }
 HE_DEV void delassus_mfma(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
     f32x16 t00 = {}, t01 = {}, t10 = {}, t11 = {};
@@ -1406,6 +1452,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
             if (nr <= 32) delassus_mfma32(z, acol, live);  // wave-uniform
+#if HE_DELASSUS48
+            else if (nr <= 48) delassus_mfma48(z, acol, live);
+#endif
             else delassus_mfma(z, acol, live);
         }
         STAMP(9);
