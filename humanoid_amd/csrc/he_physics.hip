@@ -684,16 +684,31 @@ HE_DEV void crba_tile_rows(regla::RegMat& M, const f32x16& ta, const f32x16& tb)
         if (r + 4 < NG) M.cp[(r + 4 < NG ? r + 4 : 0) >> 1][(r + 4) & 1] = b;
     }
 }
+// HE_CRBA_NOMASK: entries off the ancestor chains are left as the dense product. The elimination
+// reads only chain entries (an update of row I on lane j uses row K on lane j, and j in chain(I),
+// I in chain(K) gives j in chain(K)), stores only chain lanes, and the pivots are diagonal, so
+// those entries never reach L, D or the right-hand side; only the diagonal addends remain.
+#ifndef HE_CRBA_NOMASK
+#define HE_CRBA_NOMASK 1
+#endif
 template <int I>
 HE_DEV void crba_mask_rows(regla::RegMat& M, float dadd, float dadd2) {
     using namespace regla;
     if constexpr (I < NG) {
+#if HE_CRBA_NOMASK
+        float h = mc<I>(M);
+#else
         float h = lanes<smpl::kAncLo[I]>() ? mc<I>(M) : 0.f;
+#endif
         if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
         asm volatile("" : "+v"(h));
         mc_set<I>(M, h);
         if constexpr (I >= 64) {
+#if HE_CRBA_NOMASK
+            float h2 = mc2<I - 64>(M);
+#else
             float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? mc2<I - 64>(M) : 0.f;
+#endif
             h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
             asm volatile("" : "+v"(h2));
             mc2_set<I - 64>(M, h2);
