@@ -82,6 +82,9 @@ struct Lds {
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
 #endif
+#ifndef HE_BIAS_FROM_V  // +0.5%, but its different rounding pushes one chaotic sampled env past the
+#define HE_BIAS_FROM_V 0  // full-size parity tolerance (r01): off
+#endif
 #ifndef HE_DELASSUS48
 #define HE_DELASSUS48 1
 #endif
@@ -1412,8 +1415,23 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
 #if HE_JT_MFMA
             zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane, nr <= 32);
+#if HE_ONE_SWEEP && HE_BIAS_FROM_V
+            {
+                // J_r u0 = (rho, dd) . (V_b0 - V_b1): the contact bodies' spatial velocities about o
+                // from the kinematics (V_b = sum over the chain of S_i u0_i), not a 75-dof dot product
+                const int b0i = lane < nr ? L.cb0[ci] : 0, b1i = lane < nr ? L.cb1[ci] : -1;
+                const float* V0 = L.V[b0i];
+                const float* V1 = L.V[b1i >= 0 ? b1i : 0];
+                const float s1 = b1i >= 0 ? 1.f : 0.f;
+                const float u6[6] = {rho.x, rho.y, rho.z, dd.x, dd.y, dd.z};
+#pragma unroll
+                for (int x = 0; x < 6; ++x) bacc[x & 3] = fmaf(u6[x], V0[x] - s1 * V1[x], bacc[x & 3]);
+                if (lane >= nr) bacc[0] = bacc[1] = bacc[2] = bacc[3] = 0.f;
+            }
+#else
 #pragma unroll
             for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), HE_ONE_SWEEP ? L.u0[i] : L.uf[i], bacc[i & 3]);  // J_r u
+#endif
 #else
             {
                 // root: S = unit axes, so z = sgn0 * (rho, dd)
