@@ -1029,7 +1029,7 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // ---------------------------------------------------------------------------------- one substep
 HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
-                    unsigned long long& t_prev) {
+                    unsigned long long& t_prev, bool last) {
     using namespace regla;
     // the launch arguments through an opaque offset too: their fields are re-read (scalar loads
     // from the kernarg segment) where used instead of being held in SGPRs across the substep loop
@@ -1541,8 +1541,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             if (lane < NH) L.uf[64 + lane] += y2;
 #endif
         }
-        // ---- reported contact forces (net linear contact impulse per body / dt)
+        // ---- reported contact forces (net linear contact impulse per body / dt): the output is the
+        // last substep's, so the earlier substeps skip them (their cf rows stay zero, as set above)
         float (*fc)[6] = L.Acc;  // per-contact scratch (Acc is dead in the contact phase)
+        if (last) {
         if (lane < nc) {
             const int c = lane;
             const float ln = L.lam[3 * c], la = L.lam[3 * c + 1], lb = L.lam[3 * c + 2];
@@ -1571,6 +1573,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             L.cf[lane][0] = F3[0] / dt; L.cf[lane][1] = F3[1] / dt; L.cf[lane][2] = F3[2] / dt;
         }
         sync();
+        }  // last
     }
 #if HE_ONE_SWEEP
     else {  // no contact: uf = u0 + L^-1 D^-1/2 yh
@@ -1666,7 +1669,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;
     unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * HE_STAMP_SLOTS : nullptr;
     unsigned long long t_prev = __builtin_readcyclecounter();
-    for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev);
+    for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev, s == a.substeps - 1);
     // ---- outputs: generalized state, FK rigid-body state, forces
     kinematics<false>(L, m, lane, a.p);
     STAMP(13);
