@@ -1508,8 +1508,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             }
             __builtin_amdgcn_s_setprio(0);
         }
-        L.lam[lane] = lane < nr ? lamv : 0.f;
-        sync();
+        if (last) {  // read only by the reported contact forces
+            L.lam[lane] = lane < nr ? lamv : 0.f;
+            sync();
+        }
         STAMP(10);
         // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
         // a wave reduce-scatter sums the 75 columns into lane = dof, then one L^-1 sweep
@@ -1590,9 +1592,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     STAMP(11);
     // ---- drive force actually applied, damping, clamps, write velocities
     const float damp = 1.0f / (1.0f + dt * p.angular_damping);
-    for (int i = lane; i < NG; i += W)
-        if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
-    sync();
+    if (last) {  // the reported drive force is the last substep's
+        for (int i = lane; i < NG; i += W)
+            if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
+        sync();
+    }
     // damping, the angular-velocity clamp and the semi-implicit position update in one pass per
     // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
     // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
