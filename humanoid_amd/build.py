@@ -7,6 +7,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhumanoid_engine.so")
+# diagnostic twin with the physics kernel's per-phase cycle stamps compiled in (tools/phase_profile.py);
+# the product library leaves them out (their per-phase branches cost ~1% of the step)
+PHASES_LIB = os.path.join(HERE, "libhumanoid_engine_phases.so")
+PHASES_DEFS = {"he_physics.hip": ["-DHE_PHASE_STAMPS=1"]}
 BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("HE_OFFLOAD_ARCH", "gfx950")
 
@@ -38,34 +42,43 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
+def _compile(hipcc, cmd, src, o, force, hdr_time, verbose):
+    stamp = o + ".cmd"  # a flag change rebuilds too
+    same_cmd = os.path.exists(stamp) and open(stamp).read() == " ".join(cmd)
+    if force or not same_cmd or _mtime(o) < max(_mtime(src), hdr_time):
+        if verbose:
+            print(" ".join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr}")
+        with open(stamp, "w") as f:
+            f.write(" ".join(cmd))
+        return True
+    return False
+
+
+def _link(hipcc, lib, objs, force):
+    if force or _mtime(lib) < max(_mtime(o) for o in objs):
+        cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+
+
 def build(force=False, verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     hipcc = _hipcc()
     common = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
     hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
-    objs = []
-    rebuilt = False
-    for src, flags in SOURCES:
-        s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + ".o")
-        objs.append(o)
-        cmd = [hipcc] + common + flags + ["-c", s, "-o", o]
-        stamp = o + ".cmd"  # a flag change rebuilds too
-        same_cmd = os.path.exists(stamp) and open(stamp).read() == " ".join(cmd)
-        if force or not same_cmd or _mtime(o) < max(_mtime(s), hdr_time):
-            if verbose:
-                print(" ".join(cmd))
-            r = subprocess.run(cmd, capture_output=True, text=True)
-            if r.returncode != 0:
-                raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
-            with open(stamp, "w") as f:
-                f.write(" ".join(cmd))
-            rebuilt = True
-    if force or rebuilt or _mtime(LIB) < max(_mtime(o) for o in objs):
-        cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"link failed:\n{r.stderr}")
+    for lib, defs, suffix in ((LIB, {}, ".o"), (PHASES_LIB, PHASES_DEFS, ".phases.o")):
+        objs = []
+        for src, flags in SOURCES:
+            s = os.path.join(CSRC, src)
+            o = os.path.join(BUILD, src + (suffix if src in defs else ".o"))
+            objs.append(o)
+            cmd = [hipcc] + common + flags + defs.get(src, []) + ["-c", s, "-o", o]
+            _compile(hipcc, cmd, s, o, force and lib == LIB or force and src in defs, hdr_time, verbose)
+        _link(hipcc, lib, objs, force)
     return LIB
 
 

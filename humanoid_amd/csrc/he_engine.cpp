@@ -598,6 +598,9 @@ int he_motion_state(he_engine* h, int k, const int64_t* ids, const float* times,
 
 int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer) {
     if (!h) return fail("he_set_debug_stamps: null handle");
+    if (device_buffer && !physics_phase_stamps())
+        return fail("he_set_debug_stamps: this library is built without phase stamps "
+                    "(load libhumanoid_engine_phases.so, e.g. HE_ENGINE_LIB=humanoid_amd/libhumanoid_engine_phases.so)");
     h->stamps = reinterpret_cast<unsigned long long*>(device_buffer);
     return 0;
 }

@@ -106,6 +106,7 @@ hipError_t launch_amp(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_amp_function(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream);
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);
+bool physics_phase_stamps();  // built with HE_PHASE_STAMPS (diagnostic twin library)
 hipError_t launch_ingest(const float* pose, const float* trans, const int32_t* parents, const float* local_pos,
                          const int64_t* starts, const int64_t* nframes, const float* dt, int num_clips, int64_t F,
                          float* hot, float* cold, float* gav_raw, hipStream_t stream);

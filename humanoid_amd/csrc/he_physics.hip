@@ -118,6 +118,14 @@ HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
 
 // optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
 // s_memtime deltas per phase into stamps[block * HE_STAMP_SLOTS + phase]
+#ifndef HE_PHASE_STAMPS
+#define HE_PHASE_STAMPS 0  // diagnostic twin library only (build.py PHASES_LIB)
+#endif
+#if !HE_PHASE_STAMPS
+#define STAMP(id) \
+    do {          \
+    } while (0)
+#else
 #define STAMP(id)                                                             \
     do {                                                                      \
         if (stamps && lane == 0) {                                            \
@@ -126,6 +134,7 @@ HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
             t_prev = _t;                                                      \
         }                                                                     \
     } while (0)
+#endif
 
 // spatial inertia (m, h, I6) applied to V=(w, v): n = I w + h x v ; f = m v - h x w
 HE_DEV void si_apply(const float* I, const float* V, float* F) {
@@ -1705,6 +1714,8 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
 }  // namespace
 
 size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16; }
+
+bool physics_phase_stamps() { return HE_PHASE_STAMPS != 0; }
 
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream) {
     if (a.num_envs <= 0) return hipSuccess;

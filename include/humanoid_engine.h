@@ -284,7 +284,9 @@ int he_amp_observations(int k, const float* root_pos, const float* root_rot, con
                         const float* key_body_pos, float* out, void* stream);
 
 /* Diagnostics: when non-NULL, the physics kernel accumulates per-phase shader cycles into
- * device_buffer [N][HE_STAMP_SLOTS] (u64; phases listed in DESIGN.md §4). NULL disables (default). */
+ * device_buffer [N][HE_STAMP_SLOTS] (u64; phases listed in DESIGN.md §4). NULL disables (default).
+ * Only the diagnostic twin library (libhumanoid_engine_phases.so) carries the stamps; the product
+ * library returns nonzero for a non-NULL buffer. */
 int he_set_debug_stamps(he_engine* h, uint64_t* device_buffer);
 
 /* hash-based uniform used by he_env_step (exposed for parity tests): out[k] for env ids[k]. */

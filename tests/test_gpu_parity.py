@@ -78,6 +78,20 @@ def test_zero_copy_buffers(he_model):
         eng.set_root_state_indexed(src[:, :12], ids)
 
 
+def test_product_library_has_no_phase_stamps(he_model):
+    """The per-phase cycle stamps live only in the diagnostic twin (libhumanoid_engine_phases.so);
+    the product library refuses a stamp buffer instead of silently leaving it zero."""
+    import os
+    from humanoid_amd.engine import EngineError
+    if os.environ.get("HE_ENGINE_LIB"):
+        pytest.skip("a variant library is loaded")
+    eng = make_engine(he_model, 8)
+    buf = torch.zeros(8, 32, dtype=torch.int64, device="cuda:0")
+    with pytest.raises(EngineError, match="phase stamps"):
+        eng.set_debug_stamps(buf)
+    eng.set_debug_stamps(None)
+
+
 def test_motion_state_matches_golden(he_model, golden):
     g = golden("motion_lib")
     eng = make_engine(he_model, 4)

@@ -1,4 +1,5 @@
-"""Per-phase cycle breakdown of the physics kernel (diagnostic build path: he_set_debug_stamps).
+"""Per-phase cycle breakdown of the physics kernel (diagnostic twin library
+libhumanoid_engine_phases.so, he_set_debug_stamps).
 
 Runs the bench workload (default configs[1], 4096 envs) for a few steps with stamps enabled and
 prints mean shader cycles per env per policy step for each phase.
@@ -11,6 +12,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# the product library leaves the stamps out; this loads the diagnostic twin (humanoid_amd/build.py)
+os.environ.setdefault("HE_ENGINE_LIB", os.path.join(ROOT, "humanoid_amd", "libhumanoid_engine_phases.so"))
 
 PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba", "ltdl factor", "free solve",
           "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write",
