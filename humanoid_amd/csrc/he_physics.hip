@@ -855,16 +855,22 @@ HE_DEV void subtree_levels(float* F, float* I, int lane) {
 
 // ---------------------------------------------------------------------------------- kinematics
 // 2^k-th ancestor of every body (-1: none), for pointer jumping over the body tree
+#ifndef HE_KIN_ROOTREL  // chains relative to the root: three jumping rounds, root frame applied last
+#define HE_KIN_ROOTREL 1
+#endif
 struct JumpTable {
     int j[4][NB];
     constexpr JumpTable() : j() {
-        for (int b = 0; b < NB; ++b) j[0][b] = smpl::kParentBody[b];
+        for (int b = 0; b < NB; ++b)
+            j[0][b] = HE_KIN_ROOTREL && smpl::kParentBody[b] == 0 ? -1 : smpl::kParentBody[b];
         for (int k = 1; k < 4; ++k)
             for (int b = 0; b < NB; ++b) j[k][b] = j[k - 1][b] < 0 ? -1 : j[k - 1][j[k - 1][b]];
     }
 };
 constexpr JumpTable kJumpT{};
 static_assert(smpl::kNumBodyLevels <= 16, "four pointer-jumping rounds cover chains of 16 bodies");
+static_assert(!HE_KIN_ROOTREL || smpl::kNumBodyLevels - 1 <= 8, "three rounds cover the root's subtrees of depth 8");
+constexpr int kKinRounds = HE_KIN_ROOTREL ? 3 : 4;
 
 struct Jump4 {  // the four jump targets of each body packed as bytes (LDS table BodyTopo::jump4)
     uint32_t v[NB];
@@ -882,6 +888,9 @@ HE_DEV int jump_of(uint32_t jp) {  // byte K of the lane's packed entry, sign-ex
 // World poses and spatial velocities, lane = body, by pointer jumping: X_b <- X_{J_k(b)} o X_b and
 // V_b <- V_b + V_{J_k(b)} with J_k the 2^k-th ancestor, four rounds for chains of up to 16 bodies
 // (log depth instead of a chain walk per body). X = (q, p): (qa, pa) o (qb, pb) = (qa qb, pa + Ra pb).
+// HE_KIN_ROOTREL: the table stops below the root, so three rounds compose each chain in the root's
+// frame (SMPL subtrees are 8 deep) and the root's pose / velocity / base acceleration, uniform LDS
+// reads, are applied once at the end -- one dependent ds_bpermute round fewer per prefix.
 // Joint axes S (lane = dof) follow from the world poses.
 template <bool ACC>
 HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params& sp) {
@@ -893,8 +902,10 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     f4 q;
     f3 p;
     float u[3];
+    // the root's pose, read by every lane (uniform LDS addresses: broadcast)
+    const f4 qr = qnormalize(f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]});
     if (b == 0) {
-        q = qnormalize(f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]});
+        q = qr;
         p = o;
         u[0] = L.u0[0]; u[1] = L.u0[1]; u[2] = L.u0[2];
     } else {
@@ -917,7 +928,11 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     jump(std::integral_constant<int, 0>{});
     jump(std::integral_constant<int, 1>{});
     jump(std::integral_constant<int, 2>{});
-    jump(std::integral_constant<int, 3>{});
+    if constexpr (kKinRounds == 4) jump(std::integral_constant<int, 3>{});
+    if (HE_KIN_ROOTREL && b != 0) {  // root-frame pose of the chain -> world
+        p = o + qapply(qr, p);
+        q = qmul(qr, q);
+    }
     // own joint's velocity contribution: root (w0, v0 at o); joint b: (w, (p_b - o) x w), w = R_b u_b
     float V[6];
     if (b == 0) {
@@ -944,7 +959,11 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     vjump(std::integral_constant<int, 0>{});
     vjump(std::integral_constant<int, 1>{});
     vjump(std::integral_constant<int, 2>{});
-    vjump(std::integral_constant<int, 3>{});
+    if constexpr (kKinRounds == 4) vjump(std::integral_constant<int, 3>{});
+    if (HE_KIN_ROOTREL && b != 0) {  // plus the root's own velocity
+#pragma unroll
+        for (int x = 0; x < 6; ++x) V[x] += L.u0[x];
+    }
     if (act) {
         L.qw[b][0] = q.x; L.qw[b][1] = q.y; L.qw[b][2] = q.z; L.qw[b][3] = q.w;
         L.pw[b][0] = p.x; L.pw[b][1] = p.y; L.pw[b][2] = p.z;
@@ -955,10 +974,11 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         // joints j of V_j x (S_j u_j), the same prefix over the tree by pointer jumping. The base:
         // (0, v0 x w0 - g) for the free root (u = [w0, v0 at o]).
         float A[6];
+        const f3 vxw = cross3(f3{L.u0[3], L.u0[4], L.u0[5]}, f3{L.u0[0], L.u0[1], L.u0[2]});
+        const float A0[6] = {0.f, 0.f, 0.f, vxw.x - sp.gravity[0], vxw.y - sp.gravity[1], vxw.z - sp.gravity[2]};
         if (b == 0) {
-            const f3 vxw = cross3(f3{L.u0[3], L.u0[4], L.u0[5]}, f3{L.u0[0], L.u0[1], L.u0[2]});
-            A[0] = 0.f; A[1] = 0.f; A[2] = 0.f;
-            A[3] = vxw.x - sp.gravity[0]; A[4] = vxw.y - sp.gravity[1]; A[5] = vxw.z - sp.gravity[2];
+#pragma unroll
+            for (int x = 0; x < 6; ++x) A[x] = A0[x];
         } else {
             crm(V, vj, A);
         }
@@ -976,7 +996,11 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         ajump(std::integral_constant<int, 0>{});
         ajump(std::integral_constant<int, 1>{});
         ajump(std::integral_constant<int, 2>{});
-        ajump(std::integral_constant<int, 3>{});
+        if constexpr (kKinRounds == 4) ajump(std::integral_constant<int, 3>{});
+        if (HE_KIN_ROOTREL && b != 0) {  // plus the base acceleration
+#pragma unroll
+            for (int x = 0; x < 6; ++x) A[x] += A0[x];
+        }
         if (act)
             for (int x = 0; x < 6; ++x) L.Acc[b][x] = A[x];
     }
