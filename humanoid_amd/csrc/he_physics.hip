@@ -68,6 +68,7 @@ struct Lds {
     float cf[NB][3];
     float dforce[ND];
     float root_pos[3], root_q[4];
+    float qloc[NB][4];  // each joint's local rotation exp(q_b), from the kinematics (reused by integrate)
     int nc, nterr;                 // contacts, of which terrain (slots [0, nterr), grouped by body)
     int8_t tbase[NB], tcnt[NB];    // body b's terrain contacts: slots tbase[b] .. + tcnt[b]
     float4 bsph[NB];               // per-body bounding sphere of the collision segment (cull)
@@ -911,6 +912,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     } else {
         const int d = 3 * (b - 1);
         q = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
+        L.qloc[b][0] = q.x; L.qloc[b][1] = q.y; L.qloc[b][2] = q.z; L.qloc[b][3] = q.w;
         p = f3{T.local_pos[b][0], T.local_pos[b][1], T.local_pos[b][2]};
         u[0] = L.u0[6 + d]; u[1] = L.u0[7 + d]; u[2] = L.u0[8 + d];
     }
@@ -1645,8 +1647,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
         const int d = root ? 0 : 3 * (lane - 1);
         const f3 dtw = f3{dt * w[0], dt * w[1], dt * w[2]};
-        const f4 e1 = pqexp(root ? dtw : f3{L.q[d], L.q[d + 1], L.q[d + 2]});
-        const f4 e2 = root ? f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]} : pqexp(dtw);
+        const f4 ed = pqexp(dtw);  // exp(q_b) itself: the kinematics' qloc (L.q is unchanged since)
+        const f4 e1 = root ? ed : f4{L.qloc[lane][0], L.qloc[lane][1], L.qloc[lane][2], L.qloc[lane][3]};
+        const f4 e2 = root ? f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]} : ed;
         const f4 nq = qnormalize(qmul(e1, e2));
         if (root) {
             L.u0[3] = L.uf[3]; L.u0[4] = L.uf[4]; L.u0[5] = L.uf[5];
@@ -1737,6 +1740,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
 
 }  // namespace
 
+static_assert(sizeof(Lds) <= 20480, "two workgroups per SIMD (8 per CU) need <= 20 KB of LDS each");
 size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16; }
 
 bool physics_phase_stamps() { return HE_PHASE_STAMPS != 0; }
