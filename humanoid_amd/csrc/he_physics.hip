@@ -856,6 +856,9 @@ HE_DEV void subtree_levels(float* F, float* I, int lane) {
 
 // ---------------------------------------------------------------------------------- kinematics
 // 2^k-th ancestor of every body (-1: none), for pointer jumping over the body tree
+#ifndef HE_KIN_QCACHE  // later substeps start from the integrated local rotations instead of exp(log(.))
+#define HE_KIN_QCACHE 1
+#endif
 #ifndef HE_KIN_ROOTREL  // chains relative to the root: three jumping rounds, root frame applied last
 #define HE_KIN_ROOTREL 1
 #endif
@@ -894,7 +897,7 @@ HE_DEV int jump_of(uint32_t jp) {  // byte K of the lane's packed entry, sign-ex
 // reads, are applied once at the end -- one dependent ds_bpermute round fewer per prefix.
 // Joint axes S (lane = dof) follow from the world poses.
 template <bool ACC>
-HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params& sp) {
+HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params& sp, bool cached) {
     const BodyTopo& T = L.T;
     const bool act = lane < NB;
     const int b = act ? lane : 0;
@@ -911,8 +914,12 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         u[0] = L.u0[0]; u[1] = L.u0[1]; u[2] = L.u0[2];
     } else {
         const int d = 3 * (b - 1);
-        q = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
-        L.qloc[b][0] = q.x; L.qloc[b][1] = q.y; L.qloc[b][2] = q.z; L.qloc[b][3] = q.w;
+        if (HE_KIN_QCACHE && cached) {  // the previous substep's integrated rotation (pre-log)
+            q = f4{L.qloc[b][0], L.qloc[b][1], L.qloc[b][2], L.qloc[b][3]};
+        } else {
+            q = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
+            L.qloc[b][0] = q.x; L.qloc[b][1] = q.y; L.qloc[b][2] = q.z; L.qloc[b][3] = q.w;
+        }
         p = f3{T.local_pos[b][0], T.local_pos[b][1], T.local_pos[b][2]};
         u[0] = L.u0[6 + d]; u[1] = L.u0[7 + d]; u[2] = L.u0[8 + d];
     }
@@ -1064,7 +1071,7 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // ---------------------------------------------------------------------------------- one substep
 HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
-                    unsigned long long& t_prev, bool last) {
+                    unsigned long long& t_prev, bool first, bool last) {
     using namespace regla;
     // the launch arguments through an opaque offset too: their fields are re-read (scalar loads
     // from the kernarg segment) where used instead of being held in SGPRs across the substep loop
@@ -1090,7 +1097,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     const he_sim_params& p = a.p;
     const float dt = p.dt;
     __builtin_amdgcn_s_setprio(HE_PRIO_KIN);
-    kinematics<true>(L, m, lane, a.p);
+    kinematics<true>(L, m, lane, a.p, !first);
     __builtin_amdgcn_s_setprio(0);
     STAMP(0);
     const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
@@ -1658,6 +1665,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         } else {
             const f3 nv = pqlog(nq);
             L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
+            if (HE_KIN_QCACHE) {
+                L.qloc[lane][0] = nq.x; L.qloc[lane][1] = nq.y; L.qloc[lane][2] = nq.z; L.qloc[lane][3] = nq.w;
+            }
         }
     }
     sync();
@@ -1709,9 +1719,9 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;
     unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * HE_STAMP_SLOTS : nullptr;
     unsigned long long t_prev = __builtin_readcyclecounter();
-    for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev, s == a.substeps - 1);
+    for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev, s == 0, s == a.substeps - 1);
     // ---- outputs: generalized state, FK rigid-body state, forces
-    kinematics<false>(L, m, lane, a.p);
+    kinematics<false>(L, m, lane, a.p, a.substeps > 0);
     STAMP(13);
     float* rso = a.root_states + (size_t)e * 13;
     if (lane < 3) { rso[lane] = L.root_pos[lane]; rso[7 + lane] = L.u0[3 + lane]; rso[10 + lane] = L.u0[lane]; }
