@@ -856,6 +856,9 @@ HE_DEV void subtree_levels(float* F, float* I, int lane) {
 
 // ---------------------------------------------------------------------------------- kinematics
 // 2^k-th ancestor of every body (-1: none), for pointer jumping over the body tree
+#ifndef HE_KIN_AXES_FLAT  // joint axes S for lane = dof without the dof loop and root branch
+#define HE_KIN_AXES_FLAT 1
+#endif
 #ifndef HE_KIN_QCACHE  // later substeps start from the integrated local rotations instead of exp(log(.))
 #define HE_KIN_QCACHE 1
 #endif
@@ -1014,6 +1017,26 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
             for (int x = 0; x < 6; ++x) L.Acc[b][x] = A[x];
     }
     sync();
+#if HE_KIN_AXES_FLAT
+    // lane = dof: dofs 0..63 with the root's six unit axes selected in, then dofs 64..74 (ball
+    // joints only); no loop and no root branch
+    auto axis = [&](int i, bool may_root) {
+        const bool rd = may_root && i < 6;
+        const int k = rd ? 0 : i - 6;
+        const int kb = k / 3, c = k - 3 * kb, bb = kb + 1;
+        const f4 qb = f4{L.qw[bb][0], L.qw[bb][1], L.qw[bb][2], L.qw[bb][3]};
+        const f3 e = f3{c == 0 ? 1.f : 0.f, c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f};
+        const f3 ax = qapply(qb, e);
+        const f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]} - o, ax);
+        const float g[6] = {ax.x, ax.y, ax.z, l.x, l.y, l.z};
+        float* S = L.S[i];
+#pragma unroll
+        for (int x = 0; x < 6; ++x) S[x] = rd ? (x == i ? 1.f : 0.f) : g[x];
+    };
+    axis(lane, true);
+    static_assert(NG - W <= W && NG - W > 0, "a second set of lanes covers dofs 64..NG-1");
+    if (lane < NG - W) axis(W + lane, false);
+#else
     for (int i = lane; i < NG; i += W) {
         float* S = L.S[i];
         if (i < 6) {
@@ -1027,6 +1050,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
             S[0] = ax.x; S[1] = ax.y; S[2] = ax.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
         }
     }
+#endif
     sync();
 }
 
