@@ -856,6 +856,9 @@ HE_DEV void subtree_levels(float* F, float* I, int lane) {
 
 // ---------------------------------------------------------------------------------- kinematics
 // 2^k-th ancestor of every body (-1: none), for pointer jumping over the body tree
+#ifndef HE_DOF_FLAT  // bias / IS / drive terms for lane = dof without the dof loop and root branch
+#define HE_DOF_FLAT 1
+#endif
 #ifndef HE_KIN_AXES_FLAT  // joint axes S for lane = dof without the dof loop and root branch
 #define HE_KIN_AXES_FLAT 1
 #endif
@@ -1165,6 +1168,31 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     __builtin_amdgcn_s_setprio(0);
     STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
+#if HE_DOF_FLAT
+    // lane = dof (then dofs 64..74 on lanes 0..10), the root's six dofs selected out: no loop,
+    // no root branch, saturation by selects
+    auto dof_terms = [&](int i, bool may_root) {
+        const int b = may_root ? dof_body(i) : (i - 6) / 3 + 1;
+        const float bias = dot6(L.S[i], L.F[b]);
+        si_apply(L.Ic[b], L.S[i], L.IS[i]);
+        const bool jd = !may_root || i >= 6;
+        const int d = jd ? i - 6 : 0;
+        float kp = m.stiffness[d] * p.kp_scale, kd = m.damping[d] * p.kd_scale;
+        const float err = L.tgt[d] - L.q[d];
+        const float u = L.u0[i];
+        float tau = kp * (err - dt * u) - kd * u;
+        const float lim = m.effort[d];
+        const bool sat = fabsf(tau) > lim;
+        tau = sat ? (tau > 0.f ? lim : -lim) : tau;
+        kp = sat ? 0.f : kp;
+        kd = sat ? 0.f : kd;
+        if (jd) L.dforce[d] = tau;
+        L.rhs[i] = dt * (jd ? tau - bias : -bias);
+        L.coef[i] = jd ? dt * kp + kd : 0.f;
+    };
+    dof_terms(lane, true);
+    if (lane < NG - W) dof_terms(W + lane, false);
+#else
     for (int i = lane; i < NG; i += W) {
         int b = dof_body(i);
         float bias = dot6(L.S[i], L.F[b]);
@@ -1185,6 +1213,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         L.rhs[i] = dt * rhs;
         L.coef[i] = cf;
     }
+#endif
     sync();
     STAMP(3);
     // ---- CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i
