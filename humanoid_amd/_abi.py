@@ -13,7 +13,9 @@ NB, ND, NG = 24, 69, 75
 MAX_PAIRS, MAX_CONTACTS = 256, 21
 OBS_SELF, OBS_TASK, OBS_DIM = 358, 576, 934
 
-BUF_ROOT_STATE, BUF_DOF_STATE, BUF_RB_STATE, BUF_CONTACT_FORCE, BUF_DOF_FORCE, BUF_DOF_TARGET, BUF_NUM_CONTACTS = range(7)
+(BUF_ROOT_STATE, BUF_DOF_STATE, BUF_RB_STATE, BUF_CONTACT_FORCE, BUF_DOF_FORCE, BUF_DOF_TARGET, BUF_NUM_CONTACTS,
+ BUF_DROPPED_CONTACTS, BUF_CONTACT_CACHE) = range(9)
+CACHE_WORDS, CACHE_KEYS, CACHE_LAMBDA = 96, 8, 32  # he_sim_params warm-start cache layout
 DTYPE_F32, DTYPE_I32 = 1, 2
 
 
@@ -25,6 +27,7 @@ class HeModel(C.Structure):
         ("inertia", (C.c_float * 6) * NB), ("geom_params", (C.c_float * 10) * NB), ("geom_radius", C.c_float * NB),
         ("stiffness", C.c_float * ND), ("damping", C.c_float * ND), ("armature", C.c_float * ND),
         ("effort", C.c_float * ND), ("pairs", (C.c_int32 * 2) * MAX_PAIRS),
+        ("dof_lower", C.c_float * ND), ("dof_upper", C.c_float * ND),
     ]
 
 
@@ -35,6 +38,7 @@ class HeSimParams(C.Structure):
         ("max_angular_velocity", C.c_float), ("solver_iterations", C.c_int32), ("self_collision", C.c_int32),
         ("max_contacts", C.c_int32), ("kp_scale", C.c_float), ("kd_scale", C.c_float), ("terrain", C.c_int32),
         ("terrain_slope", C.c_float), ("step_height", C.c_float), ("step_length", C.c_float),
+        ("joint_limits", C.c_int32), ("limit_margin", C.c_float), ("warm_start", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -79,6 +83,8 @@ def make_model(m: HumanoidModel) -> HeModel:
         hm.damping[d] = float(m.damping[d])
         hm.armature[d] = float(m.armature[d])
         hm.effort[d] = float(m.effort[d])
+        hm.dof_lower[d] = float(m.dof_lower[d])
+        hm.dof_upper[d] = float(m.dof_upper[d])
     for i, (a, b) in enumerate(pairs):
         hm.pairs[i][0], hm.pairs[i][1] = int(a), int(b)
     return hm
@@ -104,6 +110,9 @@ def default_sim_params(**kw) -> HeSimParams:
     p.terrain_slope = float(np.deg2rad(10.0))
     p.step_height = 0.05
     p.step_length = 0.4
+    p.joint_limits = 1  # the MJCF ranges, enforced by PhysX (humanoid_phc.py:305-324)
+    p.limit_margin = 0.1
+    p.warm_start = 1
     for k, v in kw.items():
         setattr(p, k, v)
     return p

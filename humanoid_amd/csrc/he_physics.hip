@@ -1182,10 +1182,16 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const float u = L.u0[i];
         float tau = kp * (err - dt * u) - kd * u;
         const float lim = m.effort[d];
-        const bool sat = fabsf(tau) > lim;
-        tau = sat ? (tau > 0.f ? lim : -lim) : tau;
-        kp = sat ? 0.f : kp;
-        kd = sat ? 0.f : kd;
+        // effort limit: the implicit step's drive torque, estimated with the dof's own joint-space
+        // inertia H_ii = S_i . IS_i (+ armature) as tau - c dt (tau - bias) / (H_ii + dt c), scales
+        // the whole drive down to the limit (oracle/he_oracle_physics.c, the drive block)
+        const float c = dt * kp + kd;
+        const float hii = dot6(L.S[i], L.IS[i]) + m.armature[d];
+        const float tau_i = tau - c * dt * (tau - bias) / (hii + dt * c);
+        const float sc = fabsf(tau_i) > lim ? lim / fabsf(tau_i) : 1.f;
+        tau *= sc;
+        kp *= sc;
+        kd *= sc;
         if (jd) L.dforce[d] = tau;
         L.rhs[i] = dt * (jd ? tau - bias : -bias);
         L.coef[i] = jd ? dt * kp + kd : 0.f;
@@ -1205,7 +1211,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float u = L.u0[i];
             float tau = kp * (err - dt * u) - kd * u;
             float lim = m.effort[d];
-            if (fabsf(tau) > lim) { tau = tau > 0.f ? lim : -lim; kp = 0.f; kd = 0.f; }
+            const float c = dt * kp + kd;
+            const float tau_i = tau - c * dt * (tau - bias) / (dot6(L.S[i], L.IS[i]) + m.armature[d] + dt * c);
+            if (fabsf(tau_i) > lim) {
+                const float sc = lim / fabsf(tau_i);
+                tau *= sc; kp *= sc; kd *= sc;
+            }
             L.dforce[d] = tau;
             rhs += tau;
             cf = dt * kp + kd;

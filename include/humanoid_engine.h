@@ -53,6 +53,9 @@ typedef struct he_model {
     float geom_radius[HE_NUM_BODIES];
     float stiffness[HE_NUM_DOF], damping[HE_NUM_DOF], armature[HE_NUM_DOF], effort[HE_NUM_DOF];
     int32_t pairs[HE_MAX_PAIRS][2];      /* self-collision candidate pairs */
+    /* dof ranges (rad) from the MJCF joint ranges (get_asset_dof_properties lower/upper,
+     * humanoid_phc.py:305-324), enforced on the exp-map coordinates when joint_limits is set */
+    float dof_lower[HE_NUM_DOF], dof_upper[HE_NUM_DOF];
 } he_model;
 
 /* Simulation parameters: isaacgym_env.py:6-35 + asset options humanoid_phc.py:211-214. */
@@ -72,7 +75,24 @@ typedef struct he_sim_params {
     int32_t terrain;                 /* 0 plane everywhere, 1 per-env terrain kind (config 5) */
     float terrain_slope;             /* radians, terrain kind 1 */
     float step_height, step_length;  /* terrain kind 2 (box steps along +x) */
+    int32_t joint_limits;            /* 1: unilateral limit rows on the dof ranges (PhysX limits) */
+    float limit_margin;              /* rad: a limit row is emitted within margin + dt*closing rate */
+    int32_t warm_start;              /* 1: the solver starts from the previous solve's impulses */
+    int32_t reserved;
 } he_sim_params;
+
+/* Per-env solver warm-start cache (f32 words; HE_BUF_CONTACT_CACHE), written at the end of every
+ * step and read at the start of the next when the env's root pose still equals the signature
+ * (any external state write -- a reset -- invalidates it):
+ *   [0,7)  signature: root position, root quaternion as written by the step
+ *   7      number of cached contact slots (int32 bits)
+ *   [8,8+HE_MAX_CONTACTS)  contact keys (int32 bits): body0 | (body1 + 2) << 8 | sub << 16 with
+ *          body1 = -1 terrain (sub = candidate: capsule end / box corner), -2 joint limit
+ *          (sub = 1 + 2 axis + side), else the self-collision partner (sub = 0)
+ *   [32,32+3*HE_MAX_CONTACTS)  impulses of the slots' rows (normal, friction, friction) */
+#define HE_CACHE_WORDS 96
+#define HE_CACHE_KEYS 8
+#define HE_CACHE_LAMBDA 32
 
 /* Imitation (reward / reset / obs) parameters: config.py:37-50, 97-112; humanoid_phc.py:1230-1335. */
 typedef struct he_imitation_params {
@@ -95,8 +115,10 @@ typedef enum he_buf_kind {
     HE_BUF_CONTACT_FORCE = 3,  /* f32 [N*24,3]                            (acquire_net_contact_force_tensor) */
     HE_BUF_DOF_FORCE = 4,      /* f32 [N*69]                              (acquire_dof_force_tensor) */
     HE_BUF_DOF_TARGET = 5,     /* f32 [N,69]  position targets            (set_dof_position_target_tensor) */
-    HE_BUF_NUM_CONTACTS = 6,   /* i32 [N]     contacts used last substep  (diagnostic) */
-    HE_BUF_COUNT = 7
+    HE_BUF_NUM_CONTACTS = 6,   /* i32 [N]     contact slots used last substep (limits included) */
+    HE_BUF_DROPPED_CONTACTS = 7, /* i32 [N]   contacts generated past the capacity, last substep */
+    HE_BUF_CONTACT_CACHE = 8,  /* f32 [N,HE_CACHE_WORDS] solver warm-start cache (see above) */
+    HE_BUF_COUNT = 9
 } he_buf_kind;
 
 #define HE_DTYPE_F32 1   /* GymTensor.h:23 eGymDataTypeFp32 */

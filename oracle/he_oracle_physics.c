@@ -11,7 +11,7 @@
  * Algorithm per substep (generalized velocity u = [w_root(3), v_root(3), joint(69)],
  * joint velocity = relative angular velocity in the child frame, joint position = exp map):
  *   FK -> spatial axes S about the root origin o -> RNEA bias (gravity + Coriolis)
- *   -> CRBA mass matrix + armature -> implicit PD (effort-saturated dofs explicit)
+ *   -> CRBA mass matrix + armature -> implicit PD (effort limit: the drive scaled down)
  *   -> branch-induced sparse LTDL factorisation -> free velocity
  *   -> ground + self contacts (speculative within contact_offset) -> Delassus A = Z^T D^-1 Z
  *      with Z = L^-T J^T -> projected Gauss-Seidel (pyramidal friction) -> velocity update
@@ -27,7 +27,9 @@ typedef double R;
 #define NB HE_NUM_BODIES
 #define ND HE_NUM_DOF
 #define NG HE_NUM_GEN
-#define MAXC HE_MAX_CONTACTS
+/* The oracle's own contact capacity: max_contacts above the engine's HE_MAX_CONTACTS makes the
+ * engine's truncation visible (tests/test_contacts.py); the warm-start cache needs <= 21. */
+#define MAXC 64
 #define MAXROW (3 * MAXC)
 
 typedef struct topo {
@@ -214,11 +216,16 @@ static void body_inertia(const he_model* m, const kin* k, int b, R mass_scale, s
 }
 
 /* ---------------------------------------------------------------- contacts */
+/* A contact slot has three rows (normal, two friction directions). A joint-limit slot has the
+ * limit row in the normal position and two zero rows (mu 0), so that limits and contacts share
+ * one row layout and one Gauss-Seidel order with the engine. */
 typedef struct contact {
-    int b0, b1;       /* b1 = -1 for terrain */
+    int b0, b1;       /* b1 = -1 for terrain, -2 for a joint limit (b0 = the joint's body) */
+    int key;          /* warm-start key: b0 | (b1 + 2) << 8 | sub << 16 */
     R x[3], n[3], t1[3], t2[3];
     R gap;
     R mu;
+    R g[3];           /* joint limit: the row over the joint's three dofs */
 } contact;
 
 static R terrain_height(const he_sim_params* p, int kind, const R* x, R* n) {
@@ -308,21 +315,128 @@ static void seg_seg(const R* p1, const R* q1, const R* p2, const R* q2, R* c1, R
     for (int i = 0; i < 3; ++i) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
 }
 
-static int add_contact(contact* cs, int nc, int maxc, int b0, int b1, const R* x, const R* n, R gap, R mu) {
+static int add_contact(contact* cs, int nc, int maxc, int* total, int b0, int b1, int sub, const R* x, const R* n,
+                       R gap, R mu) {
+    ++*total; /* every generated contact counts; the ones past the capacity are dropped */
     if (nc >= maxc) return nc;
     contact* c = &cs[nc];
     c->b0 = b0; c->b1 = b1;
+    c->key = b0 | ((b1 + 2) << 8) | (sub << 16);
     memcpy(c->x, x, sizeof(R) * 3);
     memcpy(c->n, n, sizeof(R) * 3);
     c->gap = gap;
     c->mu = mu;
+    c->g[0] = c->g[1] = c->g[2] = 0;
     friction_basis(n, c->t1, c->t2);
     return nc + 1;
 }
 
-static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k, int terrain_kind, R mu, contact* cs) {
-    int maxc = p->max_contacts < MAXC ? p->max_contacts : MAXC;
+/* Row c of the inverse right Jacobian of SO(3) at the rotation vector th: the rate of the
+ * exp-map joint coordinates is J_r^-1(th) u for the joint's relative angular velocity u (child
+ * frame), because the joint integrates exp(q+) = exp(q) exp(dt u).
+ *   J_r^-1 = I + [th]x / 2 + k(|th|) [th]x^2,  k = 1/t^2 - cos(t/2) / (2 t sin(t/2)) */
+static void jr_inv_row(const R* th, int c, R* row) {
+    R t2 = dot3(th, th), t = sqrt(t2);
+    R k = t < 1e-2 ? 1.0 / 12.0 + t2 / 720.0 : 1.0 / t2 - cos(0.5 * t) / (2.0 * t * sin(0.5 * t));
+    R e[3] = {c == 0, c == 1, c == 2};
+    R cr[3]; /* row c of [th]x */
+    if (c == 0) { cr[0] = 0; cr[1] = -th[2]; cr[2] = th[1]; }
+    else if (c == 1) { cr[0] = th[2]; cr[1] = 0; cr[2] = -th[0]; }
+    else { cr[0] = -th[1]; cr[1] = th[0]; cr[2] = 0; }
+    for (int x = 0; x < 3; ++x) row[x] = e[x] + 0.5 * cr[x] + k * (th[c] * th[x] - t2 * e[x]);
+}
+
+/* Joint limits (MJCF ranges, humanoid_phc.py:305-324) as unilateral rows on the exp-map joint
+ * coordinates, speculative: a row is emitted within limit_margin + dt * (closing rate) of its bound.
+ *  - component bounds inside (-pi, pi) (none in the SMPL MJCF, whose ranges are +-180 / +-720 deg):
+ *    dof d of joint b with rate v = J_r^-1(q_b)_c . u_b, upper row -J_r^-1 row (gap upper - q_d),
+ *    lower row +J_r^-1 row (gap q_d - lower);
+ *  - the rotation angle |q_b| <= pi - LIMIT_PI_GUARD for every joint: a +-pi bound on an exp-map
+ *    coordinate sits on the log map's branch cut (|q| = pi), where the coordinate wraps to -pi and
+ *    the drive keeps spinning the joint (a +5 rad knee target). d|q|/dt = q^.u (q^ = q/|q| is a
+ *    fixed vector of J_r^-1), so the row is -q^ over the joint's dofs, gap pi - guard - |q|.
+ * Order: component rows in dof order (upper, then lower), then angle rows in joint order. */
+#define LIMIT_PI_GUARD 0.02
+/* the angle row of joint b: emitted (returns 1) within the margin of |q_b| = pi - guard */
+static int angle_row(const he_sim_params* p, const env_state* s, int b, R* gap, R* dir) {
+    const R* th = &s->q[3 * (b - 1)];
+    const R* u = &s->u[3 * (b - 1)];
+    R t = sqrt(dot3(th, th));
+    if (t < 1e-6) return 0;
+    for (int x = 0; x < 3; ++x) dir[x] = th[x] / t;
+    *gap = M_PI - LIMIT_PI_GUARD - t;
+    R closing = dot3(dir, u);
+    return *gap < p->limit_margin + p->dt * (closing > 0 ? closing : 0);
+}
+static int gen_limits(const he_model* m, const he_sim_params* p, const env_state* s, contact* cs, int maxc, int* total) {
     int nc = 0;
+    const R zero3[3] = {0, 0, 0}, up[3] = {0, 0, 1};
+    const R cut = M_PI - LIMIT_PI_GUARD;
+    for (int d = 0; d < ND; ++d) {
+        int b = d / 3 + 1, c = d % 3;
+        const R* th = &s->q[3 * (b - 1)];
+        const R* u = &s->u[3 * (b - 1)];
+        R row[3];
+        jr_inv_row(th, c, row);
+        R v = dot3(row, u);
+        for (int side = 0; side < 2; ++side) {
+            R bound = side == 0 ? m->dof_upper[d] : m->dof_lower[d];
+            if (fabs(bound) >= cut) continue; /* held by the angle row */
+            R gap = side == 0 ? bound - s->q[d] : s->q[d] - bound;
+            R closing = side == 0 ? v : -v;
+            if (gap < p->limit_margin + p->dt * (closing > 0 ? closing : 0)) {
+                int slot = nc;
+                nc = add_contact(cs, nc, maxc, total, b, -2, 1 + 2 * c + side, zero3, up, gap, 0.0);
+                if (nc > slot)
+                    for (int x = 0; x < 3; ++x) cs[slot].g[x] = side == 0 ? -row[x] : row[x];
+            }
+        }
+    }
+    for (int b = 1; b < NB; ++b) {
+        R gap, dir[3];
+        if (angle_row(p, s, b, &gap, dir)) {
+            int slot = nc;
+            nc = add_contact(cs, nc, maxc, total, b, -2, 7, zero3, up, gap, 0.0);
+            if (nc > slot)
+                for (int x = 0; x < 3; ++x) cs[slot].g[x] = -dir[x];
+        }
+    }
+    return nc;
+}
+
+/* Contact slots: joint limits, terrain (bodies in order, box corners deepest-first), self pairs.
+ * All are generated (up to the oracle's own MAXC); when they exceed max_contacts, the limits are
+ * kept and the contacts reduced to the deepest (smallest gap, ties in slot order), in slot order:
+ * the shallow speculative contacts go first, never a body's only penetrating one.
+ * Returns the slots used (<= max_contacts); *total counts every contact generated. */
+static int gen_all(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
+                   R mu, contact* cs, int* total, int* nlim_out);
+static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
+                        R mu, contact* cs, int* total) {
+    int nlim = 0;
+    int nc = gen_all(m, p, k, s, terrain_kind, mu, cs, total, &nlim);
+    int maxc = p->max_contacts < MAXC ? p->max_contacts : MAXC;
+    if (nc <= maxc) return nc;
+    int keep = maxc - nlim; /* contact slots left after the limits */
+    if (keep < 0) { keep = 0; nlim = maxc; }
+    int kept[MAXC];
+    for (int i = nlim; i < nc; ++i) {
+        int rank = 0; /* contacts deeper than i (ties: earlier slots first) */
+        for (int j = nlim; j < nc; ++j)
+            if (cs[j].gap < cs[i].gap || (cs[j].gap == cs[i].gap && j < i)) ++rank;
+        kept[i] = rank < keep;
+    }
+    int out = nlim;
+    for (int i = nlim; i < nc; ++i)
+        if (kept[i]) cs[out++] = cs[i];
+    return out;
+}
+static int gen_all(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
+                   R mu, contact* cs, int* total, int* nlim_out) {
+    int maxc = MAXC;
+    *total = 0;
+    int nc = p->joint_limits ? gen_limits(m, p, s, cs, maxc, total) : 0;
+    *nlim_out = nc;
     R off = p->contact_offset;
     for (int b = 0; b < NB; ++b) {
         const float* g = m->geom_params[b];
@@ -333,7 +447,7 @@ static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k,
             R d = terrain_height(p, terrain_kind, c, n) - g[3];
             if (d < off) {
                 for (int i = 0; i < 3; ++i) x[i] = c[i] - g[3] * n[i];
-                nc = add_contact(cs, nc, maxc, b, -1, x, n, d, mu);
+                nc = add_contact(cs, nc, maxc, total, b, -1, 0, x, n, d, mu);
             }
         } else if (m->geom_type[b] == HE_GEOM_CAPSULE) {
             for (int e = 0; e < 2; ++e) {
@@ -342,7 +456,7 @@ static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k,
                 R d = terrain_height(p, terrain_kind, c, n) - g[6];
                 if (d < off) {
                     for (int i = 0; i < 3; ++i) x[i] = c[i] - g[6] * n[i];
-                    nc = add_contact(cs, nc, maxc, b, -1, x, n, d, mu);
+                    nc = add_contact(cs, nc, maxc, total, b, -1, e, x, n, d, mu);
                 }
             }
         } else {
@@ -366,7 +480,7 @@ static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k,
                 for (int j = 1; j < ncand; ++j)
                     if (cd[cand[j]] < cd[cand[best]]) best = j;
                 int ci = cand[best];
-                nc = add_contact(cs, nc, maxc, b, -1, cx[ci], cn[ci], cd[ci], mu);
+                nc = add_contact(cs, nc, maxc, total, b, -1, ci, cx[ci], cn[ci], cd[ci], mu);
                 for (int j = best; j < ncand - 1; ++j) cand[j] = cand[j + 1];
                 --ncand;
             }
@@ -388,7 +502,7 @@ static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k,
                 else { n[0] = 0; n[1] = 0; n[2] = 1; }
                 R x[3];
                 for (int c = 0; c < 3; ++c) x[c] = cj[c] + n[c] * (rj + 0.5 * gap);
-                nc = add_contact(cs, nc, maxc, i, j, x, n, gap, mu);
+                nc = add_contact(cs, nc, maxc, total, i, j, 0, x, n, gap, mu);
             }
         }
     }
@@ -418,11 +532,22 @@ typedef struct step_out {
     R contact_force[NB][3];
     R dof_force[ND];
     int num_contacts;
+    int dropped;          /* contacts generated past the capacity (last substep) */
+    R residual;           /* max |complementarity residual| of the last substep's solve (m/s) */
 } step_out;
+
+/* Warm-start cache: the previous solve's impulses by contact key (PhysX warm-starts its solver
+ * from the previous frame's impulses). Rows of a contact whose key is found start at the cached
+ * impulse instead of 0. */
+typedef struct warm_cache {
+    int n;
+    int key[MAXC];
+    R lam[MAXC][3];
+} warm_cache;
 
 /* one substep; updates s in place */
 static void substep(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
-                    R mu, int terrain_kind, step_out* out) {
+                    R mu, int terrain_kind, step_out* out, warm_cache* ws) {
     static __thread kin k;
     static __thread R H[NG][NG];
     static __thread R Z[MAXROW][NG];
@@ -481,8 +606,15 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
             H[j][i] = v;
         }
     }
-    /* armature + implicit PD drives */
+    /* armature + implicit PD drives; a joint at its angle limit cannot give way to its drive, so
+     * its effort check takes the drive torque at rest (no implicit relief) */
     R rhs[NG], coef[NG];
+    int blocked[NB] = {0};
+    if (p->joint_limits)
+        for (int b = 1; b < NB; ++b) {
+            R gap, dir[3];
+            blocked[b] = angle_row(p, s, b, &gap, dir);
+        }
     for (int i = 0; i < NG; ++i) { rhs[i] = -bias[i]; coef[i] = 0; }
     for (int d = 0; d < ND; ++d) {
         int g = 6 + d;
@@ -492,14 +624,23 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         R u = s->u[d];
         R tau = kp * (err - dt * u) - kd * u;
         R lim = m->effort[d];
-        if (fabs(tau) <= lim) {
-            H[g][g] += dt * (kd + dt * kp);
-            out->dof_force[d] = tau; /* updated after the solve */
-        } else {
-            tau = tau > 0 ? lim : -lim;
-            out->dof_force[d] = tau;
-            kp = kd = 0;
+        /* Effort limit (dof_prop["effort"], humanoid_phc.py:324): PhysX solves the position drive
+         * implicitly and clamps its impulse to maxForce dt. Restated per dof: the implicit step's
+         * drive torque is estimated with the dof's own joint-space inertia h = H_gg (+ armature),
+         * tau(u+) ~ tau - c dt (tau - bias) / (h + dt c) with c = dt kp + kd; when it exceeds the
+         * limit, the whole drive (stiffness and damping) is scaled by lim / |tau(u+)|. The drive
+         * stays an implicit spring-damper (unconditionally stable), only weaker; an explicit +-lim
+         * torque without its damping drives light links into a bang-bang limit cycle. */
+        R c = dt * kp + kd;
+        R tau_i = blocked[d / 3 + 1] ? tau : tau - c * dt * (tau - bias[g]) / (H[g][g] + dt * c);
+        if (fabs(tau_i) > lim) {
+            R sc = lim / fabs(tau_i);
+            kp *= sc;
+            kd *= sc;
+            tau *= sc;
         }
+        H[g][g] += dt * (kd + dt * kp);
+        out->dof_force[d] = tau; /* updated after the solve */
         rhs[g] += tau;
         coef[g] = dt * kp + kd; /* d tau / d u+ for the post-solve drive force */
     }
@@ -514,8 +655,11 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     for (int d = 0; d < ND; ++d) u0[6 + d] = s->u[d];
     for (int i = 0; i < NG; ++i) uf[i] = u0[i] + du[i];
     /* contacts */
-    int nc = gen_contacts(m, p, &k, terrain_kind, mu, cs);
+    int total = 0;
+    int nc = gen_contacts(m, p, &k, s, terrain_kind, mu, cs, &total);
     out->num_contacts = nc;
+    out->dropped = total - nc;
+    out->residual = 0;
     memset(out->contact_force, 0, sizeof(out->contact_force));
     R unew[NG];
     memcpy(unew, uf, sizeof(unew));
@@ -524,17 +668,23 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         R brow[MAXROW];
         for (int r = 0; r < nr; ++r) {
             const contact* c = &cs[r / 3];
-            const R* dir = (r % 3 == 0) ? c->n : (r % 3 == 1 ? c->t1 : c->t2);
-            R rho[3], xo[3] = {c->x[0] - k.o[0], c->x[1] - k.o[1], c->x[2] - k.o[2]};
-            cross3(xo, dir, rho);
             R* z = Z[r];
-            for (int i = 0; i < NG; ++i) {
-                int bi = t->dof_body[i];
-                R sgn = 0;
-                if (t->is_anc[bi][c->b0]) sgn += 1;
-                if (c->b1 >= 0 && t->is_anc[bi][c->b1]) sgn -= 1;
-                const R* S = k.S[i];
-                z[i] = sgn == 0 ? 0 : sgn * (S[0] * rho[0] + S[1] * rho[1] + S[2] * rho[2] + S[3] * dir[0] + S[4] * dir[1] + S[5] * dir[2]);
+            if (c->b1 == -2) { /* joint limit: the row over the joint's dofs, two zero rows */
+                for (int i = 0; i < NG; ++i) z[i] = 0;
+                if (r % 3 == 0)
+                    for (int x = 0; x < 3; ++x) z[t->body_dof0[c->b0] + x] = c->g[x];
+            } else {
+                const R* dir = (r % 3 == 0) ? c->n : (r % 3 == 1 ? c->t1 : c->t2);
+                R rho[3], xo[3] = {c->x[0] - k.o[0], c->x[1] - k.o[1], c->x[2] - k.o[2]};
+                cross3(xo, dir, rho);
+                for (int i = 0; i < NG; ++i) {
+                    int bi = t->dof_body[i];
+                    R sgn = 0;
+                    if (t->is_anc[bi][c->b0]) sgn += 1;
+                    if (c->b1 >= 0 && t->is_anc[bi][c->b1]) sgn -= 1;
+                    const R* S = k.S[i];
+                    z[i] = sgn == 0 ? 0 : sgn * (S[0] * rho[0] + S[1] * rho[1] + S[2] * rho[2] + S[3] * dir[0] + S[4] * dir[1] + S[5] * dir[2]);
+                }
             }
             R ju = 0;
             for (int i = 0; i < NG; ++i) ju += z[i] * uf[i];
@@ -552,6 +702,13 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
             }
         R lam[MAXROW];
         memset(lam, 0, sizeof(lam));
+        if (ws && p->warm_start)
+            for (int ci = 0; ci < nc; ++ci)
+                for (int j = 0; j < ws->n; ++j)
+                    if (ws->key[j] == cs[ci].key) {
+                        for (int x = 0; x < 3; ++x) lam[3 * ci + x] = ws->lam[j][x];
+                        break;
+                    }
         for (int it = 0; it < p->solver_iterations; ++it) {
             for (int ci = 0; ci < nc; ++ci) {
                 int r0 = 3 * ci;
@@ -569,6 +726,30 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                 }
             }
         }
+        /* complementarity residual of the returned impulses: normal rows min(w, lambda) -> 0,
+         * friction rows w = 0 inside the cone (or lambda on the bound) */
+        for (int ci = 0; ci < nc; ++ci) {
+            int r0 = 3 * ci;
+            for (int x = 0; x < 3; ++x) {
+                int r = r0 + x;
+                R w = brow[r];
+                for (int j = 0; j < nr; ++j) w += A[r][j] * lam[j];
+                R res;
+                if (x == 0) res = fmin(w, lam[r] * A[r][r]);
+                else {
+                    R bound = cs[ci].mu * lam[r0];
+                    res = (lam[r] >= bound - 1e-12 && w < 0) || (lam[r] <= -bound + 1e-12 && w > 0) ? 0 : w;
+                }
+                if (fabs(res) > out->residual) out->residual = fabs(res);
+            }
+        }
+        if (ws) {
+            ws->n = nc;
+            for (int ci = 0; ci < nc; ++ci) {
+                ws->key[ci] = cs[ci].key;
+                for (int x = 0; x < 3; ++x) ws->lam[ci][x] = lam[3 * ci + x];
+            }
+        }
         R y[NG];
         memset(y, 0, sizeof(y));
         for (int r = 0; r < nr; ++r)
@@ -578,12 +759,15 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         for (int i = 0; i < NG; ++i) unew[i] += y[i];
         for (int ci = 0; ci < nc; ++ci) {
             const contact* c = &cs[ci];
+            if (c->b1 == -2) continue; /* joint limits are not contact forces */
             for (int x = 0; x < 3; ++x) {
                 R f = (lam[3 * ci] * c->n[x] + lam[3 * ci + 1] * c->t1[x] + lam[3 * ci + 2] * c->t2[x]) / dt;
                 out->contact_force[c->b0][x] += f;
                 if (c->b1 >= 0) out->contact_force[c->b1][x] -= f;
             }
         }
+    } else if (ws) {
+        ws->n = 0;
     }
     /* drive force actually applied: tau(u+) = tau_exp - (dt kp + kd)(u+ - u) */
     for (int d = 0; d < ND; ++d) out->dof_force[d] -= coef[6 + d] * (unew[6 + d] - u0[6 + d]);
@@ -636,10 +820,13 @@ static void write_rb(const he_model* m, const topo* t, const env_state* s, float
 
 /* gym.simulate x substeps for n envs. root_states [N,13], dof_state [N,69,2] (in/out),
  * targets [N,69]; outputs rb_state [N,24,13], contact_forces [N,24,3], dof_force [N,69],
- * num_contacts [N] (nullable). mass_scale [N,24], friction [N], terrain_kind [N] nullable. */
+ * num_contacts [N] (nullable). mass_scale [N,24], friction [N], terrain_kind [N] nullable.
+ * cache [N,HE_CACHE_WORDS] (in/out, nullable: cold solves), dropped [N] and residual [N] (out,
+ * nullable): contacts past the capacity and the solve's residual, both of the last substep. */
 void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* root_states, float* dof_state,
                      const float* targets, int substeps, float* rb_state, float* contact_forces, float* dof_force,
-                     int32_t* num_contacts, const float* mass_scale, const float* friction, const int32_t* terrain_kind) {
+                     int32_t* num_contacts, const float* mass_scale, const float* friction, const int32_t* terrain_kind,
+                     float* cache, int32_t* dropped, float* residual) {
     topo t;
     build_topo(m, &t);
 #pragma omp parallel for schedule(dynamic, 4)
@@ -657,9 +844,23 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         if (mass_scale) for (int b = 0; b < NB; ++b) ms[b] = mass_scale[(size_t)e * NB + b];
         R mu = friction ? friction[e] : p->friction;
         int tk = (p->terrain && terrain_kind) ? terrain_kind[e] : 0;
+        warm_cache ws;
+        ws.n = 0;
+        float* cw = cache ? cache + (size_t)e * HE_CACHE_WORDS : NULL;
+        if (cw && p->warm_start && memcmp(cw, rs, 7 * sizeof(float)) == 0) {
+            int32_t nn;
+            memcpy(&nn, cw + 7, 4);
+            ws.n = nn < 0 ? 0 : (nn > HE_MAX_CONTACTS ? HE_MAX_CONTACTS : nn);
+            for (int j = 0; j < ws.n; ++j) {
+                int32_t key;
+                memcpy(&key, cw + HE_CACHE_KEYS + j, 4);
+                ws.key[j] = key;
+                for (int x = 0; x < 3; ++x) ws.lam[j][x] = cw[HE_CACHE_LAMBDA + 3 * j + x];
+            }
+        }
         step_out out;
         memset(&out, 0, sizeof(out));
-        for (int it = 0; it < substeps; ++it) substep(m, &t, p, &s, mass_scale ? ms : NULL, mu, tk, &out);
+        for (int it = 0; it < substeps; ++it) substep(m, &t, p, &s, mass_scale ? ms : NULL, mu, tk, &out, &ws);
         for (int c = 0; c < 3; ++c) { rs[c] = (float)s.root_pos[c]; rs[7 + c] = (float)s.root_v[c]; rs[10 + c] = (float)s.root_w[c]; }
         for (int c = 0; c < 4; ++c) rs[3 + c] = (float)s.root_q[c];
         for (int d = 0; d < ND; ++d) {
@@ -671,6 +872,21 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         for (int b = 0; b < NB; ++b)
             for (int c = 0; c < 3; ++c) contact_forces[((size_t)e * NB + b) * 3 + c] = (float)out.contact_force[b][c];
         if (num_contacts) num_contacts[e] = out.num_contacts;
+        if (dropped) dropped[e] = out.dropped;
+        if (residual) residual[e] = (float)out.residual;
+        if (cw) {
+            memset(cw, 0, HE_CACHE_WORDS * sizeof(float));
+            if (p->warm_start) {
+                memcpy(cw, rs, 7 * sizeof(float));
+                int32_t nn = ws.n > HE_MAX_CONTACTS ? HE_MAX_CONTACTS : ws.n;
+                memcpy(cw + 7, &nn, 4);
+                for (int j = 0; j < nn; ++j) {
+                    int32_t key = ws.key[j];
+                    memcpy(cw + HE_CACHE_KEYS + j, &key, 4);
+                    for (int x = 0; x < 3; ++x) cw[HE_CACHE_LAMBDA + 3 * j + x] = (float)ws.lam[j][x];
+                }
+            }
+        }
     }
 }
 

@@ -126,20 +126,31 @@ def reset_envs(params, mt: MotionTables, env_ids, phases, motion_ids, state):
     return state
 
 
+def new_cache(n):
+    """Empty warm-start cache [N, HE_CACHE_WORDS] (float32 words, include/humanoid_engine.h)."""
+    return np.zeros((n, _abi.CACHE_WORDS), np.float32)
+
+
 def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, dof_state, targets, substeps=2,
-                 mass_scale=None, friction=None, terrain_kind=None):
-    """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays). Returns outputs."""
+                 mass_scale=None, friction=None, terrain_kind=None, cache=None):
+    """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays) and on the warm-start
+    `cache` [N, HE_CACHE_WORDS] (None = cold solves). Returns outputs, including the contacts
+    dropped past the capacity and the solve's residual (last substep)."""
     n = root_states.shape[0]
     assert root_states.dtype == np.float32 and root_states.flags.c_contiguous
     assert dof_state.dtype == np.float32 and dof_state.flags.c_contiguous
+    if cache is not None:
+        assert cache.dtype == np.float32 and cache.flags.c_contiguous and cache.shape == (n, _abi.CACHE_WORDS)
     out = dict(rb_state=np.zeros((n, 24, 13), np.float32), contact_forces=np.zeros((n, 24, 3), np.float32),
-               dof_force=np.zeros((n, 69), np.float32), num_contacts=np.zeros(n, np.int32))
+               dof_force=np.zeros((n, 69), np.float32), num_contacts=np.zeros(n, np.int32),
+               dropped=np.zeros(n, np.int32), residual=np.zeros(n, np.float32))
     ms = None if mass_scale is None else f32(mass_scale)
     fr = None if friction is None else f32(friction)
     tk = None if terrain_kind is None else np.ascontiguousarray(terrain_kind, np.int32)
     lib().ho_physics_step(C.byref(model), C.byref(sim), C.c_int(n), _p(root_states), _p(dof_state), _p(f32(targets)),
                           C.c_int(substeps), _p(out["rb_state"]), _p(out["contact_forces"]), _p(out["dof_force"]),
-                          _p(out["num_contacts"]), _p(ms), _p(fr), _p(tk))
+                          _p(out["num_contacts"]), _p(ms), _p(fr), _p(tk), _p(cache), _p(out["dropped"]),
+                          _p(out["residual"]))
     return out
 
 

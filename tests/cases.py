@@ -45,3 +45,46 @@ def lying_state(n, rng):
     dof = np.zeros((n, 69, 2), np.float32)
     dof[..., 0] = rng.uniform(-0.2, 0.2, (n, 69))
     return root, dof
+
+
+def _qmat(q):
+    """xyzw quaternions [...,4] -> rotation matrices [...,3,3] (float64)."""
+    q = np.asarray(q, np.float64)
+    x, y, z, w = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+    return np.stack([
+        np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)], -1),
+        np.stack([2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)], -1),
+        np.stack([2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)], -1)], -2)
+
+
+def center_of_mass(model, rb_state):
+    """Mass-weighted centre of mass [N,3] from rigid-body rows [N,24,13] (body origin + rotation)."""
+    rb = np.asarray(rb_state, np.float64)
+    R = _qmat(rb[..., 3:7])
+    com_w = rb[..., :3] + np.einsum("nbij,bj->nbi", R, np.asarray(model.com, np.float64))
+    m = np.asarray(model.mass, np.float64)
+    return (com_w * m[None, :, None]).sum(1) / m.sum()
+
+
+def ground_gaps(model, rb_state):
+    """Signed distance to the z=0 plane of every terrain contact candidate of each body (sphere
+    centre, capsule end points, box corners, minus the radius) -> min over candidates [N,24]."""
+    from humanoid_amd import _abi
+    rb = np.asarray(rb_state, np.float64)
+    R = _qmat(rb[..., 3:7])
+    n = rb.shape[0]
+    out = np.full((n, rb.shape[1]), np.inf)
+    for b in range(rb.shape[1]):
+        g = np.asarray(model.geom_params[b], np.float64)
+        t = int(model.geom_type[b])
+        if t == 0:
+            pts, rad = g[None, 0:3], g[3]
+        elif t == 1:
+            pts, rad = np.stack([g[0:3], g[3:6]]), g[6]
+        else:
+            bm = _qmat(g[6:10])
+            sg = np.array([[(c & 1) * 2 - 1, ((c >> 1) & 1) * 2 - 1, ((c >> 2) & 1) * 2 - 1] for c in range(8)], np.float64)
+            pts, rad = g[None, 0:3] + (sg * g[3:6]) @ bm.T, 0.0
+        w = rb[:, b, None, :3] + np.einsum("nij,kj->nki", R[:, b], pts)
+        out[:, b] = w[..., 2].min(-1) - rad
+    return out

@@ -1,0 +1,147 @@
+"""Joint limits, contact capacity and warm starting in the fp64 oracle (CPU).
+
+* Joint limits: the MJCF ranges (+-180 deg, +-720 deg at shoulders / elbows, humanoid_phc.py:305-324)
+  as unilateral rows on the exp-map coordinates. The knee-y PD scale is 5 rad (humanoid_phc.py:441-446),
+  so a saturated action targets +-5 rad, past the +-pi range: without limits the knee is driven through
+  pi, its exp-map coordinate wraps to -pi and the drive keeps spinning it; with limits it stops at pi.
+* Capacity: the engine has HE_MAX_CONTACTS = 21 slots (3 rows each, one wave). Overflow is counted
+  (`dropped`) and the slots go to the deepest contacts, so a lying body's hand keeps its penetrating
+  contact (round 1 truncated in body order: the right arm sank).
+* Warm start: the solve starting from the previous impulses converges where the cold 8-iteration PGS
+  does not (stand-still jitter, lying-body residual).
+"""
+import numpy as np
+
+from humanoid_amd import _abi
+from oracle import oracle as O
+
+import cases
+
+KNEE_Y = (4, 16)  # L_Knee / R_Knee y (humanoid_phc.py:441-446)
+
+
+def _knee_run(he_model, model, sign, steps=45, **sim):
+    rng = np.random.default_rng(7)
+    n = 4
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    root[:, 2] += 1.5  # airborne: nothing but the drives and the limits act on the knees
+    targets = np.zeros((n, 69), np.float32)
+    targets[:, list(KNEE_Y)] = sign * 5.0  # offset 0 + scale 5 x action +-1
+    sp = _abi.default_sim_params(self_collision=0, **sim)
+    cache = O.new_cache(n)
+    r, d = root.copy(), dof.copy()
+    hist = []
+    for _ in range(steps):
+        O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
+        hist.append(np.stack([d[:, k - 1:k + 2, 0] for k in KNEE_Y], axis=1))
+    return np.array(hist)  # [steps, n, knee, xyz]
+
+
+def test_knee_limit_holds_at_pi(he_model, model):
+    """The knee's rotation stops at the limit: |q| <= pi (|q| <= pi + 1e-3; the engine
+    holds the angle 0.02 rad inside the branch cut) and its y coordinate never wraps sign."""
+    for sign in (1.0, -1.0):
+        q = _knee_run(he_model, model, sign)
+        ang = np.linalg.norm(q, axis=-1)
+        assert ang.max() <= np.pi - 2e-3, ang.max()  # the 0.02 guard less the linearised row's overshoot (~0.01)
+        assert (ang[-10:] > np.pi - 0.05).all()  # driven onto the limit and held there
+        assert (sign * q[5:, :, :, 1] > 0).all()  # no wrap through pi
+
+
+def test_knee_without_limits_wraps(he_model, model):
+    """The failure the limits prevent: the +5 rad target drives the knee through pi; its exp-map
+    coordinate wraps to ~ -pi (the error to the target grows to ~8 rad) and the knee spins."""
+    q = _knee_run(he_model, model, 1.0, joint_limits=0)
+    assert (q[..., 1] < -2.0).any()
+
+
+def test_limit_rows_keep_every_dof_in_range(he_model, model):
+    """Random saturating actions (targets = the PD scale x U(-1, 1) clipped, as in early training)
+    on a standing humanoid: every dof stays within its range."""
+    from humanoid_amd.model import pd_action_offset_scale
+    rng = np.random.default_rng(8)
+    n = 8
+    off, sc = pd_action_offset_scale(model)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    sp = _abi.default_sim_params()
+    cache = O.new_cache(n)
+    lo = np.array([he_model.dof_lower[k] for k in range(69)], np.float32)
+    hi = np.array([he_model.dof_upper[k] for k in range(69)], np.float32)
+    for step in range(30):
+        a = rng.uniform(-1.0, 1.0, (n, 69)).astype(np.float32)
+        tgt = (off + sc * a).astype(np.float32)
+        O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache)
+        q = dof[..., 0]
+        assert (q <= hi + 1e-3).all() and (q >= lo - 1e-3).all(), step
+
+
+def test_overflow_is_counted_and_keeps_the_deepest(he_model, model):
+    """Lying bodies generate up to ~30 contacts. At the engine's 20 slots the overflow is reported
+    per env, and the deepest-first reduction keeps the settled penetration at the level of a run
+    with 64 slots (round 1's body-order truncation let the right hand sink 3.6 cm). cases.lying_state
+    starts up to 0.43 m inside the plane, so the bodies are thrown out at up to 10 m/s and tumble for
+    ~1.5 s (transient penetration ~2-3 cm with either capacity); they rest by 4 s."""
+    rng = np.random.default_rng(5)
+    root, dof = cases.lying_state(16, rng)
+    targets = np.zeros((16, 69), np.float32)
+    worst = {}
+    dropped = {}
+    for cap in (20, 64):
+        sp = _abi.default_sim_params(max_contacts=cap)
+        r, d = root.copy(), dof.copy()
+        cache = O.new_cache(16) if cap <= _abi.MAX_CONTACTS else None
+        drops = []
+        for _ in range(120):
+            out = O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
+            drops.append(out["dropped"].copy())
+            assert (out["num_contacts"] <= cap).all()
+        worst[cap] = cases.ground_gaps(model, out["rb_state"]).min()
+        dropped[cap] = np.array(drops)
+        assert np.abs(r[:, 7:]).max() < 0.5  # at rest
+    assert dropped[20][-1].sum() > 0 and dropped[64].max() == 0
+    assert worst[20] > -2e-3 and worst[64] > -2e-3, worst
+
+
+def test_warm_start_converges_on_lying_bodies(he_model):
+    """the solve's complementarity residual on cases.lying_state after the bodies
+    settle (steps 30-60) drops >= 5x with the warm start at the same 8 iterations."""
+    rng = np.random.default_rng(3)
+    n = 32
+    root, dof = cases.lying_state(n, rng)
+    targets = np.zeros((n, 69), np.float32)
+    res = {}
+    for ws in (0, 1):
+        sp = _abi.default_sim_params(warm_start=ws)
+        r, d = root.copy(), dof.copy()
+        cache = O.new_cache(n)
+        rr = []
+        for step in range(60):
+            out = O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
+            if step >= 30:
+                rr.append(np.median(out["residual"]))
+        res[ws] = float(np.mean(rr))
+    assert res[1] * 5 < res[0], res
+
+
+def test_cache_signature_invalidates_on_external_write(he_model, model):
+    """A state written from outside (a reset) invalidates the env's cache: the next solve is cold."""
+    rng = np.random.default_rng(9)
+    root, dof = cases.standing_state(model, 2, rng)
+    targets = np.zeros((2, 69), np.float32)
+    sp = _abi.default_sim_params()
+    cache = O.new_cache(2)
+    r, d = root.copy(), dof.copy()
+    for _ in range(3):
+        O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
+    assert cache[:, 7].view(np.int32).tolist() == [16, 16]
+    np.testing.assert_array_equal(cache[:, :3], r[:, :3])
+    # env 1 is "reset" to its start state: the warm and cold steps of it agree exactly
+    r2, d2 = r.copy(), d.copy()
+    r2[1], d2[1] = root[1], dof[1]
+    c_warm = cache.copy()
+    O.physics_step(he_model, sp, r2, d2, targets, 2, cache=c_warm)
+    r3, d3 = r.copy(), d.copy()
+    r3[1], d3[1] = root[1], dof[1]
+    O.physics_step(he_model, sp, r3, d3, targets, 2, cache=O.new_cache(2))
+    np.testing.assert_array_equal(r2[1], r3[1])
+    np.testing.assert_array_equal(d2[1], d3[1])

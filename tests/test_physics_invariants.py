@@ -1,0 +1,194 @@
+"""Physics pin: invariants of the fp64 CPU oracle (``oracle/he_oracle_physics.c``).
+
+PhysX / Isaac Gym is closed and absent, so no reference fixture pins the articulated
+step. These tests pin the oracle against physics itself instead:
+* free fall from rest with the drives off: the body stays rigid and the root follows the discrete
+  semi-implicit parabola exactly;
+* free flight: linear momentum changes by M g t, angular momentum about the centre of mass and the
+  kinetic energy (gravity off) are conserved up to the integrator's first-order drift, and that drift
+  halves when dt halves;
+* the centre of mass of a tumbling, actuated body follows the ballistic parabola (internal drive
+  torques cannot move it);
+* dt refinement: a random actuated airborne trajectory converges at first order (error ratio ~3
+  between dt, dt/2 against dt/4);
+* PD stand-still: the zero-pose humanoid on the plane settles and stays put;
+* penetration: standing and lying bodies settle with every contact candidate within the
+  Baumgarte steady state, far inside contact_offset (0.02 m).
+The GPU engine is then held to this oracle (tests/test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+
+from humanoid_amd import _abi
+from oracle import oracle as O
+
+import cases
+
+G = 9.81
+
+
+def _run(he_model, root, dof, targets, steps, substeps=2, **sim):
+    sp = _abi.default_sim_params(**sim)
+    r, d = root.copy(), dof.copy()
+    cache = O.new_cache(r.shape[0])
+    out = None
+    for _ in range(steps):
+        out = O.physics_step(he_model, sp, r, d, targets, substeps, cache=cache)
+    return r, d, out, sp
+
+
+def _drives_off(**kw):
+    sim = dict(self_collision=0, kp_scale=0.0, kd_scale=0.0, angular_damping=0.0)
+    sim.update(kw)
+    return sim
+
+
+def _com_velocity(model, he_model, root, dof):
+    me = O.momentum_energy(he_model, _abi.default_sim_params(), root, dof)
+    return me[:, :3] / float(np.sum(model.mass))
+
+
+def test_free_fall_from_rest_is_the_discrete_parabola(he_model, model):
+    """Zero velocities, drives off: no internal force ever acts, every body falls with -g. With the
+    semi-implicit update v_k = -g k dt, z_k = z_0 - g dt^2 k (k+1) / 2 exactly."""
+    rng = np.random.default_rng(0)
+    root, dof = cases.random_state(8, rng, height=(3.0, 4.0), vel=0.0)
+    dof[..., 1] = 0.0
+    n_sub = 40
+    r, d, out, sp = _run(he_model, root, dof, np.zeros((8, 69), np.float32), n_sub // 2, **_drives_off())
+    dt = sp.dt
+    assert (out["num_contacts"] == 0).all()
+    np.testing.assert_allclose(r[:, 2], root[:, 2] - G * dt * dt * n_sub * (n_sub + 1) / 2, atol=2e-5)
+    np.testing.assert_allclose(r[:, 9], -G * dt * n_sub, atol=2e-5)
+    np.testing.assert_allclose(r[:, :2], root[:, :2], atol=1e-6)
+    np.testing.assert_allclose(r[:, 3:7], root[:, 3:7], atol=1e-6)
+    np.testing.assert_allclose(d[..., 0], dof[..., 0], atol=1e-6)
+    np.testing.assert_allclose(d[..., 1], 0.0, atol=1e-6)
+
+
+def _flight_drifts(model, he_model, root, dof, gravity, dt_div, seconds=1.0):
+    sim = _drives_off(gravity=gravity, dt=1.0 / 60.0 / dt_div)
+    steps = int(round(30 * seconds * dt_div))
+    n = root.shape[0]
+    sp0 = _abi.default_sim_params(**sim)
+    me0 = O.momentum_energy(he_model, sp0, root, dof)
+    r, d, out, sp = _run(he_model, root, dof, np.zeros((n, 69), np.float32), steps, **sim)
+    assert (out["num_contacts"] == 0).all()
+    me1 = O.momentum_energy(he_model, sp, r, d)
+    arm = np.array([he_model.armature[k] for k in range(69)], np.float64)
+    M = float(np.sum(model.mass))
+    t = steps * 2 * sp.dt
+
+    def l_com(me, rr, dd):  # angular momentum about the centre of mass: L_0 - c x P
+        c = cases.center_of_mass(model, O.forward_kinematics(he_model, rr, dd))
+        return me[:, 3:6] - np.cross(c, me[:, :3])
+
+    g = np.asarray(gravity, np.float64)
+    dP = np.abs(me1[:, :3] - (me0[:, :3] + M * g * t)).max()
+    dL = np.abs(l_com(me1, r, d) - l_com(me0, root, dof)).max()
+    ke0 = me0[:, 6] + 0.5 * (arm * dof[..., 1].astype(np.float64) ** 2).sum(-1)
+    ke1 = me1[:, 6] + 0.5 * (arm * d[..., 1].astype(np.float64) ** 2).sum(-1)
+    dE = np.abs(ke1 / ke0 - 1.0).max()
+    return dP, dL, dE, np.abs(me0[:, :3]).max(), np.abs(l_com(me0, root, dof)).max()
+
+
+def test_free_flight_momentum_and_energy(he_model, model):
+    """Drives off, no damping, no contact. Linear momentum P(t) = P0 + M g t, angular momentum about
+    the CoM and (gravity off) kinetic energy incl. the armature term are conserved by the continuous
+    dynamics; the semi-implicit integrator drifts at first order: small at 1/60 s and halving with dt."""
+    rng = np.random.default_rng(1)
+    root, dof = cases.random_state(8, rng, height=(3.0, 4.0), vel=0.5, ang=0.5)
+    res = {k: _flight_drifts(model, he_model, root, dof, (0.0, 0.0, 0.0), k) for k in (1, 2)}
+    dP1, dL1, dE1, P, L = res[1]
+    dP2, dL2, dE2, _, _ = res[2]
+    # 1 s of flight at the engine's dt (joint speeds ~0.5 rad/s): measured 1.5% of |P|, 5% of |L_com|,
+    # 6% of the energy; bounded at twice that, the first-order ratio below is the real check
+    assert dP1 < 0.03 * P and dL1 < 0.1 * L and dE1 < 0.12, res[1]
+    for a, b in ((dP1, dP2), (dL1, dL2), (dE1, dE2)):
+        assert 0.35 < b / a < 0.65, (a, b)  # first order in dt
+    # with gravity: the same drifts, P gains exactly M g t up to them
+    high = root.copy()
+    high[:, 2] += 6.0  # 1 s of fall (4.9 m) stays airborne
+    dPg, dLg, _, _, _ = _flight_drifts(model, he_model, high, dof, (0.0, 0.0, -G), 1)
+    assert dPg < 0.03 * P and dLg < 0.1 * L
+
+
+def test_com_follows_ballistic_parabola_under_drives(he_model, model):
+    """Actuated tumbling in the air (PD drives on, random targets): the internal torques cannot move
+    the centre of mass, which follows c0 + v0 t - g t^2/2 up to the integrator's O(dt) drift."""
+    rng = np.random.default_rng(2)
+    n = 8
+    root, dof = cases.random_state(n, rng, height=(4.0, 5.0), vel=0.5, ang=0.5)
+    targets = rng.uniform(-1.0, 1.0, (n, 69)).astype(np.float32)
+    c0 = cases.center_of_mass(model, O.forward_kinematics(he_model, root, dof))
+    v0 = _com_velocity(model, he_model, root, dof)
+    errs = []
+    for div in (1, 2):
+        steps = 15 * div
+        r, d, out, sp = _run(he_model, root, dof, targets, steps, self_collision=0, angular_damping=0.0,
+                             dt=1.0 / 60.0 / div)
+        assert (out["num_contacts"] == 0).all()
+        t = steps * 2 * sp.dt
+        c = cases.center_of_mass(model, out["rb_state"])
+        expect = c0 + v0 * t + 0.5 * np.array([0.0, 0.0, -G]) * t * t
+        errs.append(np.abs(c - expect).max())
+    assert errs[0] < 0.15, errs  # measured 0.08 m after 0.5 s of stiff PD tumbling at 1/60 s
+    assert 0.3 < errs[1] / errs[0] < 0.7, errs
+
+
+def test_dt_refinement_converges_first_order(he_model):
+    """Random actuated airborne state for 0.5 s at dt, dt/2, dt/4: |x(dt) - x(dt/4)| / |x(dt/2) -
+    x(dt/4)| is 3 for a first-order method (joint angles and root position)."""
+    rng = np.random.default_rng(3)
+    n = 8
+    root, dof = cases.random_state(n, rng, height=(3.0, 4.0), vel=0.5, ang=0.4)
+    targets = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+    res = {}
+    for div in (1, 2, 4):
+        r, d, _, _ = _run(he_model, root, dof, targets, 15 * div, self_collision=0, dt=1.0 / 60.0 / div)
+        res[div] = np.concatenate([r[:, :3], d[..., 0]], axis=1).astype(np.float64)
+    e1 = np.linalg.norm(res[1] - res[4], axis=1)
+    e2 = np.linalg.norm(res[2] - res[4], axis=1)
+    ratio = e1 / e2
+    assert (ratio > 2.0).all() and (ratio < 4.5).all(), ratio
+    assert e1.max() < 0.05, e1
+
+
+def test_pd_stand_still_equilibrium(he_model, model):
+    """Zero-pose PD targets on the plane (configs[1]): the humanoid sways in a damped mode for ~5 s
+    (the root moves ~3 cm and sinks ~3 mm: knees give under the PD gains, feet rest ~1.4 mm deep
+    under Baumgarte), then stands exactly still -- 5 s more without drift, every velocity ~0, the
+    warm-started solve converged and the four corners of each foot / toe box in contact throughout."""
+    rng = np.random.default_rng(4)
+    n = 8
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    targets = np.zeros((n, 69), np.float32)
+    sp = _abi.default_sim_params()
+    r, d = root.copy(), dof.copy()
+    cache = O.new_cache(n)
+    ncs = []
+    for _ in range(300):
+        out = O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
+        ncs.append(out["num_contacts"].copy())
+    r1 = r.copy()
+    for _ in range(150):
+        out = O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
+        ncs.append(out["num_contacts"].copy())
+    assert np.abs(r[:, :2] - root[:, :2]).max() < 0.05 and np.abs(r[:, 2] - root[:, 2]).max() < 5e-3
+    assert np.abs(r[:, :3] - r1[:, :3]).max() < 2e-4  # still: < 0.2 mm over the last 5 s
+    assert np.abs(r[:, 7:]).max() < 1e-4 and np.abs(d[..., 1]).max() < 1e-4
+    assert np.abs(d[..., 0]).max() < 0.05
+    assert out["residual"].max() < 1e-5
+    assert (np.array(ncs) == 16).all()
+
+
+def test_penetration_within_contact_offset(he_model, model):
+    """Standing and lying bodies settle with every terrain candidate above -5 mm (the Baumgarte
+    steady state under gravity is ~ -g dt^2 / 0.2 = -1.4 mm), far inside contact_offset = 0.02 m."""
+    rng = np.random.default_rng(5)
+    targets = np.zeros((8, 69), np.float32)
+    for root, dof in (cases.standing_state(model, 8, rng, xy_jitter=1.0), cases.lying_state(8, rng)):
+        r, d, out, sp = _run(he_model, root, dof, targets, 60)
+        gaps = cases.ground_gaps(model, out["rb_state"])
+        assert gaps.min() > -5e-3, gaps.min()
+        assert gaps.min() < sp.contact_offset  # bodies rest on the plane
