@@ -6,6 +6,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -60,6 +61,9 @@ struct he_engine {
     int num_envs = 0;
     float *root = nullptr, *dof_state = nullptr, *rb = nullptr, *cf = nullptr, *dof_force = nullptr, *targets = nullptr;
     int32_t* num_contacts = nullptr;
+    int32_t* dropped = nullptr;
+    float* cache = nullptr;
+    bool component_limits = false;  // a dof bound inside (-pi + guard, pi - guard): not implemented
     const float *mass_scale = nullptr, *friction = nullptr;
     const int32_t* terrain_kind = nullptr;
     float *pd_offset = nullptr, *pd_scale = nullptr;
@@ -118,6 +122,11 @@ int he_set_model(he_engine* h, const he_model* model) {
         if (model->parents[b] < 0 || model->parents[b] >= b) return fail("he_set_model: bodies must be in DFS order");
     HE_CHECK(hipSetDevice(h->device));
     h->model = *model;
+    // the kernel holds every joint's rotation angle below pi - 0.02 (the exp-map branch cut); dof
+    // bounds inside that band would need per-component rows (the oracle has them, the kernel not)
+    h->component_limits = false;
+    for (int d = 0; d < HE_NUM_DOF; ++d)
+        if (std::fabs(model->dof_lower[d]) < 3.1215f || std::fabs(model->dof_upper[d]) < 3.1215f) h->component_limits = true;
     PhysTopo topo{};
     he_build_topo(*model, topo);
     if (topo.nnz > HE_NNZ_MAX) return fail("he_set_model: mass-matrix pattern too large (%d)", topo.nnz);
@@ -143,6 +152,8 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     HE_CHECK(dalloc(&h->dof_force, (size_t)N * HE_NUM_DOF));
     HE_CHECK(dalloc(&h->targets, (size_t)N * HE_NUM_DOF));
     HE_CHECK(dalloc(&h->num_contacts, (size_t)N));
+    HE_CHECK(dalloc(&h->dropped, (size_t)N));
+    HE_CHECK(dalloc(&h->cache, (size_t)N * HE_CACHE_WORDS));
     // humanoid_phc.py:340-347: start pose (x, y) + z 0.89, identity rotation, zero velocity
     std::vector<float> root((size_t)N * 13, 0.f);
     for (int e = 0; e < N; ++e) {
@@ -159,6 +170,8 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     HE_CHECK(hipMemset(h->dof_force, 0, (size_t)N * HE_NUM_DOF * sizeof(float)));
     HE_CHECK(hipMemset(h->targets, 0, (size_t)N * HE_NUM_DOF * sizeof(float)));
     HE_CHECK(hipMemset(h->num_contacts, 0, (size_t)N * sizeof(int32_t)));
+    HE_CHECK(hipMemset(h->dropped, 0, (size_t)N * sizeof(int32_t)));
+    HE_CHECK(hipMemset(h->cache, 0, (size_t)N * HE_CACHE_WORDS * sizeof(float)));
     h->num_envs = N;
     return 0;
 }
@@ -167,7 +180,7 @@ int he_destroy(he_engine* h) {
     if (!h) return 0;
     hipSetDevice(h->device);
     void* ptrs[] = {h->d_model, h->d_topo, h->root, h->dof_state, h->rb, h->cf, h->dof_force, h->targets,
-                    h->num_contacts, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
+                    h->num_contacts, h->dropped, h->cache, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
                     h->m_dt, h->m_starts, h->m_nframes};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -188,6 +201,8 @@ int he_get_buffer(he_engine* h, int kind, void** dptr, int64_t* shape, int* ndim
         case HE_BUF_DOF_FORCE: *dptr = h->dof_force; *ndim = 1; shape[0] = N * HE_NUM_DOF; break;
         case HE_BUF_DOF_TARGET: *dptr = h->targets; *ndim = 2; shape[0] = N; shape[1] = HE_NUM_DOF; break;
         case HE_BUF_NUM_CONTACTS: *dptr = h->num_contacts; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
+        case HE_BUF_DROPPED_CONTACTS: *dptr = h->dropped; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
+        case HE_BUF_CONTACT_CACHE: *dptr = h->cache; *ndim = 2; shape[0] = N; shape[1] = HE_CACHE_WORDS; break;
         default: return fail("he_get_buffer: unknown buffer kind %d", kind);
     }
     return 0;
@@ -280,6 +295,8 @@ static PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
     a.contact_forces = h->cf;
     a.dof_force = h->dof_force;
     a.num_contacts = h->num_contacts;
+    a.dropped = h->dropped;
+    a.cache = h->cache;
     a.mass_scale = h->mass_scale;
     a.friction = h->friction;
     a.terrain_kind = h->terrain_kind;
@@ -292,6 +309,8 @@ static PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
 
 int he_simulate(he_engine* h, int substeps, void* stream) {
     if (!h || !h->num_envs) return fail("he_simulate: no envs");
+    if (h->params.joint_limits && h->component_limits)
+        return fail("he_simulate: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
     if (substeps < 1) return fail("he_simulate: substeps must be >= 1");
     HE_CHECK(launch_physics(phys_args(h, substeps, nullptr), (hipStream_t)stream));
     return 0;
@@ -300,6 +319,8 @@ int he_simulate(he_engine* h, int substeps, void* stream) {
 int he_step_actions(he_engine* h, const float* actions, int substeps, void* stream) {
     if (!h || !h->num_envs || !actions) return fail("he_step_actions: bad arguments");
     if (!h->has_pd) return fail("he_step_actions: call he_set_pd_params first");
+    if (h->params.joint_limits && h->component_limits)
+        return fail("he_step_actions: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
     if (substeps < 1) return fail("he_step_actions: substeps must be >= 1");
     HE_CHECK(launch_physics(phys_args(h, substeps, actions), (hipStream_t)stream));
     return 0;

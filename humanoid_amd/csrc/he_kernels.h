@@ -93,6 +93,8 @@ struct PhysArgs {
     float* contact_forces;
     float* dof_force;
     int32_t* num_contacts;
+    int32_t* dropped;            // [N] contacts generated past the capacity (last substep) or null
+    float* cache;                // [N,HE_CACHE_WORDS] warm-start cache or null
     const float* mass_scale;     // [N,24] or null
     const float* friction;       // [N] or null
     const int32_t* terrain_kind; // [N] or null

@@ -64,12 +64,17 @@ struct Lds {
                                              // order); Lp[kNpack] is the elimination's store sink
     float cx[MAXC][3], cn[MAXC][3], ct1[MAXC][3], ct2[MAXC][3], cgap[MAXC], cmu[MAXC];
     int cb0[MAXC], cb1[MAXC];
-    float lam[W];
+    float lam[W];  // impulses of the last solve (lane = row): the warm-start cache and the forces
     float cf[NB][3];
     float dforce[ND];
     float root_pos[3], root_q[4];
     float qloc[NB][4];  // each joint's local rotation exp(q_b), from the kinematics (reused by integrate)
-    int nc, nterr;                 // contacts, of which terrain (slots [0, nterr), grouped by body)
+    int nc, nterr;                 // contact slots, of which limits + terrain (slots [0, nterr))
+    int nlim;                      // joint-limit slots [0, nlim)
+    int ncand;                     // contacts generated (dropped = ncand - nc), last substep
+    int ckey[MAXC];                // warm-start key of each slot (he_sim_params cache layout)
+    int wckey[MAXC];               // the previous solve's keys (its impulses: lam)
+    int nwc;                       // slots cached in wckey / lam
     int8_t tbase[NB], tcnt[NB];    // body b's terrain contacts: slots tbase[b] .. + tcnt[b]
     float4 bsph[NB];               // per-body bounding sphere of the collision segment (cull)
     BodyTopo T;
@@ -189,6 +194,21 @@ HE_DEV f3 pqlog(f4 q) {
     if (s < 1e-8f) return f3{2.f * q.x, 2.f * q.y, 2.f * q.z};
     const float k = 2.f * atan2f(s, q.w) * __builtin_amdgcn_rcpf(s);
     return f3{q.x * k, q.y * k, q.z * k};
+}
+
+// Joint-angle limit of joint b (oracle/he_oracle_physics.c angle_row): the exp-map coordinate
+// wraps at |q_b| = pi, so the MJCF's +-180 / +-720 deg ranges hold the rotation angle at
+// pi - kLimitGuard; the speculative row is emitted within limit_margin + dt * (closing rate).
+constexpr float kLimitGuard = 0.02f;
+HE_DEV bool angle_row(const Lds& L, int b, const he_sim_params& p, float& gap, f3& dir) {
+    const int d = 3 * (b - 1);
+    const f3 th = f3{L.q[d], L.q[d + 1], L.q[d + 2]};
+    const f3 u = f3{L.u0[6 + d], L.u0[7 + d], L.u0[8 + d]};
+    const float t = norm3(th);
+    dir = th * (1.0f / fmaxf(t, 1e-30f));
+    gap = (3.14159265358979f - kLimitGuard) - t;
+    const float closing = dot3(dir, u);
+    return t >= 1e-6f && gap < p.limit_margin + p.dt * fmaxf(closing, 0.f);
 }
 
 // terrain constants of the env, read once per contact phase (slope normal, step field)
@@ -1185,9 +1205,13 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // effort limit: the implicit step's drive torque, estimated with the dof's own joint-space
         // inertia H_ii = S_i . IS_i (+ armature) as tau - c dt (tau - bias) / (H_ii + dt c), scales
         // the whole drive down to the limit (oracle/he_oracle_physics.c, the drive block)
+        // A joint held at its angle limit cannot give way: its check takes the torque at rest.
         const float c = dt * kp + kd;
         const float hii = dot6(L.S[i], L.IS[i]) + m.armature[d];
-        const float tau_i = tau - c * dt * (tau - bias) / (hii + dt * c);
+        float lgap;
+        f3 ldir;
+        const bool blocked = p.joint_limits && jd && angle_row(L, b > 0 ? b : 1, p, lgap, ldir);
+        const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) / (hii + dt * c);
         const float sc = fabsf(tau_i) > lim ? lim / fabsf(tau_i) : 1.f;
         tau *= sc;
         kp *= sc;
@@ -1212,7 +1236,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float tau = kp * (err - dt * u) - kd * u;
             float lim = m.effort[d];
             const float c = dt * kp + kd;
-            const float tau_i = tau - c * dt * (tau - bias) / (dot6(L.S[i], L.IS[i]) + m.armature[d] + dt * c);
+            float lgap;
+            f3 ldir;
+            const bool blocked = p.joint_limits && angle_row(L, b, p, lgap, ldir);
+            const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) / (dot6(L.S[i], L.IS[i]) + m.armature[d] + dt * c);
             if (fabsf(tau_i) > lim) {
                 const float sc = lim / fabsf(tau_i);
                 tau *= sc; kp *= sc; kd *= sc;
@@ -1311,20 +1338,49 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #endif
     sync();
     STAMP(6);
-    // ---- contacts: terrain (bodies in order, box corners deepest-first), then self pairs
+    // ---- contact slots: joint limits, terrain (bodies in order, box corners deepest-first), self
+    // pairs (oracle/he_oracle_physics.c gen_contacts). Every contact generated is counted; when
+    // they exceed the capacity, the limits stay and the contacts are reduced to the deepest ones
+    // (smallest gap, ties in slot order), kept in slot order. The gap of each contact candidate is
+    // recorded in candidate order in the IS scratch (dead after the CRBA) for that reduction.
     const int maxc = p.max_contacts < MAXC ? p.max_contacts : MAXC;
     const float off = p.contact_offset;
     const Terrain ter = terrain_of(p, tkind);
     const bool self_col = p.self_collision;
-    int nc = 0;
-    {
-        // per-body collision geometry (lane = body), one path for every geometry type:
-        //  self segment P0-P1, radius rs: sphere P0 = P1 = centre; capsule from / to; box the
-        //    capsule proxy along its longest axis (radius geom_radius)
-        //  terrain candidates, radius rt: sphere the centre; capsule from, to; box the 8 corners
-        //    around its centre Pc (world centre +- the world half-axes, which are 0 for the others)
-        const int b = lane < NB ? lane : 0;
-        const bool isS = gt == HE_GEOM_SPHERE, isC = gt == HE_GEOM_CAPSULE, isB = !isS && !isC;
+    float* gl = &L.IS[0][0];
+    constexpr int kCand = 128;  // contact candidates considered by the reduction (a lying body: ~30)
+    static_assert(kCand <= NG * 6, "candidate gaps fit the IS scratch");
+    // the previous solve's impulses (lane = row) before the self-pair list reuses L.lam as scratch
+    const float lam_prev = L.lam[lane];
+    // -- joint-angle limit slots (lane = joint b - 1)
+    int nlim = 0, nlim_all = 0;
+    if (p.joint_limits) {
+        float lg = 0.f;
+        f3 ld = f3{0.f, 0.f, 0.f};
+        const bool act = lane < NB - 1 && angle_row(L, lane + 1, p, lg, ld);
+        const int pre = wave_prefix(act, lane, nlim_all);
+        if (act && pre < maxc) {
+            // the row -q^ over the joint's dofs travels in the contact position (unused by a limit)
+            store_contact(L, pre, lane + 1, -2, ld * -1.f, f3{0.f, 0.f, 1.f}, lg, 0.f);
+            L.ckey[pre] = (lane + 1) | (7 << 16);
+        }
+        nlim = nlim_all < maxc ? nlim_all : maxc;
+    }
+    int nc = nlim;
+    int terr_all = 0, self_all = 0;
+    // -- terrain candidates of the lane's body: one path for every geometry type
+    //  self segment P0-P1, radius rs: sphere P0 = P1 = centre; capsule from / to; box the capsule
+    //    proxy along its longest axis (radius geom_radius)
+    //  terrain candidates, radius rt: sphere the centre; capsule from, to; box the 8 corners around
+    //    its centre Pc (world centre +- the world half-axes, which are 0 for the others)
+    const int tb_ = lane < NB ? lane : 0;
+    const bool isS = gt == HE_GEOM_SPHERE, isC = gt == HE_GEOM_CAPSULE, isB = !isS && !isC;
+    float cd[8];
+    f3 cxs[8], cns[8];
+    bool cand[8];
+    int rank[8];
+    int myn = 0, base = 0;
+    auto terrain_candidates = [&]() {
         const f4 bq = isB ? f4{gv[6], gv[7], gv[8], gv[9]} : f4{0.f, 0.f, 0.f, 1.f};
         int ax = 0;
         float emax = gv[3];
@@ -1335,8 +1391,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // mat-vecs instead of ten quaternion applications
         f3 bc0, bc1, bc2, wc0, wc1, wc2;
         qcols(bq, bc0, bc1, bc2);
-        qcols(f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]}, wc0, wc1, wc2);
-        const f3 pwb = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]};
+        qcols(f4{L.qw[tb_][0], L.qw[tb_][1], L.qw[tb_][2], L.qw[tb_][3]}, wc0, wc1, wc2);
+        const f3 pwb = f3{L.pw[tb_][0], L.pw[tb_][1], L.pw[tb_][2]};
         const f3 dir = (ax == 0 ? bc0 : (ax == 1 ? bc1 : bc2)) * half;
         const f3 ctr = f3{gv[0], gv[1], gv[2]};
         const f3 l0 = isB ? ctr - dir : ctr;
@@ -1358,9 +1414,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const f3 ez = rot(bc2 * (isB ? gv[5] : 0.f));
         const f3 base0 = isB ? Pc : P0;
         const int ncand = lane < NB ? (isS ? 1 : (isC ? 2 : 8)) : 0;
-        float cd[8];
-        f3 cxs[8], cns[8];
-        bool cand[8];
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci) {
             const f3 bs = (ci == 1 && isC) ? P1 : base0;
@@ -1369,12 +1422,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             cxs[ci] = x - cns[ci] * rt;
             cand[ci] = ci < ncand && cd[ci] < off;
         }
-        STAMP(14);
         // rank among this body's candidates: box corners by depth, ties (and sphere / capsule end
         // points, keyed 0) by index; non-candidates keyed +inf never go first. With rank[k]
         // starting at k, one comparison per unordered pair i < j moves both ranks:
         // rank[k] = #{i < k : key_i <= key_k} + #{j > k : key_j < key_k} (vector ops only)
-        int rank[8];
         float key[8];
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci) { rank[ci] = ci; key[ci] = cand[ci] ? (isB ? cd[ci] : 0.f) : __builtin_inff(); }
@@ -1386,58 +1437,77 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 rank[ci] += c;
                 rank[cj] -= c;
             }
-        int myn = 0;
+        myn = 0;
 #pragma unroll
         for (int ci = 0; ci < 8; ++ci)
             if (cand[ci] && rank[ci] < 4) ++myn;
         // exclusive prefix of myn (0..4) over the lanes: three bit ballots, v_mbcnt per bit
-        int base = 0, total = 0;
+        base = 0;
+        int total = 0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const uint64_t bm = __ballot((myn >> k) & 1);
             base += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << k;
             total += __popcll(bm) << k;
         }
+        return total;
+    };
+    {
+        terr_all = terrain_candidates();
         STAMP(16);
+        // candidate k = base + rank (in slot order): its gap for the reduction, its slot nlim + k
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci)
-            if (cand[ci] && rank[ci] < 4 && base + rank[ci] < maxc)
-                store_contact(L, base + rank[ci], b, -1, cxs[ci], cns[ci], cd[ci], mu);
-        nc = total < maxc ? total : maxc;
+        for (int ci = 0; ci < 8; ++ci) {
+            if (cand[ci] && rank[ci] < 4) {
+                const int k = base + rank[ci];
+                if (k < kCand) gl[k] = cd[ci];
+                if (nlim + k < maxc) {
+                    store_contact(L, nlim + k, tb_, -1, cxs[ci], cns[ci], cd[ci], mu);
+                    L.ckey[nlim + k] = tb_ | (1 << 8) | (ci << 16);
+                }
+            }
+        }
+        nc = nlim + terr_all < maxc ? nlim + terr_all : maxc;
         if (lane < NB) {  // the body's slot range, for the per-body force sums
-            L.tbase[lane] = (int8_t)(base < maxc ? base : maxc);
-            L.tcnt[lane] = (int8_t)(base + myn < maxc ? myn : (base < maxc ? maxc - base : 0));
+            const int s0 = nlim + base;
+            L.tbase[lane] = (int8_t)(s0 < maxc ? s0 : maxc);
+            L.tcnt[lane] = (int8_t)(s0 + myn < maxc ? myn : (s0 < maxc ? maxc - s0 : 0));
         }
         if (lane == 0) L.nterr = nc;
     }
     STAMP(17);
-    if (self_col && nc < maxc) {
+    // -- self pairs: broad phase (bounding spheres, survivors compacted in pair order into the lam
+    // scratch), narrow phase W survivors per pass; `visit(hit, i, j, x, n, gap, k)` gets every hit
+    // with its candidate index k (in pair order after the terrain candidates)
+    auto self_pairs = [&](auto visit) {
         sync();
-        STAMP(18);
-        // broad phase: a pair whose bounding spheres (segment midpoint, half length + radius) are
-        // apart by more than the contact offset plus a 1 mm guard cannot reach gap < offset; the
-        // survivors are compacted in pair order into the lam scratch (dead until the solver)
         int* list = reinterpret_cast<int*>(L.lam);
-        int nsurv = 0;
+        auto compact = [&](int skip) {  // survivors skip .. skip + W - 1 into the list
+            int k = 0;
 #pragma unroll
-        for (int rd = 0; rd < ROUNDS; ++rd) {
-            const int i = prs[rd].x, j = prs[rd].y;
-            bool need = false;
-            if (i >= 0) {
-                const float4 bi = L.bsph[i], bj = L.bsph[j];
-                const f3 d = f3{bi.x - bj.x, bi.y - bj.y, bi.z - bj.z};
-                const float lim = bi.w + bj.w + off + 1e-3f;
-                need = dot3(d, d) < lim * lim;
+            for (int rd = 0; rd < ROUNDS; ++rd) {
+                const int i = prs[rd].x, j = prs[rd].y;
+                bool need = false;
+                if (i >= 0) {
+                    const float4 bi = L.bsph[i], bj = L.bsph[j];
+                    const f3 d = f3{bi.x - bj.x, bi.y - bj.y, bi.z - bj.z};
+                    const float lim = bi.w + bj.w + off + 1e-3f;
+                    need = dot3(d, d) < lim * lim;
+                }
+                const uint64_t bm = __ballot(need);
+                const int slot = k + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) - skip;
+                if (need && slot >= 0 && slot < W) list[slot] = (rd * W + lane) | (i << 16) | (j << 24);
+                k += __popcll(bm);
             }
-            const uint64_t bm = __ballot(need);
-            const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-            if (need && slot < W) list[slot] = (rd * W + lane) | (i << 16) | (j << 24);
-            nsurv += __popcll(bm);
-        }
-        sync();
+            sync();
+            return k;
+        };
+        // broad phase: a pair whose bounding spheres (segment midpoint, half length + radius) are
+        // apart by more than the contact offset plus a 1 mm guard cannot reach gap < offset
+        const int nsurv = compact(0);
         STAMP(19);
-        // narrow phase on the survivors, W per pass, in pair order
-        for (int s0 = 0; s0 < nsurv && nc < maxc; s0 += W) {
+        int nhit = 0;
+        for (int s0 = 0; s0 < nsurv; s0 += W) {
             bool hit = false;
             f3 px = f3{0.f, 0.f, 0.f}, pn = f3{0.f, 0.f, 0.f};
             float pgap = 0.f;
@@ -1462,32 +1532,81 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             }
             int total;
             const int pre = wave_prefix(hit, lane, total);
-            if (hit && nc + pre < maxc) store_contact(L, nc + pre, i, j, px, pn, pgap, mu);
-            nc = nc + total < maxc ? nc + total : maxc;
-            if (s0 + W < nsurv) {  // more than W survivors: compact the next pass (rare)
-                sync();
-                // recompute the next W survivors into the list
-                int k = 0;
-                for (int rd = 0; rd < ROUNDS; ++rd) {
-                    const int ii = prs[rd].x, jj = prs[rd].y;
-                    bool need = false;
-                    if (ii >= 0) {
-                        const float4 bi = L.bsph[ii], bj = L.bsph[jj];
-                        const f3 d = f3{bi.x - bj.x, bi.y - bj.y, bi.z - bj.z};
-                        const float lim = bi.w + bj.w + off + 1e-3f;
-                        need = dot3(d, d) < lim * lim;
-                    }
-                    const uint64_t bm = __ballot(need);
-                    const int slot = k + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) - (s0 + W);
-                    if (need && slot >= 0 && slot < W) list[slot] = (rd * W + lane) | (ii << 16) | (jj << 24);
-                    k += __popcll(bm);
+            visit(hit, i, j, px, pn, pgap, terr_all + nhit + pre);
+            nhit += total;
+            if (s0 + W < nsurv) compact(s0 + W);  // more than W survivors: the next pass (rare)
+        }
+        return nhit;
+    };
+    if (self_col) {
+        self_all = self_pairs([&](bool hit, int i, int j, f3 px, f3 pn, float pgap, int k) {
+            if (hit && k < kCand) gl[k] = pgap;
+            if (hit && nlim + k < maxc) {
+                store_contact(L, nlim + k, i, j, px, pn, pgap, mu);
+                L.ckey[nlim + k] = i | ((j + 2) << 8);
+            }
+        });
+        nc = nlim + terr_all + self_all < maxc ? nlim + terr_all + self_all : maxc;
+    }
+    const int ncand_all = nlim_all + terr_all + self_all;
+    if (nlim + terr_all + self_all > maxc && nlim < maxc) {
+        // ---- overflow (rare, wave-uniform): keep the `keep` deepest contacts, in slot order
+        sync();
+        const int keep = maxc - nlim;
+        const int T = terr_all + self_all < kCand ? terr_all + self_all : kCand;
+        uint64_t km[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int k = h * W + lane;
+            bool kept = false;
+            if (k < T) {
+                const float gk = gl[k];
+                int r = 0;
+                for (int jj = 0; jj < T; ++jj) {  // uniform LDS reads (broadcast)
+                    const float g2 = gl[jj];
+                    r += (g2 < gk || (g2 == gk && jj < k)) ? 1 : 0;
                 }
-                sync();
+                kept = r < keep;
+            }
+            km[h] = __ballot(kept);
+        }
+        auto before = [&](int k) {  // kept candidates below index k
+            const uint64_t lo = k >= W ? km[0] : (k <= 0 ? 0ull : km[0] & ((~0ull) >> (W - k)));
+            const uint64_t hi = k <= W ? 0ull : (k >= 2 * W ? km[1] : km[1] & ((~0ull) >> (2 * W - k)));
+            return __popcll(lo) + __popcll(hi);
+        };
+        auto is_kept = [&](int k) { return k < 2 * W && ((km[k >= W ? 1 : 0] >> (k & (W - 1))) & 1ull); };
+        terrain_candidates();
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) {
+            if (cand[ci] && rank[ci] < 4) {
+                const int k = base + rank[ci];
+                if (is_kept(k)) {
+                    const int slot = nlim + before(k);
+                    store_contact(L, slot, tb_, -1, cxs[ci], cns[ci], cd[ci], mu);
+                    L.ckey[slot] = tb_ | (1 << 8) | (ci << 16);
+                }
             }
         }
+        if (lane < NB) {
+            const int s0 = nlim + before(base);
+            L.tbase[lane] = (int8_t)s0;
+            L.tcnt[lane] = (int8_t)(nlim + before(base + myn) - s0);
+        }
+        if (lane == 0) L.nterr = nlim + before(terr_all);
+        if (self_col) {
+            self_pairs([&](bool hit, int i, int j, f3 px, f3 pn, float pgap, int k) {
+                if (hit && is_kept(k)) {
+                    const int slot = nlim + before(k);
+                    store_contact(L, slot, i, j, px, pn, pgap, mu);
+                    L.ckey[slot] = i | ((j + 2) << 8);
+                }
+            });
+        }
+        nc = nlim + before(T);
     }
     STAMP(15);
-    if (lane == 0) L.nc = nc;
+    if (lane == 0) { L.nc = nc; L.nlim = nlim; L.ncand = ncand_all; }
     if (lane < NB) { L.cf[lane][0] = 0.f; L.cf[lane][1] = 0.f; L.cf[lane][2] = 0.f; }
     sync();
     if (lane < nc) {  // tangent basis of every contact at once (lane = contact)
@@ -1504,6 +1623,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // Delassus operator A = Zh Zh^T is a plain Gram matrix of the lanes' registers
         const int nr = 3 * nc;
         float brow = 0.f, diag = 0.f, lamv = 0.f;
+        float lam0 = 0.f;  // warm start: the previous solve's impulse of this row's contact key
         float acol[MAXR];  // lane c: A[r][c]
         regla::ZVec z;     // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
         {
@@ -1521,6 +1641,19 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
 #if HE_JT_MFMA
             zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane, nr <= 32);
+            // joint-limit slots: the normal row is the stored row over the joint's three dofs (its
+            // support is the joint's ancestor chain, anc0), the two friction rows are zero
+            const bool limrow = lane < nr && L.cb1[ci] == -2;
+            if (__ballot(limrow)) {  // wave-uniform
+                const int bl = limrow ? L.cb0[ci] : 0;
+                const float g3[3] = {kind == 0 ? L.cx[ci][0] : 0.f, kind == 0 ? L.cx[ci][1] : 0.f,
+                                     kind == 0 ? L.cx[ci][2] : 0.f};
+#pragma unroll
+                for (int i = 0; i < NG; ++i) {
+                    const float v = i < 6 ? 0.f : (bl == (i < 6 ? 0 : (i - 6) / 3 + 1) ? g3[i < 6 ? 0 : (i - 6) % 3] : 0.f);
+                    ZV(z, i) = limrow ? v : ZV(z, i);
+                }
+            }
 #if HE_ONE_SWEEP && HE_BIAS_FROM_V
             {
                 // J_r u0 = (rho, dd) . (V_b0 - V_b1): the contact bodies' spatial velocities about o
@@ -1539,6 +1672,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), HE_ONE_SWEEP ? L.u0[i] : L.uf[i], bacc[i & 3]);  // J_r u
 #endif
 #else
+#error "joint-limit rows and the warm start are implemented on the MFMA J^T path (HE_JT_MFMA=1)"
             {
                 // root: S = unit axes, so z = sgn0 * (rho, dd)
                 const float s0 = (float)(anc0 & 1u) - (float)(anc1 & 1u);
@@ -1583,6 +1717,16 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
             }
 #endif
+            {  // warm start: find the row's contact key among the previous solve's keys
+                const int nw = __builtin_amdgcn_readfirstlane(L.nwc);
+                if (nw > 0) {
+                    const int key = L.ckey[ci];
+                    int src = -1;
+                    for (int j = 0; j < nw; ++j) src = (src < 0 && L.wckey[j] == key) ? j : src;
+                    const float v = __shfl(lam_prev, src >= 0 ? 3 * src + kind : 0, W);
+                    lam0 = (lane < nr && src >= 0) ? v : 0.f;
+                }
+            }
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
 #pragma unroll
@@ -1600,7 +1744,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
         {
             const float invd = 1.0f / (lane < nr ? diag + 1e-12f : 1.f);
-            float cd = lane < nr ? -brow * invd : 0.f;
+            // residual at the warm start: w = brow + A lambda0 (acol: lane c holds A[r][c] = A[c][r])
+            float w0 = brow;
+            if (__ballot(lam0 != 0.f)) {  // wave-uniform
+#pragma unroll
+                for (int r = 0; r < MAXR; ++r) w0 = fmaf(acol[r], regla::rdlane(lam0, r), w0);
+            }
+            lamv = lam0;
+            float cd = lane < nr ? -w0 * invd : 0.f;
             const float ninvd = -invd;
 #pragma unroll
             for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
@@ -1614,10 +1765,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             }
             __builtin_amdgcn_s_setprio(0);
         }
-        if (last) {  // read only by the reported contact forces
-            L.lam[lane] = lane < nr ? lamv : 0.f;
-            sync();
-        }
+        // the solve's impulses and keys: the next solve's warm start and the reported forces
+        L.lam[lane] = lane < nr ? lamv : 0.f;
+        if (lane < nc) L.wckey[lane] = L.ckey[lane];
+        if (lane == 0) L.nwc = nc;
+        sync();
         STAMP(10);
         // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
         // a wave reduce-scatter sums the 75 columns into lane = dof, then one L^-1 sweep
@@ -1683,8 +1835,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         sync();
         }  // last
     }
+    if (nc == 0) {  // nothing to warm-start the next solve from
+        L.lam[lane] = 0.f;
+        if (lane == 0) L.nwc = 0;
+    }
 #if HE_ONE_SWEEP
-    else {  // no contact: uf = u0 + L^-1 D^-1/2 yh
+    if (nc == 0) {  // no contact: uf = u0 + L^-1 D^-1/2 yh
         float yl = L.yh[lane] * L.sDinv[lane];
         float y2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
@@ -1777,6 +1933,25 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         }
         L.tgt[d] = t;
     }
+    // ---- warm-start cache (include/humanoid_engine.h HE_CACHE_WORDS): valid while the root pose
+    // still equals the signature the previous step wrote (an external write -- a reset -- breaks it)
+    {
+        const float* cw = a.cache ? a.cache + (size_t)e * HE_CACHE_WORDS : nullptr;
+        const float w1 = cw ? cw[lane] : 0.f;
+        const float w2 = cw && lane < HE_CACHE_WORDS - W ? cw[W + (lane < HE_CACHE_WORDS - W ? lane : 0)] : 0.f;
+        const float sig = lane < 3 ? rs[lane] : (lane < 7 ? rs[lane < 7 ? lane : 0] : 0.f);
+        const bool diff = lane < 7 && __float_as_uint(w1) != __float_as_uint(sig);
+        const bool valid = cw && a.p.warm_start && __ballot(diff) == 0ull;
+        const int nw = valid ? __builtin_amdgcn_readlane(__float_as_int(w1), 7) : 0;
+        const int nwc = nw < 0 ? 0 : (nw > MAXC ? MAXC : nw);
+        if (lane >= HE_CACHE_KEYS && lane < HE_CACHE_KEYS + MAXC) L.wckey[lane - HE_CACHE_KEYS] = __float_as_int(w1);
+        // impulses: words 32..63 from the first read, 64..94 from the second
+        if (lane >= HE_CACHE_LAMBDA) L.lam[lane - HE_CACHE_LAMBDA] = valid ? w1 : 0.f;
+        if (lane < W - HE_CACHE_LAMBDA) L.lam[W - HE_CACHE_LAMBDA + lane] = valid ? w2 : 0.f;
+        if (lane == 0) L.nwc = nwc;
+    }
+    static_assert(HE_CACHE_LAMBDA + 3 * MAXC <= HE_CACHE_WORDS && HE_CACHE_KEYS + MAXC <= HE_CACHE_LAMBDA &&
+                  HE_CACHE_WORDS <= 2 * W, "cache layout");
     sync();
     const float* ms = a.mass_scale ? a.mass_scale + (size_t)e * NB : nullptr;
     float mu = a.friction ? a.friction[e] : a.p.friction;
@@ -1810,6 +1985,23 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     }
     for (int t = lane; t < NB * 3; t += W) a.contact_forces[(size_t)e * NB * 3 + t] = L.cf[t / 3][t % 3];
     if (lane == 0 && a.num_contacts) a.num_contacts[e] = L.nc;
+    if (lane == 0 && a.dropped) a.dropped[e] = L.ncand - L.nc;
+    if (a.cache) {  // signature (the root pose just written), slot count, keys, impulses
+        float* cw = a.cache + (size_t)e * HE_CACHE_WORDS;
+        const int nwc = a.p.warm_start ? L.nwc : 0;
+        float v = 0.f;
+        if (lane < 3) v = L.root_pos[lane];
+        else if (lane < 7) v = L.root_q[lane < 7 ? lane - 3 : 0];
+        else if (lane == 7) v = __int_as_float(nwc);
+        else if (lane < HE_CACHE_KEYS + MAXC) v = lane - HE_CACHE_KEYS < nwc ? __int_as_float(L.wckey[lane - HE_CACHE_KEYS]) : 0.f;
+        else if (lane >= HE_CACHE_LAMBDA) v = lane - HE_CACHE_LAMBDA < 3 * nwc ? L.lam[lane - HE_CACHE_LAMBDA] : 0.f;
+        if (!a.p.warm_start) v = 0.f;
+        cw[lane] = v;
+        if (lane < HE_CACHE_WORDS - W) {
+            const int r = W - HE_CACHE_LAMBDA + lane;
+            cw[W + lane] = a.p.warm_start && r < 3 * nwc ? L.lam[r] : 0.f;
+        }
+    }
 }
 
 }  // namespace

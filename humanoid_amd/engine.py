@@ -196,7 +196,18 @@ class Engine:
 
     @property
     def num_contacts(self):
+        """i32 [N]: contact slots (joint limits included) used by the last substep."""
         return self.buffer(_abi.BUF_NUM_CONTACTS)
+
+    @property
+    def dropped_contacts(self):
+        """i32 [N]: contacts generated past the capacity in the last substep (the deepest kept)."""
+        return self.buffer(_abi.BUF_DROPPED_CONTACTS)
+
+    @property
+    def contact_cache(self):
+        """f32 [N, HE_CACHE_WORDS]: the solver's warm-start cache (signature, keys, impulses)."""
+        return self.buffer(_abi.BUF_CONTACT_CACHE)
 
     # ------------------------------------------------------------------ state writes
     def _contig(self, t, dtype=None):

@@ -36,7 +36,11 @@ def random_state(n, rng, height=(0.9, 1.6), ang=0.6, vel=1.0, tilt=0.3):
     return root, dof
 
 
-def lying_state(n, rng):
+def lying_state(n, rng, on_floor=False, model=None):
+    """A body lying on its back/front (pi/2 about x) with random joint angles in +-0.2 rad. By default
+    the root sits at 0.12-0.15 m, so limbs start up to ~0.4 m inside the plane and are thrown out
+    (a violent, tumbling transient); with on_floor=True each body is lifted so its lowest contact
+    candidate is 5 mm above the plane (a fallen body at rest: ~20-30 contacts)."""
     root = np.zeros((n, 13), np.float32)
     th = np.pi / 2
     root[:, 3] = np.sin(th / 2)
@@ -44,6 +48,13 @@ def lying_state(n, rng):
     root[:, 2] = 0.12 + rng.uniform(0, 0.03, n)
     dof = np.zeros((n, 69, 2), np.float32)
     dof[..., 0] = rng.uniform(-0.2, 0.2, (n, 69))
+    if on_floor:
+        from humanoid_amd import _abi
+        from humanoid_amd.model import load_default_model
+        from oracle import oracle as O
+        model = model or load_default_model()
+        rb = O.forward_kinematics(_abi.make_model(model), root, dof)
+        root[:, 2] += (0.005 - ground_gaps(model, rb).min(-1)).astype(np.float32)
     return root, dof
 
 

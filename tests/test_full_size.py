@@ -68,22 +68,28 @@ def test_full_size_sample_matches_oracle(model, he_model, config):
     idx = np.sort(rng.choice(4096, 48, replace=False))
     root = ro.eng.root_states.cpu().numpy()[idx].copy()
     dof = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy()
+    cache = ro.eng.contact_cache.cpu().numpy()[idx].copy()  # the engine's warm start, for the oracle too
     ro.eng.step_actions(ro.actions, 2)
     torch.cuda.synchronize()
     tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
-    from test_gpu_parity import _cond_close
+    from test_gpu_parity import CondStats, _cond_close, contact_keys
     sp = _abi.default_sim_params(max_contacts=20)
     probes = []
     for seed in (123, 124, 125):  # the oracle's own sensitivity (see _cond_close)
         r_s, d_s = root.copy(), dof.copy()
         d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
-        O.physics_step(he_model, sp, r_s, d_s, tgt, 2)
+        O.physics_step(he_model, sp, r_s, d_s, tgt, 2, cache=cache.copy())
         probes.append((r_s, d_s))
-    out = O.physics_step(he_model, sp, root, dof, tgt, 2)
-    same = ro.eng.num_contacts.cpu().numpy()[idx] == out["num_contacts"]
-    assert same.mean() >= 0.9
+    c_o = cache.copy()
+    out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o)
+    kg = contact_keys(ro.eng.contact_cache.cpu().numpy()[idx])
+    same = np.array([a == b for a, b in zip(kg, contact_keys(c_o))])
+    assert same.mean() >= 0.95
     rg = ro.eng.root_states.cpu().numpy()[idx]
     dg = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx]
-    _cond_close("root pos", rg[same, :3], root[same, :3], [r[same, :3] for r, _ in probes], 1e-4)
-    _cond_close("dof pos", dg[same, :, 0], dof[same, :, 0], [d[same, :, 0] for _, d in probes], 1e-4)
-    _cond_close("dof vel", dg[same, :, 1], dof[same, :, 1], [d[same, :, 1] for _, d in probes], 1e-2, 1e-3)
+    st = CondStats()
+    _cond_close("root pos", rg[same, :3], root[same, :3], [r[same, :3] for r, _ in probes], 1e-4, stats=st)
+    _cond_close("dof pos", dg[same, :, 0], dof[same, :, 0], [d[same, :, 0] for _, d in probes], 1e-4, stats=st)
+    _cond_close("dof vel", dg[same, :, 1], dof[same, :, 1], [d[same, :, 1] for _, d in probes], 1e-2, 1e-3, stats=st)
+    print(f"widened elements {st.widened}/{st.total}: {st.by_name}")
+    assert st.frac <= 0.05

@@ -3,12 +3,13 @@
 Tolerances (float32 kernels vs the reference's float32 torch / the fp64 oracle):
 * imitation outputs: 5e-5 abs (+1e-5 rel) on obs/reward, exact on reset/terminate/progress;
   quaternions up to sign within 5e-6 (the slerp is evaluated in torch's float32 order on both);
-* physics after one policy step (2 substeps): positions 1e-4 m, joint angles 1e-4 rad (BASELINE's
-  1e-4 rad/m), velocities 1e-2 abs + 1e-3 rel (PGS / LTDL in fp32 vs fp64 at joint speeds up to
-  ~100 rad/s), each widened per env by 4x the oracle's own sensitivity to a 1e-6 rad change of the
-  initial joint angles (ill-conditioned many-contact PGS, see _cond_close) -- envs whose contact sets
-  differ between fp32 and fp64 (a point within rounding of the 0.02 m contact offset) are counted
-  and must be rare.
+* physics (both solvers warm-start from their own caches): positions, joint angles and the centre of
+  mass 1e-4 m / rad (BASELINE's 1e-4 rad/m), velocities 1e-2 abs + 1e-3 rel (PGS / LTDL in fp32 vs
+  fp64 at joint speeds up to ~100 rad/s), over 1-30 policy steps. An element is widened to 4x the
+  oracle's own sensitivity to a 1e-6 rad change of the initial joint angles only where that
+  sensitivity exceeds the tolerance (see _cond_close), and each test bounds the share of widened
+  elements (0-5%). Contact SETS are compared by key (body, partner, candidate) each step; envs
+  whose sets differ (a point within rounding of the 0.02 m offset) are excluded, at most 2-5%.
 """
 import numpy as np
 import pytest
@@ -189,23 +190,52 @@ def test_reset_envs_matches_golden(he_model, golden):
     assert (reset.cpu().numpy()[I] == 0).all()
 
 
-def _cond_close(name, g, o, s, atol, rtol=0.0, k=4.0):
-    """|gpu - oracle| <= atol + rtol*|oracle| + k * (per-env oracle sensitivity), elementwise.
+class CondStats:
+    """Counts the elements whose tolerance was widened (see _cond_close) over a whole test."""
 
-    The sensitivity is the oracle's own change when the initial joint angles move by 1e-6 rad (fp32
-    rounding level): a lying body with ~20 contacts has an ill-conditioned, unconverged PGS whose
-    fp64 answer itself moves by ~0.1-1 rad/s under such a perturbation, so no fp32 engine can
-    match it tighter than that. Well-conditioned envs (the vast majority) get the plain atol.
-    `s` may be a list of probes (independent perturbations): the sensitivity is their maximum, a
-    steadier estimate for the chaotic envs than one draw."""
+    def __init__(self):
+        self.widened = 0
+        self.total = 0
+        self.by_name = {}
+
+    @property
+    def frac(self):
+        return self.widened / max(self.total, 1)
+
+
+def _cond_close(name, g, o, s, atol, rtol=0.0, k=4.0, stats=None):
+    """|gpu - oracle| <= atol + rtol*|oracle| elementwise, widened to + k * sens only for the
+    elements whose oracle sensitivity `sens` exceeds atol.
+
+    sens is the oracle's own change of that element when the initial joint angles move by 1e-6 rad
+    (fp32 rounding level), the maximum over the probes `s` (independent perturbations). An element
+    whose fp64 answer moves by more than the tolerance under rounding-level noise is ill-conditioned
+    -- a toe resting on four box corners settles its yaw wherever friction holds it, a many-contact
+    solve of a tumbling body is sensitive -- and no fp32 engine can match it tighter. Everything
+    else gets the plain tolerance; `stats` counts the widened elements so that the caller bounds
+    their share."""
     n = g.shape[0]
     probes = s if isinstance(s, (list, tuple)) else [s]
     g, o = g.reshape(n, -1), o.reshape(n, -1)
-    sens = np.max([np.abs(p.reshape(n, -1) - o).max(-1) for p in probes], axis=0)[:, None]
-    allow = atol + rtol * np.abs(o) + k * sens
+    sens = np.max([np.abs(p.reshape(n, -1) - o) for p in probes], axis=0)
+    ill = sens > atol
+    allow = atol + rtol * np.abs(o) + np.where(ill, k * sens, 0.0)
     bad = np.abs(g - o) > allow
+    if stats is not None:
+        stats.widened += int(ill.sum())
+        stats.total += ill.size
+        stats.by_name[name] = (int(ill.sum()), ill.size)
     assert not bad.any(), (f"{name}: {bad.any(-1).sum()} envs out of tolerance; worst excess "
-                           f"{(np.abs(g - o) - allow).max():.3e}")
+                           f"{(np.abs(g - o) - allow).max():.3e} (|gpu - oracle| max {np.abs(g - o).max():.3e})")
+
+
+def contact_keys(cache):
+    """Per env: the sorted contact keys (body, partner, candidate) of the last solve, from a
+    warm-start cache [N, HE_CACHE_WORDS] (engine buffer or oracle array)."""
+    c = np.ascontiguousarray(cache, np.float32)
+    n = c[:, 7].view(np.int32)
+    keys = c[:, _abi.CACHE_KEYS:_abi.CACHE_KEYS + _abi.MAX_CONTACTS].view(np.int32)
+    return [tuple(sorted(keys[e, :n[e]].tolist())) for e in range(c.shape[0])]
 
 
 def _obs_tol(oo):
@@ -221,30 +251,46 @@ def _obs_tol(oo):
     return tol
 
 
-def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=1e-4, vel_tol=1e-2, max_skip=0.1,
-                     **sim):
+def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=1e-4, vel_tol=1e-2, max_skip=0.02,
+                     max_widened=0.05, env_props=None, **sim):
+    """Engine vs oracle for `steps` policy steps from the same state, both warm-starting from their
+    own caches. Envs whose contact SETS (keys: body, partner, candidate) ever differ are excluded
+    (a point within rounding of the 0.02 m offset, or a tie in the deepest-first reduction), at most
+    `max_skip` of them; at most `max_widened` of the compared elements may need the sensitivity
+    widening (_cond_close)."""
     n = root.shape[0]
     eng = make_engine(he_model, n, **sim)
+    props = {}
+    if env_props is not None:  # config 5: mass scale [N,24], friction [N], terrain kind [N]
+        ms, fr, tk = env_props
+        eng.set_env_properties(cu(ms), cu(fr), cu(tk))
+        props = dict(mass_scale=ms, friction=fr, terrain_kind=tk)
+        sim = dict(sim, terrain=1)
     eng.root_states.copy_(cu(root))
     eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
     eng.dof_targets.copy_(cu(targets))
-    r_o, d_o = root.copy(), dof.copy()
+    r_o, d_o, c_o = root.copy(), dof.copy(), O.new_cache(n)
     # sensitivity probes: joint angles moved by 1e-6 rad (three independent draws)
     probes = []
     for seed in (123, 124, 125):
         r_s, d_s = root.copy(), dof.copy()
         d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
-        probes.append([r_s, d_s, None])
+        probes.append([r_s, d_s, None, O.new_cache(n)])
     sp = _abi.default_sim_params(**sim)
     mismatch = np.zeros(n, bool)
     for _ in range(steps):
         eng.simulate(substeps)
-        out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, substeps)
+        out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, substeps, cache=c_o, **props)
         for pr in probes:
-            pr[2] = O.physics_step(eng.he_model, sp, pr[0], pr[1], targets, substeps)
+            pr[2] = O.physics_step(eng.he_model, sp, pr[0], pr[1], targets, substeps, cache=pr[3], **props)
         torch.cuda.synchronize()
+        kg = contact_keys(eng.contact_cache.cpu().numpy())
+        ko = contact_keys(c_o)
+        mismatch |= np.array([a != b for a, b in zip(kg, ko)])
         mismatch |= eng.num_contacts.cpu().numpy() != out["num_contacts"]
+        mismatch |= eng.dropped_contacts.cpu().numpy() != out["dropped"]
     ok = ~mismatch
+    print(f"contact-set mismatch: {mismatch.sum()}/{n} envs")
     assert mismatch.mean() <= max_skip, f"contact-set mismatch in {mismatch.sum()}/{n} envs"
     rg = eng.root_states.cpu().numpy()
     dg = eng.dof_state.view(n, 69, 2).cpu().numpy()
@@ -255,30 +301,56 @@ def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=
     R = [p[0] for p in probes]
     D = [p[1] for p in probes]
     OS = [p[2] for p in probes]
-    _cond_close("root pos", rg[ok, :3], r_o[ok, :3], [r[ok, :3] for r in R], pos_tol)
+    st = CondStats()
+    kw = dict(stats=st)
+    _cond_close("root pos", rg[ok, :3], r_o[ok, :3], [r[ok, :3] for r in R], pos_tol, **kw)
     _cond_close("root quat", align(rg[ok, 3:7], r_o[ok, 3:7]), r_o[ok, 3:7],
-                [align(r[ok, 3:7], r_o[ok, 3:7]) for r in R], pos_tol)
-    _cond_close("dof pos", dg[ok, :, 0], d_o[ok, :, 0], [d[ok, :, 0] for d in D], pos_tol)
-    _cond_close("root vel", rg[ok, 7:], r_o[ok, 7:], [r[ok, 7:] for r in R], vel_tol, 1e-3)
-    _cond_close("dof vel", dg[ok, :, 1], d_o[ok, :, 1], [d[ok, :, 1] for d in D], vel_tol, 1e-3)
-    _cond_close("body pos", rbg[ok, :, :3], out["rb_state"][ok, :, :3], [o_["rb_state"][ok, :, :3] for o_ in OS], pos_tol)
+                [align(r[ok, 3:7], r_o[ok, 3:7]) for r in R], pos_tol, **kw)
+    _cond_close("dof pos", dg[ok, :, 0], d_o[ok, :, 0], [d[ok, :, 0] for d in D], pos_tol, **kw)
+    _cond_close("root vel", rg[ok, 7:], r_o[ok, 7:], [r[ok, 7:] for r in R], vel_tol, 1e-3, **kw)
+    _cond_close("dof vel", dg[ok, :, 1], d_o[ok, :, 1], [d[ok, :, 1] for d in D], vel_tol, 1e-3, **kw)
+    _cond_close("body pos", rbg[ok, :, :3], out["rb_state"][ok, :, :3], [o_["rb_state"][ok, :, :3] for o_ in OS],
+                pos_tol, **kw)
+    com_g = cases.center_of_mass(_model(), rbg[ok])
+    com_o = cases.center_of_mass(_model(), out["rb_state"][ok])
+    com_s = [cases.center_of_mass(_model(), o_["rb_state"][ok]) for o_ in OS]
+    _cond_close("CoM", com_g, com_o, com_s, pos_tol, **kw)
     _cond_close("dof force", eng.dof_force.view(n, 69).cpu().numpy()[ok], out["dof_force"][ok],
-                [o_["dof_force"][ok] for o_ in OS], 0.5, 1e-3)
+                [o_["dof_force"][ok] for o_ in OS], 0.5, 1e-3, **kw)
+    print(f"sensitivity-widened elements: {st.widened}/{st.total} ({100 * st.frac:.2f}%) {st.by_name}")
+    assert st.frac <= max_widened, f"{st.widened}/{st.total} elements needed the widening: {st.by_name}"
     return eng, out
+
+
+def _model():
+    from humanoid_amd.model import load_default_model
+    return load_default_model()
 
 
 def test_physics_airborne_matches_oracle(he_model):
     rng = np.random.default_rng(1)
     root, dof = cases.random_state(64, rng, height=(3.0, 4.0))
     targets = rng.uniform(-0.5, 0.5, (64, 69)).astype(np.float32)
-    _physics_compare(he_model, root, dof, targets, self_collision=0, max_skip=0.0)
+    _physics_compare(he_model, root, dof, targets, self_collision=0, max_skip=0.0, max_widened=0.0)
 
 
 def test_physics_standing_matches_oracle(he_model, model):
     rng = np.random.default_rng(2)
     root, dof = cases.standing_state(model, 64, rng, xy_jitter=1.0)
     targets = np.zeros((64, 69), np.float32)
-    _physics_compare(he_model, root, dof, targets, steps=5)
+    _physics_compare(he_model, root, dof, targets, steps=5, max_skip=0.0, max_widened=0.05)
+
+
+def test_physics_trajectories_30_steps(he_model, model):
+    """north_star: joint-angle and CoM trajectories within 1e-4 rad / m, over 30 policy steps (1 s,
+    60 substeps, both solvers warm-starting from their own caches): airborne actuated bodies (self
+    collision on) and the PD stand-still on the plane."""
+    rng = np.random.default_rng(11)
+    root, dof = cases.random_state(32, rng, height=(6.0, 7.0), ang=0.4, vel=0.5)
+    targets = rng.uniform(-0.5, 0.5, (32, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, steps=30, max_skip=0.0, max_widened=0.01)
+    root, dof = cases.standing_state(model, 32, rng, xy_jitter=1.0)
+    _physics_compare(he_model, root, dof, np.zeros((32, 69), np.float32), steps=30, max_skip=0.0, max_widened=0.05)
 
 
 def test_physics_contact_rich_matches_oracle(he_model):
@@ -292,7 +364,8 @@ def test_physics_contact_rich_matches_oracle(he_model):
 
 
 def test_physics_domain_randomised_terrain(he_model, model):
-    """Config 5 extension: per-env mass scale, friction and terrain kind vs the oracle."""
+    """Config 5 extension: per-env mass scale, friction and terrain kind vs the oracle, 3 steps,
+    positions and velocities."""
     n = 48
     rng = np.random.default_rng(4)
     root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
@@ -300,21 +373,36 @@ def test_physics_domain_randomised_terrain(he_model, model):
     ms = rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32)
     fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
     tk = (np.arange(n) % 3).astype(np.int32)
-    eng = make_engine(he_model, n, terrain=1)
-    eng.set_env_properties(cu(ms), cu(fr), cu(tk))
-    eng.root_states.copy_(cu(root))
-    eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
-    sp = _abi.default_sim_params(terrain=1)
-    r_o, d_o = root.copy(), dof.copy()
-    for _ in range(3):
-        eng.simulate(2)
-        out = O.physics_step(eng.he_model, sp, r_o, d_o, np.zeros((n, 69), np.float32), 2, mass_scale=ms, friction=fr,
-                             terrain_kind=tk)
-    torch.cuda.synchronize()
-    ok = eng.num_contacts.cpu().numpy() == out["num_contacts"]
-    assert ok.mean() >= 0.9
-    np.testing.assert_allclose(eng.root_states.cpu().numpy()[ok, :3], r_o[ok, :3], atol=1e-4)
-    np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[ok, :, 0], d_o[ok, :, 0], atol=1e-4)
+    # a 0.1 m drop onto slopes and step edges (feet straddling an edge tip over): the divergent
+    # contact-set stress case; 5.7% of the elements were ill-conditioned on the r02 box
+    _physics_compare(he_model, root, dof, np.zeros((n, 69), np.float32), steps=3, env_props=(ms, fr, tk),
+                     max_widened=0.08)
+
+
+def test_knee_limit_matches_oracle(he_model, model):
+    """Knee-y driven at +-5 rad targets (humanoid_phc.py:441-446): the joint angle stops inside pi on
+    the GPU too, and the trajectory follows the oracle's (limit rows, the blocked-joint effort rule)."""
+    n = 8
+    rng = np.random.default_rng(7)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    root[:, 2] += 1.5
+    targets = np.zeros((n, 69), np.float32)
+    targets[:, [4, 16]] = np.where(np.arange(n) % 2 == 0, 5.0, -5.0)[:, None]
+    eng, _ = _physics_compare(he_model, root, dof, targets, steps=20, self_collision=0, max_skip=0.0)
+    q = eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0]
+    ang = np.linalg.norm(q.reshape(n, 23, 3), axis=-1)
+    assert ang.max() < np.pi and ang[:, [1, 5]].min() > np.pi - 0.05  # knees (joints 2, 6) on the limit
+
+
+def test_contact_overflow_counted_and_reduced(he_model):
+    """Lying bodies exceed the 20 contact slots: the engine reports the overflow per env exactly as
+    the oracle, keeps the same (deepest) contact set, and the settled state matches."""
+    rng = np.random.default_rng(5)
+    root, dof = cases.lying_state(32, rng)
+    targets = np.zeros((32, 69), np.float32)
+    # the first step: limbs start inside the plane, ~25-30 contacts per env (the overflow case)
+    eng, out = _physics_compare(he_model, root, dof, targets, steps=1, max_skip=0.05, max_widened=0.05)
+    assert (out["dropped"] > 0).sum() >= 3, "the case must overflow"  # 5 of 32 envs on the box (r02)
 
 
 def test_env_step_fused_matches_oracle(he_model, model, golden):
@@ -354,22 +442,29 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
     for step in range(4):
         r_pre = eng.root_states.cpu().numpy().copy()
         d_pre = eng.dof_state.view(n, 69, 2).cpu().numpy().copy()
+        c_pre = eng.contact_cache.cpu().numpy().copy()
         st_o = st.cpu().numpy().copy(); so_o = so.cpu().numpy().copy(); go_o = go.cpu().numpy().copy()
         prog_o = prog.cpu().numpy().copy()
         eng.step_actions(cu(actions), 2)
         torch.cuda.synchronize()
         np.testing.assert_allclose(eng.dof_targets.cpu().numpy(), tgt, atol=1e-6)
-        r_s, d_s = r_pre.copy(), d_pre.copy()  # oracle sensitivity probe (see _cond_close)
-        d_s[:, :, 0] += (1e-6 * np.random.default_rng(step).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
-        out = O.physics_step(eng.he_model, sp, r_pre, d_pre, tgt.astype(np.float32), 2)
-        O.physics_step(eng.he_model, sp, r_s, d_s, tgt.astype(np.float32), 2)
-        same = eng.num_contacts.cpu().numpy() == out["num_contacts"]
-        _cond_close("root pos", eng.root_states.cpu().numpy()[same, :3], r_pre[same, :3], r_s[same, :3], 1e-4)
-        # saturating actions (targets up to +-pi): the effort-limit switch (|tau| vs 500 Nm) is a
-        # discrete decision taken in fp32 here and fp64 in the oracle, so a dof whose predicted torque
-        # sits within rounding of the limit can take the other branch; the tight physics parity is in
-        # the test_physics_* cases, this test checks the fused imitation/reset half exactly below.
-        np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[same, :, 0], d_pre[same, :, 0], atol=5e-3)
+        # the oracle starts from the engine's own warm-start cache (its signature is r_pre's pose)
+        probes = []
+        for k in range(3):  # oracle sensitivity probes (see _cond_close)
+            r_s, d_s = r_pre.copy(), d_pre.copy()
+            d_s[:, :, 0] += (1e-6 * np.random.default_rng(100 * step + k).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
+            O.physics_step(eng.he_model, sp, r_s, d_s, tgt.astype(np.float32), 2, cache=c_pre.copy())
+            probes.append((r_s, d_s))
+        c_o = c_pre.copy()
+        out = O.physics_step(eng.he_model, sp, r_pre, d_pre, tgt.astype(np.float32), 2, cache=c_o)
+        same = np.array([a == b for a, b in zip(contact_keys(eng.contact_cache.cpu().numpy()), contact_keys(c_o))])
+        assert same.mean() >= 0.9
+        # saturating actions (targets up to +-pi, knees +-5 rad): the effort limit scales the drive
+        # continuously, so joint angles are held at the physics tolerance too
+        _cond_close("root pos", eng.root_states.cpu().numpy()[same, :3], r_pre[same, :3],
+                    [r[same, :3] for r, _ in probes], 1e-4)
+        _cond_close("dof pos", eng.dof_state.view(n, 69, 2).cpu().numpy()[same, :, 0], d_pre[same, :, 0],
+                    [d[same, :, 0] for _, d in probes], 1e-4)
         # oracle imitation + reset on the GPU's post-physics state
         rb = eng.rb_state.view(n, 24, 13).cpu().numpy().copy()
         dstate = eng.dof_state.view(n, 69, 2).cpu().numpy().copy()
