@@ -71,6 +71,7 @@ struct Lds {
     float qloc[NB][4];  // each joint's local rotation exp(q_b), from the kinematics (reused by integrate)
     int nc, nterr;                 // contact slots, of which limits + terrain (slots [0, nterr))
     int nlim;                      // joint-limit slots [0, nlim)
+    uint32_t limmask;              // bodies whose joint-angle limit row is emitted this substep
     int ncand;                     // contacts generated (dropped = ncand - nc), last substep
     int ckey[MAXC];                // warm-start key of each slot (he_sim_params cache layout)
     int wckey[MAXC];               // the previous solve's keys (its impulses: lam)
@@ -204,12 +205,18 @@ HE_DEV bool angle_row(const Lds& L, int b, const he_sim_params& p, float& gap, f
     const int d = 3 * (b - 1);
     const f3 th = f3{L.q[d], L.q[d + 1], L.q[d + 2]};
     const f3 u = f3{L.u0[6 + d], L.u0[7 + d], L.u0[8 + d]};
-    const float t = norm3(th);
-    dir = th * (1.0f / fmaxf(t, 1e-30f));
+    const float t = __builtin_amdgcn_sqrtf(dot3(th, th));
+    dir = th * __builtin_amdgcn_rcpf(fmaxf(t, 1e-30f));
     gap = (3.14159265358979f - kLimitGuard) - t;
     const float closing = dot3(dir, u);
     return t >= 1e-6f && gap < p.limit_margin + p.dt * fmaxf(closing, 0.f);
 }
+
+// The substep's limit rows (gap, row over the joint's dofs) per joint b - 1, from the kinematics to
+// the contact phase, kept in the friction-basis arrays: those are dead from the previous substep's
+// forces until this substep's friction-basis pass, which runs after the limit slots are stored.
+HE_DEV float* limit_rows(Lds& L) { return &L.ct1[0][0]; }
+static_assert(4 * (NB - 1) <= 6 * MAXC, "the limit rows fit the ct1 / ct2 arrays");
 
 // terrain constants of the env, read once per contact phase (slope normal, step field)
 struct Terrain {
@@ -1038,6 +1045,20 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         }
         if (act)
             for (int x = 0; x < 6; ++x) L.Acc[b][x] = A[x];
+        // joint-angle limits of this substep (lane = body b >= 1): which rows are emitted, their
+        // gap and direction (LimitRows), read by the drive terms (a joint on its limit cannot give
+        // way) and by the contact phase (the limit slots)
+        if (sp.joint_limits) {
+            float lg = 0.f;
+            f3 ld = f3{0.f, 0.f, 0.f};
+            const bool on = act && b > 0 && angle_row(L, b, sp, lg, ld);
+            const uint64_t bm = __ballot(on);
+            if (on) {
+                float* lr = limit_rows(L) + 4 * (b - 1);
+                lr[0] = lg; lr[1] = -ld.x; lr[2] = -ld.y; lr[3] = -ld.z;  // the row is -q^
+            }
+            if (lane == 0) L.limmask = (uint32_t)bm;
+        }
     }
     sync();
 #if HE_KIN_AXES_FLAT
@@ -1188,6 +1209,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     __builtin_amdgcn_s_setprio(0);
     STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
+    const uint32_t limmask = p.joint_limits ? (uint32_t)__builtin_amdgcn_readfirstlane((int)L.limmask) : 0u;
 #if HE_DOF_FLAT
     // lane = dof (then dofs 64..74 on lanes 0..10), the root's six dofs selected out: no loop,
     // no root branch, saturation by selects
@@ -1208,10 +1230,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // A joint held at its angle limit cannot give way: its check takes the torque at rest.
         const float c = dt * kp + kd;
         const float hii = dot6(L.S[i], L.IS[i]) + m.armature[d];
-        float lgap;
-        f3 ldir;
-        const bool blocked = p.joint_limits && jd && angle_row(L, b > 0 ? b : 1, p, lgap, ldir);
-        const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) / (hii + dt * c);
+        const bool blocked = p.joint_limits && jd && ((limmask >> b) & 1u);
+        const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) * __builtin_amdgcn_rcpf(hii + dt * c);
         const float sc = fabsf(tau_i) > lim ? lim / fabsf(tau_i) : 1.f;
         tau *= sc;
         kp *= sc;
@@ -1236,9 +1256,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float tau = kp * (err - dt * u) - kd * u;
             float lim = m.effort[d];
             const float c = dt * kp + kd;
-            float lgap;
-            f3 ldir;
-            const bool blocked = p.joint_limits && angle_row(L, b, p, lgap, ldir);
+            const bool blocked = p.joint_limits && ((limmask >> b) & 1u);
             const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) / (dot6(L.S[i], L.IS[i]) + m.armature[d] + dt * c);
             if (fabsf(tau_i) > lim) {
                 const float sc = lim / fabsf(tau_i);
@@ -1355,13 +1373,13 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     // -- joint-angle limit slots (lane = joint b - 1)
     int nlim = 0, nlim_all = 0;
     if (p.joint_limits) {
-        float lg = 0.f;
-        f3 ld = f3{0.f, 0.f, 0.f};
-        const bool act = lane < NB - 1 && angle_row(L, lane + 1, p, lg, ld);
+        const uint32_t lm = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.limmask);
+        const bool act = lane < NB - 1 && ((lm >> (lane + 1)) & 1u);
         const int pre = wave_prefix(act, lane, nlim_all);
         if (act && pre < maxc) {
-            // the row -q^ over the joint's dofs travels in the contact position (unused by a limit)
-            store_contact(L, pre, lane + 1, -2, ld * -1.f, f3{0.f, 0.f, 1.f}, lg, 0.f);
+            // the row over the joint's dofs travels in the contact position (unused by a limit)
+            const float* lr = limit_rows(L) + 4 * lane;
+            store_contact(L, pre, lane + 1, -2, f3{lr[1], lr[2], lr[3]}, f3{0.f, 0.f, 1.f}, lr[0], 0.f);
             L.ckey[pre] = (lane + 1) | (7 << 16);
         }
         nlim = nlim_all < maxc ? nlim_all : maxc;
@@ -1437,10 +1455,16 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 rank[ci] += c;
                 rank[cj] -= c;
             }
+        // the kept candidates (a box's 4 deepest corners) take the body's slots in candidate index
+        // order, so that resting contacts keep their slots from one substep to the next (the
+        // warm start then maps impulses one to one); rank[] becomes that slot offset
         myn = 0;
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci)
-            if (cand[ci] && rank[ci] < 4) ++myn;
+        for (int ci = 0; ci < 8; ++ci) {
+            const bool kept = cand[ci] && rank[ci] < 4;
+            rank[ci] = kept ? myn : 8;
+            myn += kept ? 1 : 0;
+        }
         // exclusive prefix of myn (0..4) over the lanes: three bit ballots, v_mbcnt per bit
         base = 0;
         int total = 0;
@@ -1617,13 +1641,37 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     sync();
     STAMP(7);
+    // ---- warm start: the previous solve's impulse of each row's contact key (lane c matches its
+    // slot's key against the old keys by readlane, row lanes fetch the index and the impulse)
+    float lam0 = 0.f;
+    {
+        const int nw = __builtin_amdgcn_readfirstlane(L.nwc);
+        if (nw > 0 && nc > 0) {
+            const int wk = lane < nw ? L.wckey[lane < MAXC ? lane : 0] : -1;
+            const int ck = lane < nc ? L.ckey[lane < MAXC ? lane : 0] : -2;
+            const int nr = 3 * nc;
+            if (nw == nc && __ballot(lane < nc && wk != ck) == 0ull) {
+                lam0 = lane < nr ? lam_prev : 0.f;  // the same contacts in the same slots (at rest)
+            } else {
+                int src = -1;
+                for (int j = 0; j < nw; ++j) {
+                    const int kj = __builtin_amdgcn_readlane(wk, j);
+                    src = (src < 0 && kj == ck) ? j : src;
+                }
+                const int r = lane < nr ? lane : 0;
+                const int ci = r / 3, kind = r - 3 * ci;
+                const int srow = __shfl(src, ci, W);
+                const float v = __shfl(lam_prev, srow >= 0 ? 3 * srow + kind : 0, W);
+                lam0 = (lane < nr && srow >= 0) ? v : 0.f;
+            }
+        }
+    }
     if (nc > 0) {
         // ---- contact rows, one per lane: z = J_r^T, brow = J_r uf + bias, then z <- D^-1/2 L^-T z
         // (dofs outside every row's support stay zero and are skipped wave-uniformly), so that the
         // Delassus operator A = Zh Zh^T is a plain Gram matrix of the lanes' registers
         const int nr = 3 * nc;
         float brow = 0.f, diag = 0.f, lamv = 0.f;
-        float lam0 = 0.f;  // warm start: the previous solve's impulse of this row's contact key
         float acol[MAXR];  // lane c: A[r][c]
         regla::ZVec z;     // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
         {
@@ -1717,16 +1765,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
             }
 #endif
-            {  // warm start: find the row's contact key among the previous solve's keys
-                const int nw = __builtin_amdgcn_readfirstlane(L.nwc);
-                if (nw > 0) {
-                    const int key = L.ckey[ci];
-                    int src = -1;
-                    for (int j = 0; j < nw; ++j) src = (src < 0 && L.wckey[j] == key) ? j : src;
-                    const float v = __shfl(lam_prev, src >= 0 ? 3 * src + kind : 0, W);
-                    lam0 = (lane < nr && src >= 0) ? v : 0.f;
-                }
-            }
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
 #pragma unroll
@@ -1746,9 +1784,17 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const float invd = 1.0f / (lane < nr ? diag + 1e-12f : 1.f);
             // residual at the warm start: w = brow + A lambda0 (acol: lane c holds A[r][c] = A[c][r])
             float w0 = brow;
-            if (__ballot(lam0 != 0.f)) {  // wave-uniform
+            if (__ballot(lam0 != 0.f)) {  // wave-uniform; rows >= nr hold no impulse
+                auto aw = [&](auto nrows) {  // four independent accumulation chains
+                    constexpr int NRW = decltype(nrows)::value;
+                    float wa[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int r = 0; r < MAXR; ++r) w0 = fmaf(acol[r], regla::rdlane(lam0, r), w0);
+                    for (int r = 0; r < NRW; ++r) wa[r & 3] = fmaf(acol[r], regla::rdlane(lam0, r), wa[r & 3]);
+                    w0 += (wa[0] + wa[1]) + (wa[2] + wa[3]);
+                };
+                if (nr <= 32) aw(std::integral_constant<int, 32>{});
+                else if (nr <= 48) aw(std::integral_constant<int, 48>{});
+                else aw(std::integral_constant<int, MAXR>{});
             }
             lamv = lam0;
             float cd = lane < nr ? -w0 * invd : 0.f;

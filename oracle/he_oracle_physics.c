@@ -474,16 +474,19 @@ static int gen_all(const he_model* m, const he_sim_params* p, const kin* k, cons
                 cd[ci] = terrain_height(p, terrain_kind, cx[ci], cn[ci]);
                 if (cd[ci] < off) cand[ncand++] = ci;
             }
-            /* selection of up to 4 deepest */
+            /* the 4 deepest (ties by corner index), emitted in corner index order (resting
+             * contacts keep their slots from one substep to the next) */
+            int keep[8] = {0};
             for (int sel = 0; sel < 4 && ncand > 0; ++sel) {
                 int best = 0;
                 for (int j = 1; j < ncand; ++j)
                     if (cd[cand[j]] < cd[cand[best]]) best = j;
-                int ci = cand[best];
-                nc = add_contact(cs, nc, maxc, total, b, -1, ci, cx[ci], cn[ci], cd[ci], mu);
+                keep[cand[best]] = 1;
                 for (int j = best; j < ncand - 1; ++j) cand[j] = cand[j + 1];
                 --ncand;
             }
+            for (int ci = 0; ci < 8; ++ci)
+                if (keep[ci]) nc = add_contact(cs, nc, maxc, total, b, -1, ci, cx[ci], cn[ci], cd[ci], mu);
         }
     }
     if (p->self_collision) {

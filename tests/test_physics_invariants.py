@@ -183,12 +183,13 @@ def test_pd_stand_still_equilibrium(he_model, model):
 
 
 def test_penetration_within_contact_offset(he_model, model):
-    """Standing and lying bodies settle with every terrain candidate above -5 mm (the Baumgarte
-    steady state under gravity is ~ -g dt^2 / 0.2 = -1.4 mm), far inside contact_offset = 0.02 m."""
+    """Standing and lying bodies settle with every terrain candidate above -2 mm (the Baumgarte
+    steady state under gravity is ~ -g dt^2 / 0.2 = -1.4 mm), far inside contact_offset = 0.02 m.
+    cases.lying_state starts limbs inside the plane; its bodies tumble for ~1.5 s and rest by 4 s."""
     rng = np.random.default_rng(5)
     targets = np.zeros((8, 69), np.float32)
     for root, dof in (cases.standing_state(model, 8, rng, xy_jitter=1.0), cases.lying_state(8, rng)):
-        r, d, out, sp = _run(he_model, root, dof, targets, 60)
+        r, d, out, sp = _run(he_model, root, dof, targets, 120)
         gaps = cases.ground_gaps(model, out["rb_state"])
-        assert gaps.min() > -5e-3, gaps.min()
+        assert gaps.min() > -2e-3, gaps.min()
         assert gaps.min() < sp.contact_offset  # bodies rest on the plane
