@@ -48,6 +48,8 @@ def parse(argv=None):
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
+    ap.add_argument("--no-tracking", action="store_true",
+                    help="skip the configs[2] tracking-action leg (throughput + joint-pose L2 vs ref)")
     return ap.parse_args(argv)
 
 
@@ -120,6 +122,7 @@ class Rollout:
         from humanoid_amd.model import pd_action_offset_scale
         from humanoid_amd.body_sets import frozen_dof_mask
         self.args = args
+        self.model = model
         n = args.num_envs
         tables, actions, rng = build_workload(args, model, rank)
         sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0)
@@ -153,6 +156,27 @@ class Rollout:
         phases = torch.as_tensor(rng.uniform(0, 1, n).astype(np.float32), device=dev)
         self.eng.reset_envs(self.p, self.em, ids, phases, self.obs, self.reset, self.term)
 
+    def tracking_actions(self):
+        """a = clip(ref_dof_pos / scale, -1, 1) with the reference pose at
+        the env's next motion time (humanoid_phc.py motion_times = progress * dt + start + offset),
+        on the device: one motion-state launch + elementwise ops."""
+        import torch
+        if not hasattr(self, "inv_scale"):
+            from humanoid_amd.model import pd_action_offset_scale
+            _, sc = pd_action_offset_scale(self.model)
+            self.inv_scale = torch.as_tensor(1.0 / np.asarray(sc, np.float32), device=self.eng.device)
+        t = (self.prog.float() + 1.0) * self.p.control_dt + self.st + self.so
+        ref = self.eng.motion_state(self.mids, t, None)["dof_pos"]
+        torch.clamp(ref * self.inv_scale, -1.0, 1.0, out=self.actions)
+
+    def joint_pose_l2(self):
+        """BASELINE metric's "joint-pose L2 vs ref": mean over envs of ||q - q_ref(t)||_2 (rad, 69
+        dofs) at the env's current motion time."""
+        t = self.prog.float() * self.p.control_dt + self.st + self.so
+        ref = self.eng.motion_state(self.mids, t, None)["dof_pos"]
+        q = self.eng.dof_state.view(self.args.num_envs, 69, 2)[..., 0]
+        return (q - ref).norm(dim=1)
+
     def step(self, ev=None):
         """ev: optional (start, mid, end) torch.cuda.Events around the two kernels."""
         if ev is not None:
@@ -165,6 +189,48 @@ class Rollout:
         if ev is not None:
             ev[2].record()
         self.step_index += 1
+
+
+def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
+    """configs[2] with the tracking action stream: 4096 envs over 128 clips,
+    actions = clip(ref_dof_pos / scale) computed on the device every step inside the timed region;
+    then the joint-pose L2 vs the reference over `l2_steps` further steps (untimed)."""
+    import torch
+    a = argparse.Namespace(**vars(args))
+    a.config = "imitation"
+    ro = Rollout(a, model, device_index, 0)
+    for _ in range(warmup):
+        ro.tracking_actions()
+        ro.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ro.tracking_actions()
+        ro.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    l2 = []
+    for _ in range(l2_steps):
+        ro.tracking_actions()
+        ro.step()
+        l2.append(ro.joint_pose_l2())
+    l2 = torch.stack(l2).cpu().numpy()
+    return {"value": round(a.num_envs * steps / dt, 1), "unit": "env-steps/s", "steps": steps,
+            "workload": "configs[2]: 4096 envs over 128 synthetic clips, actions = clip(ref_dof_pos / scale) "
+                        "computed on the device each step (inside the timed region)",
+            "joint_pose_l2_rad": {"mean": round(float(l2.mean()), 5), "p90": round(float(np.percentile(l2, 90)), 5),
+                                  "steps": l2_steps,
+                                  "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x steps"}}
+
+
+def cpu_model_name():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(args, model):
@@ -197,10 +263,11 @@ def cpu_baseline(args, model):
         ms = rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32)
         fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
         tk = (np.arange(n) % 3).astype(np.int32)
+    cache = O.new_cache(n)  # the engine's warm start
     t0 = time.perf_counter()
     for step in range(a.cpu_steps):
         out = O.physics_step(hm, sim, st["root_states"], st["dof_state"], tgt, 2, mass_scale=ms, friction=fr,
-                             terrain_kind=tk)
+                             terrain_kind=tk, cache=cache)
         im = O.imitation_step(p, mt, out["rb_state"], st["dof_state"][..., 1], out["dof_force"], st["progress"],
                               np.arange(n), st["start_times"], st["start_offsets"], st["global_offset"])
         st["progress"][:] = im["progress"]
@@ -213,8 +280,9 @@ def cpu_baseline(args, model):
     dt = time.perf_counter() - t0
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": n * a.cpu_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model_name(), "nproc": os.cpu_count(),
             "sample": f"{n} envs x {a.cpu_steps} policy steps of the C oracle (fp64 physics + imitation + resets), "
-                      f"OpenMP over envs, {dt:.1f} s"}
+                      f"OpenMP over envs ({threads} threads), {dt:.1f} s"}
 
 
 def main():
@@ -259,6 +327,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    nc = ro.eng.num_contacts.cpu().numpy()
+    dropped = ro.eng.dropped_contacts.cpu().numpy()
     phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs.values()]))
     imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs.values()]))
     if world > 1:
@@ -271,7 +341,17 @@ def main():
     if rank == 0:
         phys_tflops = PHYS_FLOP_PER_ENV_STEP * n / (phys_ms * 1e-3) / 1e12
         imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
-        traffic = imit_traffic = None
+        traffic = imit_traffic = mfma = None
+        mfile = os.path.join(ROOT, "profiles", "pmc_mfma.json")  # rocprofv3 SQ counters of the bench
+        if os.path.exists(mfile):
+            try:
+                e = json.load(open(mfile)).get(f"{args.config}:{n}")
+                if e:
+                    mfma = {"util": e["mfma_util"], "valu_issue_frac": e["valu_issue_frac"],
+                            "source": "profiles/pmc_mfma.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / "
+                                      "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
+            except Exception:
+                mfma = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
             try:
@@ -300,14 +380,26 @@ def main():
                                     "dr": "configs[4]: 4096 envs, mass/friction randomisation + 3 terrains"}[args.config],
                        "num_envs_per_gpu": n, "substeps": 2, "sim_dt": 1 / 60, "max_contacts": args.max_contacts,
                        "parallelism": f"replicas{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
+            # the physics kernel is bound by the latency of its per-env serial chains (elimination,
+            # Gauss-Seidel sweeps, triangular solves) at 2 waves / SIMD, not by HBM or the matrix
+            # cores: priced against the FP32 vector / matrix peak with the canonical dense-equivalent
+            # flop count; mfma_util is the measured matrix-core busy share (rocprofv3 SQ counters)
+            "roofline": {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                         "kernel": "physics_kernel (fp32 vector; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
-                         "avg_launch_ms": round(phys_ms, 4)},
+                         "kernel": "physics_kernel (fp32 VALU + MFMA; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
+                         "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma},
+            "contacts": {"slots_mean": round(float(nc.mean()), 3), "slots_max": int(nc.max()),
+                         "capacity": args.max_contacts, "envs_dropping": int((dropped > 0).sum()),
+                         "dropped_mean": round(float(dropped.mean()), 4)},
             "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(imit_gbs / HBM_PEAK_GBS, 5), "avg_launch_ms": round(imit_ms, 4),
                                  "traffic": imit_traffic},
         }
+        if not args.no_tracking and world == 1 and args.num_envs == 4096:
+            try:
+                line["tracking_configs2"] = tracking_leg(args, model, local)
+            except Exception as exc:  # report, never fake
+                line["tracking_configs2"] = {"value": None, "error": repr(exc)}
         if not args.no_puffer_level and world == 1:
             try:
                 line["puffer_env_step"] = puffer_level(args, model)
