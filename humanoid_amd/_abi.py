@@ -48,7 +48,7 @@ class HeImitationParams(C.Structure):
         ("w_pos", C.c_float), ("w_rot", C.c_float), ("w_vel", C.c_float), ("w_ang_vel", C.c_float),
         ("power_coef", C.c_float), ("use_power_reward", C.c_int32), ("control_dt", C.c_float),
         ("enable_early_termination", C.c_int32), ("eval_mode", C.c_int32), ("reset_body_mask", C.c_int32),
-        ("term_dist", C.c_float * NB),
+        ("term_dist", C.c_float * NB), ("state_init", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -120,7 +120,7 @@ def default_sim_params(**kw) -> HeSimParams:
 
 def imitation_params(reward=None, control_dt=1.0 / 30.0, use_power_reward=True, power_coef=0.0005,
                      enable_early_termination=True, eval_mode=False, termination_distance=0.25,
-                     reset_body_ids=None) -> HeImitationParams:
+                     reset_body_ids=None, state_init_start=False) -> HeImitationParams:
     """config.py:37-50 (RewardConfig), :97-112 (EnvConfig) defaults."""
     r = dict(k_pos=100.0, k_rot=10.0, k_vel=0.1, k_ang_vel=0.1, w_pos=0.5, w_rot=0.3, w_vel=0.1, w_ang_vel=0.1)
     if reward:
@@ -139,6 +139,7 @@ def imitation_params(reward=None, control_dt=1.0 / 30.0, use_power_reward=True, 
     td = np.broadcast_to(np.asarray(termination_distance, np.float32), (NB,))
     for b in range(NB):
         p.term_dist[b] = float(td[b])
+    p.state_init = 1 if state_init_start else 0
     return p
 
 

@@ -423,7 +423,9 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
         }
         if (a.mode == 1 && reset) {
             do_reset = true;
-            float ph = hash_uniform(a.seed, a.step, (uint32_t)e);
+            // Random: sample_time_interval of a hashed phase; Start (and test mode): time 0
+            // (humanoid_phc.py:848-852)
+            float ph = a.p.state_init == 1 ? 0.f : hash_uniform(a.seed, a.step, (uint32_t)e);
             reset_time = sample_time_interval(ph, mm.len);
         }
     } else {

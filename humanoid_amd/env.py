@@ -50,11 +50,34 @@ class RewardConfig:  # config.py:37-50
 class RobotConfig:  # config.py:53-86 (the fields the hot path reads)
     humanoid_type: str = "smpl"
     has_self_collision: bool = True
+    has_smpl_pd_offset: bool = False  # PD offsets from the SMPL rest pose (humanoid_phc.py:411-440)
+    has_upright_start: bool = True    # the clips' upright start (obs heading frame, common.py:106-176)
+    has_dof_subset: bool = True       # AMP's 19-joint dof subset (humanoid_phc.py:186-194)
     has_mesh: bool = False
+    has_shape_obs: bool = False
+    has_shape_obs_disc: bool = False
+    has_limb_weight_obs: bool = False
+    has_limb_weight_obs_disc: bool = False
     reduce_action: bool = False
     freeze_hand: bool = True
     freeze_toe: bool = True
     bias_offset: bool = False
+
+    def check(self):
+        """Raise for the reference options the engine's fused kernels do not implement (their
+        defaults are what the engine bakes in); never silently ignore one."""
+        unsupported = {"has_upright_start": (self.has_upright_start, True), "has_dof_subset": (self.has_dof_subset, True),
+                       "has_mesh": (self.has_mesh, False), "has_shape_obs": (self.has_shape_obs, False),
+                       "has_shape_obs_disc": (self.has_shape_obs_disc, False),
+                       "has_limb_weight_obs": (self.has_limb_weight_obs, False),
+                       "has_limb_weight_obs_disc": (self.has_limb_weight_obs_disc, False),
+                       "reduce_action": (self.reduce_action, False)}
+        for name, (value, supported) in unsupported.items():
+            if bool(value) != supported:
+                raise NotImplementedError(f"RobotConfig.{name}={value} is not supported by the engine "
+                                          f"(the reference default {supported} is)")
+        if self.humanoid_type != "smpl":
+            raise ValueError(f"humanoid_type {self.humanoid_type!r}: only 'smpl' (config.py:56)")
 
 
 @dataclass
@@ -76,7 +99,10 @@ class EnvConfig:  # config.py:89-157
     kd_scale: float = 1.0
     log_interval: int = 32
     rew_power_coef: float = 0.0005
-    state_init: str = "Random"
+    state_init: str = "Random"   # StateInit (config.py:114): Random, Start (Default / Hybrid raise)
+    hybrid_init_prob: float = 0.5  # config.py:139 (Hybrid only)
+    add_obs_noise: bool = False    # config.py:120-121, humanoid_phc.py:956
+    obs_noise_std: float = 0.1
     min_motion_len: int = 5
     max_motion_len: int = 600
     robot: RobotConfig = field(default_factory=RobotConfig)
@@ -123,8 +149,16 @@ class HumanoidPHC:
         from .motion_lib import MotionLibSMPL
         if cfg.device_type != "cuda":
             raise ValueError("the engine runs on the GPU only (device_type='cuda')")
-        if cfg.robot.reduce_action:
-            raise NotImplementedError("reduce_action is off in the reference defaults and not supported")
+        cfg.robot.check()
+        # _reset_actors (humanoid_phc.py:679-686): Random and Start sample the reference motion
+        # (_reset_ref_state_init); Default (the initial pose, no reference) and Hybrid (a Bernoulli
+        # mix of both) need a reset path that writes the initial state and the observation without a
+        # motion sample, which the engine does not have: they raise instead of resetting otherwise
+        if cfg.state_init in ("Default", "Hybrid"):
+            raise NotImplementedError(f"state_init={cfg.state_init!r} is not supported by the engine "
+                                      "(Random, the reference default, and Start are)")
+        if cfg.state_init not in ("Random", "Start"):
+            raise ValueError(f"Unsupported state initialization strategy: {cfg.state_init}")
         self.cfg = cfg
         self.device = torch.device(cfg.device)
         n = cfg.num_envs
@@ -138,7 +172,8 @@ class HumanoidPHC:
         rng = np.random.default_rng(cfg.seed)
         self.engine = Engine(self.model, n, device=self.device.index or 0, sim_params=sim,
                              start_xy=rng.uniform(-1.0, 1.0, (n, 2)).astype(np.float32))
-        off, sc = pd_action_offset_scale(self.model, bias_offset=cfg.robot.bias_offset)
+        off, sc = pd_action_offset_scale(self.model, bias_offset=cfg.robot.bias_offset,
+                                         has_smpl_pd_offset=cfg.robot.has_smpl_pd_offset)
         frozen = np.zeros(self.num_dof, np.int32)
         if cfg.robot.freeze_hand or cfg.robot.freeze_toe:
             frozen = np.array(frozen_dof_mask(freeze_hand=cfg.robot.freeze_hand, freeze_toe=cfg.robot.freeze_toe),
@@ -194,13 +229,28 @@ class HumanoidPHC:
         self._load(sample_idxes=torch.from_numpy(idx))
 
     # -- parameters ----------------------------------------------------------------------
+    @property
+    def _start_at_zero(self):
+        """_sample_ref_state (humanoid_phc.py:848-855): motion time 0 for Start and in test mode."""
+        return self.cfg.state_init == "Start" or self.flag_test
+
+    def _obs_noise(self):
+        """humanoid_phc.py:956: obs + N(0, obs_noise_std) while training (not in test mode)."""
+        import torch
+        if self.cfg.add_obs_noise and not self.flag_test:
+            if not hasattr(self, "_noise_gen"):  # its own stream: the reset phases stay the same
+                self._noise_gen = torch.Generator(device=self.device).manual_seed(self.cfg.seed + 7919)
+            self.obs_buf.add_(torch.randn(self.obs_buf.shape, device=self.device, generator=self._noise_gen)
+                              * self.cfg.obs_noise_std)
+
     def _update_params(self):
         r = dataclasses.asdict(self.cfg.reward)
         self._params = _abi.imitation_params(reward=r, use_power_reward=self.cfg.reward.use_power_reward,
                                              power_coef=self.cfg.rew_power_coef,
                                              enable_early_termination=self.cfg.enable_early_termination,
                                              eval_mode=self.flag_im_eval, termination_distance=self._term_dist,
-                                             reset_body_ids=self._reset_bodies)
+                                             reset_body_ids=self._reset_bodies,
+                                             state_init_start=self._start_at_zero)
 
     def set_termination_distances(self, termination_distances):  # :1338-1339
         self._term_dist = termination_distances
@@ -228,9 +278,13 @@ class HumanoidPHC:
         import torch
         if len(env_ids) == 0:
             return
-        phases = torch.rand(len(env_ids), device=self.device, generator=self._gen)
+        if self._start_at_zero:
+            phases = torch.zeros(len(env_ids), device=self.device)
+        else:
+            phases = torch.rand(len(env_ids), device=self.device, generator=self._gen)
         self.engine.reset_envs(self._params, self._em, env_ids.to(torch.int32), phases, self.obs_buf,
                                self._reset_u8, self._term_u8)
+        self._obs_noise()
 
     def reset(self, env_ids=None):
         safe_reset = env_ids is None or len(env_ids) == self.cfg.num_envs
@@ -247,6 +301,7 @@ class HumanoidPHC:
         self._attach_eval()
         self.engine.imitation_step(self._params, self._em, self.obs_buf, self.rew_buf, self.reward_raw,
                                    self._reset_u8, self._term_u8)
+        self._obs_noise()
         self.extras["terminate"] = self._terminate_buf.clone()
         self.extras["reward_raw"] = self.reward_raw.detach()
         if self.cfg.use_amp_obs:  # the launch above also shifted the history and wrote row 0 (:154-157)
@@ -432,6 +487,7 @@ class PHCPufferEnv:
         e._attach_eval()
         e.engine.imitation_reset_step(e._params, e._em, e.obs_buf, e.rew_buf, e.reward_raw, e._reset_u8, e._term_u8,
                                       seed=self.cfg.seed, step_index=self.tick)
+        e._obs_noise()
         # the step's returned copies and the episode bookkeeping (env.py:120-160) in one launch
         rew = torch.empty_like(self.rewards)
         term_copy = torch.empty_like(e._term_u8)

@@ -105,6 +105,9 @@ typedef struct he_imitation_params {
     int32_t eval_mode;               /* flag_im_eval: mean-distance termination */
     int32_t reset_body_mask;         /* bit b set = body b in _reset_bodies_id */
     float term_dist[HE_NUM_BODIES];  /* _termination_distances */
+    int32_t state_init;              /* reset motion time (humanoid_phc.py:848-852): 0 Random =
+                                        sample_time_interval (config.py:114), 1 Start / test mode = 0 */
+    int32_t reserved;
 } he_imitation_params;
 
 /* Buffer kinds (humanoid_phc.py:497-554, the tensors gymtorch.wrap_tensor exposed). */

@@ -233,3 +233,50 @@ def test_puffer_env_amp_obs(model):
         prev = cur.clone()
     assert n_reset > 0
     assert torch.isfinite(pe.amp_obs).all()
+
+
+# ------------------------------------------------------------- config branches (A11 mirror)
+def test_env_config_branches_raise_before_the_gpu():
+    """state_init Default / Hybrid and the obs / robot options the fused kernels do not implement
+    raise (NotImplementedError), unknown values raise as the reference does (ValueError,
+    humanoid_phc.py:679-686) -- before any GPU work, so this runs on the CPU."""
+    from humanoid_amd.env import EnvConfig, HumanoidPHC, RobotConfig
+    for si in ("Default", "Hybrid"):
+        with pytest.raises(NotImplementedError, match="state_init"):
+            HumanoidPHC(EnvConfig(num_envs=4, state_init=si))
+    with pytest.raises(ValueError, match="Unsupported state initialization"):
+        HumanoidPHC(EnvConfig(num_envs=4, state_init="Middle"))
+    for kw in (dict(has_upright_start=False), dict(has_shape_obs=True), dict(reduce_action=True), dict(has_mesh=True)):
+        with pytest.raises(NotImplementedError, match="RobotConfig"):
+            HumanoidPHC(EnvConfig(num_envs=4, robot=RobotConfig(**kw)))
+    RobotConfig(has_smpl_pd_offset=True).check()  # supported (pd_action_offset_scale)
+
+
+@pytest.mark.gpu
+def test_state_init_start_and_obs_noise(model):
+    """state_init=Start: every reset (the full reset and the fused device resets of PHCPufferEnv)
+    starts the motion at time 0 (humanoid_phc.py:850-851); add_obs_noise adds N(0, 0.1) to the
+    observations while training (humanoid_phc.py:956)."""
+    from humanoid_amd.env import EnvConfig, PHCPufferEnv
+    n = 32
+    pe = PHCPufferEnv(EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=5, state_init="Start"))
+    pe.reset()
+    e = pe.env
+    assert (e._motion_start_times == 0).all()
+    rng = np.random.default_rng(1)
+    resets = 0
+    for _ in range(20):
+        pe.step(rng.uniform(-1, 1, (n, 69)).astype(np.float32))
+        r = e.reset_buf.clone()
+        resets += int(r.sum())
+        assert (e._motion_start_times[r] == 0).all()
+    assert resets > 0
+    pe.close()
+    clean = PHCPufferEnv(EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=5))
+    noisy = PHCPufferEnv(EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=5, add_obs_noise=True))
+    o0, _ = clean.reset()
+    o1, _ = noisy.reset()
+    d = (o1 - o0).float()
+    assert abs(float(d.std()) - 0.1) < 0.01 and abs(float(d.mean())) < 0.01
+    clean.close()
+    noisy.close()
