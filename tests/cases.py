@@ -99,3 +99,22 @@ def ground_gaps(model, rb_state):
         w = rb[:, b, None, :3] + np.einsum("nij,kj->nki", R[:, b], pts)
         out[:, b] = w[..., 2].min(-1) - rad
     return out
+
+
+def expmap_tol(dof_pos, atol=1e-4, dq=1e-6):
+    """Per-element tolerance of exp-map joint coordinates (quat_to_exp_map, torch_utils.py) computed
+    from float32 quaternions: the angle is 2 acos(w), whose conditioning is 1 / sin(theta / 2), so a
+    quaternion that agrees to dq (a few float32 ulps of w ~ 1) gives an angle -- and exp-map
+    components -- that agree to 2 dq / sin(theta / 2): 1e-4 (north_star) for joints bent past
+    ~1.2 deg, the fp32 acos bound below that (torch's own float32 rounding of the reference)."""
+    v = np.asarray(dof_pos, np.float64).reshape(dof_pos.shape[0], -1, 3)
+    th = np.linalg.norm(v, axis=-1, keepdims=True)
+    tol = atol + 2.0 * dq / np.maximum(np.sin(th / 2.0), 1e-12)
+    return np.broadcast_to(tol, v.shape).reshape(dof_pos.shape)
+
+
+def assert_expmap_close(got, ref):
+    tol = expmap_tol(ref)
+    bad = np.abs(np.asarray(got) - np.asarray(ref)) > tol
+    assert not bad.any(), (f"{bad.sum()} exp-map coordinates out of tolerance: got {np.asarray(got)[bad][:4]} "
+                           f"ref {np.asarray(ref)[bad][:4]} tol {tol[bad][:4]}")

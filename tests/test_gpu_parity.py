@@ -105,7 +105,7 @@ def test_motion_state_matches_golden(he_model, golden):
     np.testing.assert_allclose(r["body_ang_vel"], g["ms_body_ang_vel"], atol=1e-5)
     np.testing.assert_allclose(r["dof_vel"], g["ms_dof_vel"], atol=1e-5)
     quat_close(r["rb_rot"], g["ms_rb_rot"], 5e-6)
-    np.testing.assert_allclose(r["dof_pos"], g["ms_dof_pos"], atol=2e-4)
+    cases.assert_expmap_close(r["dof_pos"], g["ms_dof_pos"])
 
 
 def _load_env_state(eng, g):
@@ -176,9 +176,9 @@ def test_reset_envs_matches_golden(he_model, golden):
     quat_close(rs[:, 3:7], gr[:, 3:7], 5e-6)
     np.testing.assert_allclose(rs[:, 7:], gr[:, 7:], atol=1e-5)
     ds = eng.dof_state.view(n, 69, 2).cpu().numpy()[I]
-    np.testing.assert_allclose(ds[..., 0], g["dof_pos"][I], atol=2e-4)
+    cases.assert_expmap_close(ds[..., 0], g["dof_pos"][I])
     np.testing.assert_allclose(ds[..., 1], g["dof_vel"][I], atol=1e-5)
-    np.testing.assert_allclose(eng.dof_targets.cpu().numpy()[I], g["dof_pos"][I], atol=2e-4)
+    cases.assert_expmap_close(eng.dof_targets.cpu().numpy()[I], g["dof_pos"][I])
     rb = eng.rb_state.view(n, 24, 13).cpu().numpy()[I]
     grb = g["rb_state"][I]
     np.testing.assert_allclose(rb[..., :3], grb[..., :3], atol=2e-6)
@@ -496,9 +496,8 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
         np.testing.assert_array_equal(st.cpu().numpy(), state["start_times"])
         if len(ids):
             np.testing.assert_allclose(eng.root_states.cpu().numpy()[ids, :3], state["root_states"][ids, :3], atol=2e-6)
-            np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[ids, :, 0],
-                                       state["dof_state"][ids, :, 0], atol=2e-4)
-            np.testing.assert_allclose(eng.dof_targets.cpu().numpy()[ids], state["dof_targets"][ids], atol=2e-4)
+            cases.assert_expmap_close(eng.dof_state.view(n, 69, 2).cpu().numpy()[ids, :, 0], state["dof_state"][ids, :, 0])
+            cases.assert_expmap_close(eng.dof_targets.cpu().numpy()[ids], state["dof_targets"][ids])
             assert (eng.contact_forces.view(n, 24, 3).cpu().numpy()[ids] == 0).all()
     assert n_reset > 0, "test should exercise the device reset path"
 

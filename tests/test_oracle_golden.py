@@ -8,11 +8,14 @@ Quaternions are compared up to sign (q and -q are the same rotation; slerp's sig
 the frame pair chosen at exact frame boundaries).
 """
 import numpy as np
+
 import pytest
 
 from humanoid_amd import _abi
 from humanoid_amd.body_sets import EVAL_BODIES, body_ids
 from oracle import oracle as O
+
+import cases
 
 
 def quat_close(a, b, atol):
@@ -64,7 +67,7 @@ def test_motion_state(golden):
     np.testing.assert_allclose(r["body_ang_vel"], g["ms_body_ang_vel"], atol=1e-5)
     np.testing.assert_allclose(r["dof_vel"], g["ms_dof_vel"], atol=1e-5)
     quat_close(r["rb_rot"], g["ms_rb_rot"], 5e-6)
-    np.testing.assert_allclose(r["dof_pos"], g["ms_dof_pos"], atol=2e-4)
+    cases.assert_expmap_close(r["dof_pos"], g["ms_dof_pos"])
     np.testing.assert_allclose(r["rg_pos"][:, 0], g["ms_root_pos"], atol=2e-6)
     r0 = O.motion_state(mt, g["q_ids"], g["q_times"], None)
     np.testing.assert_allclose(r0["rg_pos"], g["msno_rg_pos"], atol=2e-6)
@@ -135,9 +138,9 @@ def test_env_reset_glue(golden):
     np.testing.assert_allclose(rs[:, :3], gr[:, :3], atol=2e-6)
     quat_close(rs[:, 3:7], gr[:, 3:7], 5e-6)
     np.testing.assert_allclose(rs[:, 7:], gr[:, 7:], atol=1e-5)
-    np.testing.assert_allclose(st["dof_state"][ids, :, 0], g["dof_pos"][ids], atol=2e-4)
+    cases.assert_expmap_close(st["dof_state"][ids, :, 0], g["dof_pos"][ids])
     np.testing.assert_allclose(st["dof_state"][ids, :, 1], g["dof_vel"][ids], atol=1e-5)
-    np.testing.assert_allclose(st["dof_targets"][ids], g["dof_pos"][ids], atol=2e-4)
+    cases.assert_expmap_close(st["dof_targets"][ids], g["dof_pos"][ids])
     rb, grb = st["rb_state"][ids], g["rb_state"][ids]
     np.testing.assert_allclose(rb[..., :3], grb[..., :3], atol=2e-6)
     quat_close(rb[..., 3:7], grb[..., 3:7], 5e-6)
