@@ -13,10 +13,12 @@
  *   Math is double precision; the frame-index arithmetic follows the reference's float32 ops
  *   exactly (the oracle is compiled with -ffp-contract=off).
  *
- * Part 2 (physics, A1-A4): the engine's own articulated-body specification.
- *   Isaac Gym/PhysX is closed and absent: PHYSICS PARITY VS PHYSX IS UNPINNED.
- *   This fp64 scalar implementation is the reference the HIP kernel is checked against, and is
- *   itself checked by invariant tests (free fall, momentum, PD equilibrium, contact, refinement).
+ * Part 2 (physics, A1-A4, he_oracle_physics.c): the engine's own articulated-body specification
+ *   (DESIGN.md §5). Isaac Gym/PhysX is closed and absent: PHYSICS PARITY VS PHYSX IS
+ *   UNPINNED. This fp64 scalar implementation is the reference the HIP kernel is checked against,
+ *   and is itself pinned by the invariant tests of tests/test_physics_invariants.py (free fall,
+ *   momentum / angular momentum / energy drift, ballistic CoM, dt refinement, PD stand-still,
+ *   penetration) and tests/test_limits_contacts.py (joint limits, overflow reduction, warm start).
  */
 #include <math.h>
 #include <stdint.h>
