@@ -38,7 +38,7 @@ class HeSimParams(C.Structure):
         ("max_angular_velocity", C.c_float), ("solver_iterations", C.c_int32), ("self_collision", C.c_int32),
         ("max_contacts", C.c_int32), ("kp_scale", C.c_float), ("kd_scale", C.c_float), ("terrain", C.c_int32),
         ("terrain_slope", C.c_float), ("step_height", C.c_float), ("step_length", C.c_float),
-        ("joint_limits", C.c_int32), ("limit_margin", C.c_float), ("warm_start", C.c_int32), ("reserved", C.c_int32),
+        ("joint_limits", C.c_int32), ("limit_margin", C.c_float), ("warm_start", C.c_int32), ("solver_tolerance", C.c_float),
     ]
 
 
@@ -113,6 +113,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.joint_limits = 1  # the MJCF ranges, enforced by PhysX (humanoid_phc.py:305-324)
     p.limit_margin = 0.1
     p.warm_start = 1
+    p.solver_tolerance = 0.0
     for k, v in kw.items():
         setattr(p, k, v)
     return p

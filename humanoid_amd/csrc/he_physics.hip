@@ -1804,10 +1804,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const float muL = lane < nr ? L.cmu[lane / 3] : 0.f;
             const int ncu = __builtin_amdgcn_readfirstlane(nc);
             __builtin_amdgcn_s_setprio(HE_PRIO_PGS);
+            const float tol = p.solver_tolerance;
             for (int it = 0; it < p.solver_iterations; ++it) {
                 float dvec = 0.f;
                 pgs_sweep<0>(cd, dvec, lamv, acol, muL, ncu);
                 lamv += dvec;
+                // converged (optional, solver_tolerance > 0): no row's velocity moved by more than
+                // the tolerance in this sweep, |d lambda_r| A_rr (oracle: the same test)
+                if (tol > 0.f && __ballot(lane < nr && fabsf(dvec) * diag > tol) == 0ull) break;
             }
             __builtin_amdgcn_s_setprio(0);
         }

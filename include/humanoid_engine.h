@@ -78,7 +78,8 @@ typedef struct he_sim_params {
     int32_t joint_limits;            /* 1: unilateral limit rows on the dof ranges (PhysX limits) */
     float limit_margin;              /* rad: a limit row is emitted within margin + dt*closing rate */
     int32_t warm_start;              /* 1: the solver starts from the previous solve's impulses */
-    int32_t reserved;
+    float solver_tolerance;          /* m/s: stop the sweeps once no row's velocity moves by more
+                                        (|d lambda_r| A_rr) in a sweep; 0 = always solver_iterations */
 } he_sim_params;
 
 /* Per-env solver warm-start cache (f32 words; HE_BUF_CONTACT_CACHE), written at the end of every

@@ -537,6 +537,7 @@ typedef struct step_out {
     int num_contacts;
     int dropped;          /* contacts generated past the capacity (last substep) */
     R residual;           /* max |complementarity residual| of the last substep's solve (m/s) */
+    int sweeps;           /* Gauss-Seidel sweeps of the last substep's solve */
 } step_out;
 
 /* Warm-start cache: the previous solve's impulses by contact key (PhysX warm-starts its solver
@@ -712,7 +713,11 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                         for (int x = 0; x < 3; ++x) lam[3 * ci + x] = ws->lam[j][x];
                         break;
                     }
+        int sweeps = 0;
         for (int it = 0; it < p->solver_iterations; ++it) {
+            R lam_prev[MAXROW];
+            memcpy(lam_prev, lam, sizeof(R) * nr);
+            ++sweeps;
             for (int ci = 0; ci < nc; ++ci) {
                 int r0 = 3 * ci;
                 R w = brow[r0];
@@ -728,7 +733,18 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                     lam[r] = lt > bound ? bound : (lt < -bound ? -bound : lt);
                 }
             }
+            /* converged: no row's velocity moved by more than solver_tolerance in this sweep
+             * (|d lambda_r| A_rr); 0 runs every sweep */
+            if (p->solver_tolerance > 0) {
+                R mx = 0;
+                for (int r = 0; r < nr; ++r) {
+                    R dv = fabs(lam[r] - lam_prev[r]) * A[r][r];
+                    if (dv > mx) mx = dv;
+                }
+                if (mx <= p->solver_tolerance) break;
+            }
         }
+        out->sweeps = sweeps;
         /* complementarity residual of the returned impulses: normal rows min(w, lambda) -> 0,
          * friction rows w = 0 inside the cone (or lambda on the bound) */
         for (int ci = 0; ci < nc; ++ci) {
@@ -824,12 +840,13 @@ static void write_rb(const he_model* m, const topo* t, const env_state* s, float
 /* gym.simulate x substeps for n envs. root_states [N,13], dof_state [N,69,2] (in/out),
  * targets [N,69]; outputs rb_state [N,24,13], contact_forces [N,24,3], dof_force [N,69],
  * num_contacts [N] (nullable). mass_scale [N,24], friction [N], terrain_kind [N] nullable.
- * cache [N,HE_CACHE_WORDS] (in/out, nullable: cold solves), dropped [N] and residual [N] (out,
- * nullable): contacts past the capacity and the solve's residual, both of the last substep. */
+ * cache [N,HE_CACHE_WORDS] (in/out, nullable: cold solves), dropped [N], residual [N] and
+ * sweeps [N] (out, nullable): contacts past the capacity, the solve's residual and its sweep count,
+ * all of the last substep. */
 void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* root_states, float* dof_state,
                      const float* targets, int substeps, float* rb_state, float* contact_forces, float* dof_force,
                      int32_t* num_contacts, const float* mass_scale, const float* friction, const int32_t* terrain_kind,
-                     float* cache, int32_t* dropped, float* residual) {
+                     float* cache, int32_t* dropped, float* residual, int32_t* sweeps) {
     topo t;
     build_topo(m, &t);
 #pragma omp parallel for schedule(dynamic, 4)
@@ -877,6 +894,7 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         if (num_contacts) num_contacts[e] = out.num_contacts;
         if (dropped) dropped[e] = out.dropped;
         if (residual) residual[e] = (float)out.residual;
+        if (sweeps) sweeps[e] = out.sweeps;
         if (cw) {
             memset(cw, 0, HE_CACHE_WORDS * sizeof(float));
             if (p->warm_start) {

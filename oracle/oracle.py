@@ -143,14 +143,14 @@ def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, do
         assert cache.dtype == np.float32 and cache.flags.c_contiguous and cache.shape == (n, _abi.CACHE_WORDS)
     out = dict(rb_state=np.zeros((n, 24, 13), np.float32), contact_forces=np.zeros((n, 24, 3), np.float32),
                dof_force=np.zeros((n, 69), np.float32), num_contacts=np.zeros(n, np.int32),
-               dropped=np.zeros(n, np.int32), residual=np.zeros(n, np.float32))
+               dropped=np.zeros(n, np.int32), residual=np.zeros(n, np.float32), sweeps=np.zeros(n, np.int32))
     ms = None if mass_scale is None else f32(mass_scale)
     fr = None if friction is None else f32(friction)
     tk = None if terrain_kind is None else np.ascontiguousarray(terrain_kind, np.int32)
     lib().ho_physics_step(C.byref(model), C.byref(sim), C.c_int(n), _p(root_states), _p(dof_state), _p(f32(targets)),
                           C.c_int(substeps), _p(out["rb_state"]), _p(out["contact_forces"]), _p(out["dof_force"]),
                           _p(out["num_contacts"]), _p(ms), _p(fr), _p(tk), _p(cache), _p(out["dropped"]),
-                          _p(out["residual"]))
+                          _p(out["residual"]), _p(out["sweeps"]))
     return out
 
 

@@ -363,6 +363,15 @@ def test_physics_contact_rich_matches_oracle(he_model):
     _physics_compare(he_model, root, dof, targets)
 
 
+def test_physics_solver_tolerance_matches_oracle(he_model):
+    """The optional convergence stop (solver_tolerance = 1e-5 m/s: a sweep that moves no row's
+    velocity by more ends the solve) on contact-rich states, 5 steps: the same stop in both."""
+    rng = np.random.default_rng(13)
+    root, dof = cases.random_state(64, rng, height=(0.85, 1.0), ang=0.8, vel=0.5)
+    targets = rng.uniform(-0.5, 0.5, (64, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, steps=5, solver_tolerance=1e-5)
+
+
 def test_physics_domain_randomised_terrain(he_model, model):
     """Config 5 extension: per-env mass scale, friction and terrain kind vs the oracle, 3 steps,
     positions and velocities."""
