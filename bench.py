@@ -29,6 +29,7 @@ FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector = FP32 matrix 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 # SURVEY.md §8(d) canonical algorithmic counts per env-step
 PHYS_FLOP_PER_ENV_STEP = 1_309_278          # dense-equivalent physics, 2 substeps, n_c = 8
+FUSED_FLOP_PER_ENV_STEP = PHYS_FLOP_PER_ENV_STEP + 30_000  # + the imitation step (≈0.03 MFLOP)
 IMIT_BYTES_PER_ENV_STEP = 13_200            # fused imitation kernel share of the 16.0 KB/env-step
 
 
@@ -48,6 +49,9 @@ def parse(argv=None):
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
+    ap.add_argument("--fused", action="store_true",
+                    help="he_env_step as one launch (the imitation step in the physics kernel's epilogue); "
+                         "at 4096 envs the two launches are faster (DESIGN §4.1)")
     ap.add_argument("--no-tracking", action="store_true",
                     help="skip the configs[2] tracking-action leg (throughput + joint-pose L2 vs ref)")
     return ap.parse_args(argv)
@@ -123,6 +127,7 @@ class Rollout:
         from humanoid_amd.body_sets import frozen_dof_mask
         self.args = args
         self.model = model
+        self.fused = bool(getattr(args, "fused", False))
         n = args.num_envs
         tables, actions, rng = build_workload(args, model, rank)
         sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0)
@@ -155,6 +160,7 @@ class Rollout:
         ids = torch.arange(n, dtype=torch.int32, device=dev)
         phases = torch.as_tensor(rng.uniform(0, 1, n).astype(np.float32), device=dev)
         self.eng.reset_envs(self.p, self.em, ids, phases, self.obs, self.reset, self.term)
+        self.eng.set_fused_step(self.fused)
 
     def tracking_actions(self):
         """a = clip(ref_dof_pos / scale, -1, 1) with the reference pose at
@@ -178,17 +184,28 @@ class Rollout:
         return (q - ref).norm(dim=1)
 
     def step(self, ev=None):
-        """ev: optional (start, mid, end) torch.cuda.Events around the two kernels."""
+        """One he_env_step (fused: one launch; `--unfused`: the physics and imitation launches).
+        ev: optional (start, mid, end) torch.cuda.Events; unfused, mid splits the two kernels."""
         if ev is not None:
             ev[0].record()
-        self.eng.step_actions(self.actions, 2)
-        if ev is not None:
-            ev[1].record()
-        self.eng.imitation_reset_step(self.p, self.em, self.obs, self.rew, self.raw, self.reset, self.term,
-                                      seed=self.seed, step_index=self.step_index)
+        if self.fused:
+            self.eng.env_step(self.p, self.em, self.actions, self.obs, self.rew, self.raw, self.reset, self.term,
+                              seed=self.seed, step_index=self.step_index)
+            if ev is not None:
+                ev[1].record()
+        else:
+            self.eng.step_actions(self.actions, 2)
+            if ev is not None:
+                ev[1].record()
+            self.eng.imitation_reset_step(self.p, self.em, self.obs, self.rew, self.raw, self.reset, self.term,
+                                          seed=self.seed, step_index=self.step_index)
         if ev is not None:
             ev[2].record()
         self.step_index += 1
+
+    def set_fused(self, fused):
+        self.fused = bool(fused)
+        self.eng.set_fused_step(self.fused)
 
 
 def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
@@ -329,8 +346,21 @@ def main():
     elapsed = time.perf_counter() - t0
     nc = ro.eng.num_contacts.cpu().numpy()
     dropped = ro.eng.dropped_contacts.cpu().numpy()
+    step_ms = float(np.mean([e[0].elapsed_time(e[2]) for e in evs.values()]))
     phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs.values()]))
     imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs.values()]))
+    # the two kernels apart (unfused form, a short sampled pass after the timed region), for the
+    # physics kernel's own roofline and the imitation kernel's HBM share
+    split = None
+    if ro.fused:
+        ro.set_fused(False)
+        sev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(10)]
+        for k in range(20):
+            ro.step(sev[k // 2] if k % 2 else None)
+        torch.cuda.synchronize()
+        split = (float(np.mean([e[0].elapsed_time(e[1]) for e in sev])),
+                 float(np.mean([e[1].elapsed_time(e[2]) for e in sev])))
+        ro.set_fused(True)
     if world > 1:
         t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -339,6 +369,9 @@ def main():
     total_steps = n * args.steps * world
     value = total_steps / elapsed
     if rank == 0:
+        if split is not None:  # fused: the one launch is the dominant kernel
+            fused_ms = step_ms
+            phys_ms, imit_ms = split
         phys_tflops = PHYS_FLOP_PER_ENV_STEP * n / (phys_ms * 1e-3) / 1e12
         imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
         traffic = imit_traffic = mfma = None
@@ -362,6 +395,22 @@ def main():
                     imit_traffic = tr[key].get("imitation_bytes_per_launch")
             except Exception:
                 traffic = imit_traffic = None
+        # the physics kernel alone (the unfused launch): latency-bound, priced against the FP32
+        # vector / matrix peak with the canonical dense-equivalent flop count; mfma_util is the
+        # measured matrix-core busy share (rocprofv3 SQ counters)
+        phys_roof = {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
+                     "kernel": "physics_kernel (fp32 VALU + MFMA; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
+                     "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma}
+        if split is not None:  # the fused launch (physics + the imitation epilogue) is the dominant kernel
+            f_tflops = FUSED_FLOP_PER_ENV_STEP * n / (fused_ms * 1e-3) / 1e12
+            roof = {"bound": "latency", "achieved": round(f_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(f_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
+                    "kernel": "physics_kernel, fused he_env_step (physics + imitation epilogue; canonical "
+                              "1.309 + 0.03 MFLOP/env-step, SURVEY §8d)",
+                    "avg_launch_ms": round(fused_ms, 4), "mfma_util": mfma}
+        else:
+            roof = phys_roof
         line = {
             "metric": "env-steps/sec (4096 SMPL humanoids per GPU)",
             "value": round(value, 1),
@@ -384,16 +433,15 @@ def main():
             # Gauss-Seidel sweeps, triangular solves) at 2 waves / SIMD, not by HBM or the matrix
             # cores: priced against the FP32 vector / matrix peak with the canonical dense-equivalent
             # flop count; mfma_util is the measured matrix-core busy share (rocprofv3 SQ counters)
-            "roofline": {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                         "kernel": "physics_kernel (fp32 VALU + MFMA; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
-                         "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma},
+            "roofline": roof,
             "contacts": {"slots_mean": round(float(nc.mean()), 3), "slots_max": int(nc.max()),
                          "capacity": args.max_contacts, "envs_dropping": int((dropped > 0).sum()),
                          "dropped_mean": round(float(dropped.mean()), 4)},
-            "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(imit_gbs / HBM_PEAK_GBS, 5), "avg_launch_ms": round(imit_ms, 4),
-                                 "traffic": imit_traffic},
+            "unfused_kernels": {
+                "physics_kernel": phys_roof,
+                "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS,
+                                     "unit": "GB/s", "frac": round(imit_gbs / HBM_PEAK_GBS, 5),
+                                     "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic}},
         }
         if not args.no_tracking and world == 1 and args.num_envs == 4096:
             try:

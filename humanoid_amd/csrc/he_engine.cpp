@@ -64,6 +64,7 @@ struct he_engine {
     int32_t* dropped = nullptr;
     float* cache = nullptr;
     bool component_limits = false;  // a dof bound inside (-pi + guard, pi - guard): not implemented
+    int fused_step = -1;            // he_env_step as one launch: 1 / 0 (he_set_fused_step), -1 auto
     const float *mass_scale = nullptr, *friction = nullptr;
     const int32_t* terrain_kind = nullptr;
     float *pd_offset = nullptr, *pd_scale = nullptr;
@@ -549,8 +550,42 @@ int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motio
 int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, const float* actions,
                 int substeps, uint64_t seed, uint64_t step_index, float* obs, float* rew, float* reward_raw,
                 uint8_t* reset, uint8_t* terminate, void* stream) {
-    if (he_step_actions(h, actions, substeps, stream)) return 1;
-    return he_imitation_reset_step(h, p, em, seed, step_index, obs, rew, reward_raw, reset, terminate, stream);
+    if (!h || !h->num_envs || !actions) return fail("he_env_step: bad arguments");
+    // auto: one launch while the envs fit one round of waves on the chip (2 per SIMD: launch and
+    // tail latency dominate there); past it two launches, because the imitation step at one env
+    // per 250-VGPR wave adds more than the stand-alone kernel costs at full occupancy (r02 A/B at
+    // 4096 envs: 0.218 against 0.209 ms per step)
+    const bool fused = h->fused_step == 1 || (h->fused_step < 0 && h->num_envs <= 2048);
+    if (h->has_eval || !fused) {  // eval recording lives in the stand-alone imitation kernel
+        if (he_step_actions(h, actions, substeps, stream)) return 1;
+        return he_imitation_reset_step(h, p, em, seed, step_index, obs, rew, reward_raw, reset, terminate, stream);
+    }
+    // one launch: actions -> PD targets -> physics -> the imitation step with the device reset of
+    // flagged envs in the physics kernel's epilogue (the same results as the two launches)
+    if (!h->has_pd) return fail("he_env_step: call he_set_pd_params first");
+    if (substeps < 1) return fail("he_env_step: substeps must be >= 1");
+    if (h->params.joint_limits && h->component_limits)
+        return fail("he_env_step: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
+    ImitArgs a;
+    if (imit_common(h, p, em, a, "he_env_step")) return 1;
+    if (!obs || !rew || !reward_raw || !reset || !terminate) return fail("he_env_step: null output");
+    a.obs = obs; a.rew = rew; a.reward_raw = reward_raw; a.reset = reset; a.terminate = terminate;
+    a.count = h->num_envs;
+    a.mode = 1;
+    a.seed = seed;
+    a.step = step_index;
+    PhysArgs pa = phys_args(h, substeps, actions);
+    pa.fused = 1;
+    pa.im = a;
+    HE_CHECK(launch_physics(pa, (hipStream_t)stream));
+    HE_CHECK(amp_after(h, a, 1, (hipStream_t)stream));
+    return 0;
+}
+
+int he_set_fused_step(he_engine* h, int enable) {
+    if (!h) return fail("he_set_fused_step: null engine");
+    h->fused_step = enable < 0 ? -1 : (enable != 0);
+    return 0;
 }
 
 int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, uint64_t seed,

@@ -22,179 +22,7 @@ constexpr int GROUP = 32;
 constexpr int HOT = HE_MOTION_HOT;    // floats per body in a hot frame record
 constexpr int COLD = HE_MOTION_COLD;  // floats per body in a cold frame record
 
-HE_DEV float group_sum(float v) {
-#pragma unroll
-    for (int o = GROUP / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, GROUP);
-    return v;
-}
-HE_DEV float group_max(float v) {
-#pragma unroll
-    for (int o = GROUP / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, GROUP));
-    return v;
-}
-HE_DEV float bcast0(float v) { return __shfl(v, 0, GROUP); }
-
-struct FrameSel {
-    int64_t g0, g1;
-    float blend;
-};
-
-// motion_lib.py:655-665 in float32
-HE_DEV int64_t clamp_mid(const MotionDev& m, int64_t mid) {
-    return mid < 0 ? 0 : (mid >= m.num_motions ? (int64_t)m.num_motions - 1 : mid);
-}
-
-struct MotionMeta {
-    float len, dt;
-    int64_t nf, start;
-};
-
-HE_DEV MotionMeta motion_meta(const MotionDev& m, int64_t mid) {  // mid already clamped
-    return MotionMeta{m.lengths[mid], m.dt[mid], m.num_frames[mid], m.length_starts[mid]};
-}
-
-HE_DEV FrameSel frame_select(const MotionMeta& mm, float time) {
-    const float len = mm.len, dt = mm.dt;
-    const int64_t nf = mm.nf;
-    float phase = time / len;
-    phase = phase < 0.0f ? 0.0f : (phase > 1.0f ? 1.0f : phase);
-    if (time < 0.0f) time = 0.0f;
-    int64_t f0 = (int64_t)(phase * (float)(nf - 1));
-    int64_t f1 = f0 + 1 < nf - 1 ? f0 + 1 : nf - 1;
-    float bl = (time - (float)f0 * dt) / dt;
-    bl = bl < 0.0f ? 0.0f : (bl > 1.0f ? 1.0f : bl);
-    return FrameSel{mm.start + f0, mm.start + f1, bl};
-}
-
-HE_DEV FrameSel frame_select(const MotionDev& m, int64_t mid, float time) {
-    mid = clamp_mid(m, mid);
-    float len = m.lengths[mid];
-    int64_t nf = m.num_frames[mid];
-    float dt = m.dt[mid];
-    float phase = time / len;
-    phase = phase < 0.0f ? 0.0f : (phase > 1.0f ? 1.0f : phase);
-    if (time < 0.0f) time = 0.0f;
-    int64_t f0 = (int64_t)(phase * (float)(nf - 1));
-    int64_t f1 = f0 + 1 < nf - 1 ? f0 + 1 : nf - 1;
-    float bl = (time - (float)f0 * dt) / dt;
-    bl = bl < 0.0f ? 0.0f : (bl > 1.0f ? 1.0f : bl);
-    int64_t s = m.length_starts[mid];
-    return FrameSel{s + f0, s + f1, bl};
-}
-
-struct BodyRef {
-    f3 pos, vel, ang;
-    f4 rot;
-};
-
-// motion_lib.py:577-610 for one body
-HE_DEV BodyRef body_ref(const MotionDev& m, const FrameSel& fs, int b, f3 off) {
-    const float* r0 = m.hot + (fs.g0 * NB + b) * HOT;
-    const float* r1 = m.hot + (fs.g1 * NB + b) * HOT;
-    float bl = fs.blend, a = 1.0f - bl;
-    BodyRef o;
-    o.pos = f3{a * r0[0] + bl * r1[0], a * r0[1] + bl * r1[1], a * r0[2] + bl * r1[2]};
-    o.pos = o.pos + off;
-    o.rot = slerp_ref(f4{r0[3], r0[4], r0[5], r0[6]}, f4{r1[3], r1[4], r1[5], r1[6]}, bl);
-    o.vel = f3{a * r0[7] + bl * r1[7], a * r0[8] + bl * r1[8], a * r0[9] + bl * r1[9]};
-    o.ang = f3{a * r0[10] + bl * r1[10], a * r0[11] + bl * r1[11], a * r0[12] + bl * r1[12]};
-    return o;
-}
-
-// local rotation slerp -> exp-map dof pos, dof vel lerp (motion_lib.py:562-606, 670-673)
-HE_DEV void body_dof_ref(const MotionDev& m, const FrameSel& fs, int b, f3& dpos, f3& dvel) {
-    const float* c0 = m.cold + (fs.g0 * NB + b) * COLD;
-    const float* c1 = m.cold + (fs.g1 * NB + b) * COLD;
-    float bl = fs.blend, a = 1.0f - bl;
-    f4 lr = slerp_ref(f4{c0[0], c0[1], c0[2], c0[3]}, f4{c1[0], c1[1], c1[2], c1[3]}, bl);
-    dpos = q_to_exp_map(lr);
-    dvel = f3{a * c0[4] + bl * c1[4], a * c0[5] + bl * c1[5], a * c0[6] + bl * c1[6]};
-}
-
-HE_DEV float env_time(int progress, float cdt, float start, float off) {
-    float t = (float)progress * cdt;
-    t = t + start;
-    t = t + off;
-    return t;
-}
-
-struct SimBody {
-    f3 pos, vel, ang;
-    f4 rot;
-};
-
-HE_DEV SimBody load_body(const float* rb) {
-    SimBody s;
-    s.pos = f3{rb[0], rb[1], rb[2]};
-    s.rot = f4{rb[3], rb[4], rb[5], rb[6]};
-    s.vel = f3{rb[7], rb[8], rb[9]};
-    s.ang = f3{rb[10], rb[11], rb[12]};
-    return s;
-}
-
-// common.py:22-103 (self) and :106-176 (task, time_steps=1) for body b of one env
-HE_DEV void write_obs(float* o, int b, const SimBody& s, f3 root_pos, f4 hinv, f4 hq, const BodyRef& r) {
-    float tn[6];
-    if (b == 0) o[0] = root_pos.z;
-    if (b > 0) {
-        f3 lp = qrot_ref(hinv, s.pos - root_pos);
-        o[1 + (b - 1) * 3 + 0] = lp.x; o[1 + (b - 1) * 3 + 1] = lp.y; o[1 + (b - 1) * 3 + 2] = lp.z;
-    }
-    tan_norm(qmul_ref(hinv, s.rot), tn);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) o[70 + b * 6 + c] = tn[c];
-    f3 v = qrot_ref(hinv, s.vel);
-    o[214 + b * 3 + 0] = v.x; o[214 + b * 3 + 1] = v.y; o[214 + b * 3 + 2] = v.z;
-    v = qrot_ref(hinv, s.ang);
-    o[286 + b * 3 + 0] = v.x; o[286 + b * 3 + 1] = v.y; o[286 + b * 3 + 2] = v.z;
-    float* t = o + HE_OBS_SELF;
-    v = qrot_ref(hinv, r.pos - s.pos);
-    t[b * 3 + 0] = v.x; t[b * 3 + 1] = v.y; t[b * 3 + 2] = v.z;
-    f4 dq = qmul_ref(qmul_ref(hinv, qmul_ref(r.rot, qconj(s.rot))), hq);
-    tan_norm(dq, tn);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) t[72 + b * 6 + c] = tn[c];
-    v = qrot_ref(hinv, r.vel - s.vel);
-    t[216 + b * 3 + 0] = v.x; t[216 + b * 3 + 1] = v.y; t[216 + b * 3 + 2] = v.z;
-    v = qrot_ref(hinv, r.ang - s.ang);
-    t[288 + b * 3 + 0] = v.x; t[288 + b * 3 + 1] = v.y; t[288 + b * 3 + 2] = v.z;
-    v = qrot_ref(hinv, r.pos - root_pos);
-    t[360 + b * 3 + 0] = v.x; t[360 + b * 3 + 1] = v.y; t[360 + b * 3 + 2] = v.z;
-    tan_norm(qmul_ref(hinv, r.rot), tn);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) t[432 + b * 6 + c] = tn[c];
-}
-
-// humanoid_phc.py:694-731 + 747-780 + 901-931 for body b of env e: set the env to the
-// reference state at time t (offset = the env's pre-reset global offset, :858-860)
-HE_DEV void reset_body(const ImitArgs& a, int e, int b, int64_t mid, float t, f3 off) {
-    FrameSel fs = frame_select(a.m, mid, t);
-    BodyRef r = body_ref(a.m, fs, b, off);
-    float* rb = a.rb_state + ((size_t)e * NB + b) * 13;
-    rb[0] = r.pos.x; rb[1] = r.pos.y; rb[2] = r.pos.z;
-    rb[3] = r.rot.x; rb[4] = r.rot.y; rb[5] = r.rot.z; rb[6] = r.rot.w;
-    rb[7] = r.vel.x; rb[8] = r.vel.y; rb[9] = r.vel.z;
-    rb[10] = r.ang.x; rb[11] = r.ang.y; rb[12] = r.ang.z;
-    if (a.contact_forces) {
-        float* cf = a.contact_forces + ((size_t)e * NB + b) * 3;
-        cf[0] = cf[1] = cf[2] = 0.0f;
-    }
-    if (b == 0) {
-        float* rs = a.root_states + (size_t)e * 13;
-#pragma unroll
-        for (int c = 0; c < 13; ++c) rs[c] = rb[c];
-    } else {
-        f3 dp, dv;
-        body_dof_ref(a.m, fs, b, dp, dv);
-        int d = 3 * (b - 1);
-        float* ds = a.dof_state + ((size_t)e * ND + d) * 2;
-        ds[0] = dp.x; ds[1] = dv.x; ds[2] = dp.y; ds[3] = dv.y; ds[4] = dp.z; ds[5] = dv.z;
-        if (a.dof_targets) {
-            float* tg = a.dof_targets + (size_t)e * ND + d;
-            tg[0] = dp.x; tg[1] = dp.y; tg[2] = dp.z;
-        }
-    }
-}
+#include "he_imitation_env.h"
 
 // ---------------- eval-mode recording (include/humanoid_engine.h he_eval_buffers)
 HE_DEV double group_sum_d(double v) {
@@ -361,101 +189,9 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
     if (a.mode != 2 && p.use_power_reward && lane < NB - 1) {  // humanoid_phc.py:1297-1305
         const float* f = a.dof_force + (size_t)e * ND + 3 * lane;
         const float* v = a.dof_state + ((size_t)e * ND + 3 * lane) * 2 + 1;
-        pw = fabsf(f[0] * v[0]) + fabsf(f[1] * v[2]) + fabsf(f[2] * v[4]);
+        pw = power_term(f, v, 2);
     }
-    // trip 2: the motion's metadata; trip 3: both samples' frame records
-    const MotionMeta mm = motion_meta(a.m, mid);
-    bool do_reset = false;
-    float reset_time = 0.0f;
-    if (a.mode != 2) prog += 1;  // post-physics half of HumanoidPHC.step (humanoid_phc.py:138-149)
-    const float t = env_time(prog, p.control_dt, start, soff);
-    const BodyRef r = body_ref(a.m, frame_select(mm, t), b, off);
-    BodyRef r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
-
-    if (a.mode != 2) {
-        // reward terms, common.py:298-317
-        f3 d = r.pos - s.pos;
-        float dp = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
-        d = r.vel - s.vel;
-        float dv = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
-        d = r.ang - s.ang;
-        float da = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
-        float ang = q_angle_axis(qmul_ref(r.rot, qconj(s.rot)), nullptr);
-        float dr = act ? ang * ang : 0.0f;
-        dp = group_sum(dp) / NB;
-        dv = group_sum(dv) / NB;
-        da = group_sum(da) / NB;
-        dr = group_sum(dr) / NB;
-        float rp = expf(-p.k_pos * dp), rr = expf(-p.k_rot * dr), rv = expf(-p.k_vel * dv), ra = expf(-p.k_ang_vel * da);
-        float rew = p.w_pos * rp + p.w_rot * rr + p.w_vel * rv + p.w_ang_vel * ra;
-        float pr = 0.0f;
-        if (p.use_power_reward) {
-            pw = group_sum(pw);
-            pr = -p.power_coef * pw;
-            if (prog <= 3) pr = 0.0f;
-            rew += pr;
-        }
-        // termination, common.py:325-364 + humanoid_phc.py:1313-1335
-        bool pass_time = t >= mm.len;
-        bool fallen = false;
-        if (p.enable_early_termination) {
-            bool inset = act && ((p.reset_body_mask >> b) & 1);
-            float dist = norm3(s.pos - r.pos);
-            if (p.eval_mode) {
-                float sum = group_sum(inset ? dist : 0.0f);
-                float cnt = group_sum(inset ? 1.0f : 0.0f);
-                int first = __ffs(p.reset_body_mask) - 1;
-                fallen = cnt > 0.0f && (sum / cnt) > p.term_dist[first < 0 ? 0 : first];
-            } else {
-                fallen = group_max(inset && dist > p.term_dist[b] ? 1.0f : 0.0f) > 0.0f;
-            }
-            fallen = fallen && prog > 1;
-        }
-        bool reset = pass_time || fallen;
-        if (EVAL) eval_record(a.ev, e, lane, act, s.pos, r.pos);  // before any fused reset
-        if (lane == 0) {
-            a.rew[e] = rew;
-            float* raw = a.reward_raw + (size_t)e * HE_REWARD_RAW;
-            raw[0] = rp; raw[1] = rr; raw[2] = rv; raw[3] = ra; raw[4] = pr;
-            a.reset[e] = reset;
-            a.terminate[e] = fallen;
-            a.progress[e] = (int16_t)prog;
-        }
-        if (a.mode == 1 && reset) {
-            do_reset = true;
-            // Random: sample_time_interval of a hashed phase; Start (and test mode): time 0
-            // (humanoid_phc.py:848-852)
-            float ph = a.p.state_init == 1 ? 0.f : hash_uniform(a.seed, a.step, (uint32_t)e);
-            reset_time = sample_time_interval(ph, mm.len);
-        }
-    } else {
-        do_reset = true;
-        reset_time = sample_time_interval(a.phases[slot], mm.len);
-    }
-
-    if (do_reset) {  // the group's branch is uniform
-        if (act) reset_body(a, e, b, mid, reset_time, off);
-        off = f3{0.f, 0.f, 0.f};
-        start = reset_time;
-        soff = 0.0f;
-        prog = 0;
-        if (lane == 0) {
-            a.global_offset[3 * e] = 0.0f; a.global_offset[3 * e + 1] = 0.0f; a.global_offset[3 * e + 2] = 0.0f;
-            a.start_times[e] = reset_time;
-            a.start_offsets[e] = 0.0f;
-            a.progress[e] = 0;
-            if (a.mode == 2) { a.reset[e] = 0; a.terminate[e] = 0; }
-        }
-        s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);  // the row this lane just wrote
-        r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
-    }
-
-    // ---------------- observations for the next step (humanoid_phc.py:937-961, 1063-1067)
-    f3 root_pos = f3{bcast0(s.pos.x), bcast0(s.pos.y), bcast0(s.pos.z)};
-    f4 root_rot = f4{bcast0(s.rot.x), bcast0(s.rot.y), bcast0(s.rot.z), bcast0(s.rot.w)};
-    float h = calc_heading(root_rot);
-    f4 hinv = heading_quat(-h), hq = heading_quat(h);
-    if (act) write_obs(a.obs + (size_t)e * HE_OBS_DIM, b, s, root_pos, hinv, hq, r2);
+    imitation_group<EVAL>(a, slot, e, lane, lane == 0, mid, off, start, soff, prog, s, pw);
 }
 
 // MotionLibBase.get_motion_state for K queries (motion_lib.py:549-626)

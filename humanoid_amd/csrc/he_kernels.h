@@ -101,6 +101,8 @@ struct PhysArgs {
     int num_envs;
     int substeps;
     unsigned long long* stamps;  // diagnostics: [N][16] phase cycles or null
+    int fused;                   // 1: the imitation step (mode 1) runs in the epilogue (he_env_step)
+    ImitArgs im;                 // its arguments when fused
 };
 
 hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream);

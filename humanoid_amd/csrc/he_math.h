@@ -6,6 +6,10 @@
 #include <stdint.h>
 
 #define HE_DEV __device__ __forceinline__
+// The imitation helpers (*_ref, tan_norm, angle / exp maps, heading, the reset-time hash) follow the
+// reference's float32 torch rounding: each body carries `#pragma clang fp contract(off)`, so no
+// multiply-add is fused even when they are inlined into a TU compiled with contraction (the physics
+// kernel's fused imitation epilogue).
 
 struct f3 { float x, y, z; };
 struct f4 { float x, y, z, w; };
@@ -22,6 +26,7 @@ HE_DEV f4 qneg(f4 q) { return f4{-q.x, -q.y, -q.z, -q.w}; }
 
 // torch_utils.py:54-75 (8-multiplication form)
 HE_DEV f4 qmul_ref(f4 a, f4 b) {
+#pragma clang fp contract(off)
     float x1 = a.x, y1 = a.y, z1 = a.z, w1 = a.w, x2 = b.x, y2 = b.y, z2 = b.z, w2 = b.w;
     float ww = (z1 + x1) * (x2 + y2);
     float yy = (w1 - y1) * (w2 + z2);
@@ -37,9 +42,11 @@ HE_DEV f4 qmul_ref(f4 a, f4 b) {
 
 // torch_utils.py:273-281 my_quat_rotate
 HE_DEV f3 qrot_ref(f4 q, f3 v) {
+#pragma clang fp contract(off)
     float s = 2.0f * (q.w * q.w) - 1.0f;
-    f3 qv = f3{q.x, q.y, q.z};
-    f3 c = cross3(qv, v);
+    // the cross product written out here (cross3 is a shared helper, compiled with contraction in
+    // the physics TU)
+    f3 c = f3{q.y * v.z - q.z * v.y, q.z * v.x - q.x * v.z, q.x * v.y - q.y * v.x};
     float d = v.x * q.x + v.y * q.y + v.z * q.z;
     return f3{v.x * s + c.x * q.w * 2.0f + q.x * d * 2.0f, v.y * s + c.y * q.w * 2.0f + q.y * d * 2.0f,
               v.z * s + c.z * q.w * 2.0f + q.z * d * 2.0f};
@@ -47,15 +54,19 @@ HE_DEV f3 qrot_ref(f4 q, f3 v) {
 
 // torch_utils.py:284-297: (tan, norm) = (q*ex, q*ez)
 HE_DEV void tan_norm(f4 q, float* o) {
+#pragma clang fp contract(off)
     f3 t = qrot_ref(q, f3{1.f, 0.f, 0.f});
     f3 n = qrot_ref(q, f3{0.f, 0.f, 1.f});
     o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = n.x; o[4] = n.y; o[5] = n.z;
 }
 
-HE_DEV float normalize_angle(float x) { return atan2f(sinf(x), cosf(x)); }
+HE_DEV float normalize_angle(float x) {
+#pragma clang fp contract(off)
+    return atan2f(sinf(x), cosf(x)); }
 
 // torch_utils.py:85-106 -- angle; axis written when non-null
 HE_DEV float q_angle_axis(f4 q, f3* axis) {
+#pragma clang fp contract(off)
     float s = sqrtf(1.0f - q.w * q.w);
     float angle = normalize_angle(2.0f * acosf(q.w));
     bool mask = fabsf(s) > 1e-5f;  // NaN -> false
@@ -65,6 +76,7 @@ HE_DEV float q_angle_axis(f4 q, f3* axis) {
 
 // torch_utils.py:143-150
 HE_DEV f3 q_to_exp_map(f4 q) {
+#pragma clang fp contract(off)
     f3 ax;
     float a = q_angle_axis(q, &ax);
     return ax * a;
@@ -73,6 +85,7 @@ HE_DEV f3 q_to_exp_map(f4 q) {
 // torch_utils.py:334-365 exp_map_to_quat = exp_map_to_angle_axis + quat_from_angle_axis
 // (normalize and quat_unit clamp the norm at 1e-9), float32 in torch's operation order
 HE_DEV f4 exp_map_to_quat_ref(f3 e) {
+#pragma clang fp contract(off)
     float angle = sqrtf(e.x * e.x + e.y * e.y + e.z * e.z);
     f3 axis = f3{e.x / angle, e.y / angle, e.z / angle};
     angle = normalize_angle(angle);
@@ -87,6 +100,7 @@ HE_DEV f4 exp_map_to_quat_ref(f3 e) {
 
 // torch_utils.py:109-131 in torch's float32 operation order (sequential dot product)
 HE_DEV f4 slerp_ref(f4 q0, f4 q1, float t) {
+#pragma clang fp contract(off)
     float c = q0.x * q1.x;
     c = c + q0.y * q1.y;
     c = c + q0.z * q1.z;
@@ -105,11 +119,13 @@ HE_DEV f4 slerp_ref(f4 q0, f4 q1, float t) {
 
 // torch_utils.py:368-380: x-axis heading on the xy plane
 HE_DEV float calc_heading(f4 q) {
+#pragma clang fp contract(off)
     f3 d = qrot_ref(q, f3{1.f, 0.f, 0.f});
     return atan2f(d.y, d.x);
 }
 // torch_utils.py:353-358 quat_from_angle_axis(h, z) (normalize then quat_unit)
 HE_DEV f4 heading_quat(float h) {
+#pragma clang fp contract(off)
     float s = sinf(h / 2.0f), c = cosf(h / 2.0f);
     float n = fmaxf(sqrtf(s * s + c * c), 1e-9f);
     return f4{0.f, 0.f, s / n, c / n};
@@ -155,6 +171,7 @@ HE_DEV f3 qapply(f4 q, f3 v) {  // R(q) v
 
 // motion_lib.py:526-535 sample_time_interval, float32 ops as torch does them
 HE_DEV float sample_time_interval(float phase, float len) {
+#pragma clang fp contract(off)
     const float curr = (float)(1.0 / 30.0);
     float x = (phase * len) / curr;
     long long k = (long long)x;
@@ -163,6 +180,7 @@ HE_DEV float sample_time_interval(float phase, float len) {
 
 // counter-based uniform in [0,1) shared with the oracle (splitmix64 finaliser)
 HE_DEV float hash_uniform(uint64_t seed, uint64_t step, uint32_t env) {
+#pragma clang fp contract(off)
     uint64_t z = seed * 0x9E3779B97F4A7C15ull ^ (step + 0x632BE59BD9B4E019ull) * 0xBF58476D1CE4E5B9ull ^
                  ((uint64_t)env + 0x2545F4914F6CDD1Dull) * 0x94D049BB133111EBull;
     z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;

@@ -73,6 +73,7 @@ struct Lds {
     int nlim;                      // joint-limit slots [0, nlim)
     uint32_t limmask;              // bodies whose joint-angle limit row is emitted this substep
     int ncand;                     // contacts generated (dropped = ncand - nc), last substep
+    alignas(8) int imbook[14];     // fused imitation: the env's bookkeeping + motion metadata (ImitBook)
     int ckey[MAXC];                // warm-start key of each slot (he_sim_params cache layout)
     int wckey[MAXC];               // the previous solve's keys (its impulses: lam)
     int nwc;                       // slots cached in wckey / lam
@@ -1136,6 +1137,30 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
     }
 }
 
+// ---------------------------------------------------------------------------------- fused imitation
+// he_env_step's imitation step (reward / reset / observations + the device reset of flagged envs)
+// as the physics kernel's epilogue, from the post-step state in LDS: the same code as the stand-alone
+// imitation kernel (he_imitation_env.h), with its float32 rounding (no contraction)
+constexpr int GROUP = 32;
+constexpr int HOT = HE_MOTION_HOT;
+constexpr int COLD = HE_MOTION_COLD;
+#pragma clang fp contract(off)
+#include "he_imitation_env.h"
+#pragma clang fp contract(fast)
+
+// body b's rigid-body row (he_get_buffer RB_STATE layout) from the final kinematics: origin, world
+// rotation, linear velocity of the origin, angular velocity
+HE_DEV SimBody body_row(const Lds& L, int b) {
+    SimBody s;
+    s.pos = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]};
+    s.rot = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
+    const f3 w = f3{L.V[b][0], L.V[b][1], L.V[b][2]};
+    const f3 r = f3{L.pw[b][0] - L.root_pos[0], L.pw[b][1] - L.root_pos[1], L.pw[b][2] - L.root_pos[2]};
+    s.vel = f3{L.V[b][3], L.V[b][4], L.V[b][5]} + cross3(w, r);
+    s.ang = w;
+    return s;
+}
+
 // ---------------------------------------------------------------------------------- one substep
 HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
@@ -2002,6 +2027,14 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     }
     static_assert(HE_CACHE_LAMBDA + 3 * MAXC <= HE_CACHE_WORDS && HE_CACHE_KEYS + MAXC <= HE_CACHE_LAMBDA &&
                   HE_CACHE_WORDS <= 2 * W, "cache layout");
+    if (a.fused && lane == 0) {  // fused imitation: bookkeeping + motion metadata (trips 1, 2) now
+        const ImitArgs& im = a.im;
+        const int64_t mid = clamp_mid(im.m, im.motion_ids[e]);
+        const ImitBook bk = imitation_book(im, mid, f3{im.global_offset[3 * e], im.global_offset[3 * e + 1],
+                                                       im.global_offset[3 * e + 2]},
+                                           im.start_times[e], im.start_offsets[e], im.progress[e]);
+        __builtin_memcpy(L.imbook, &bk, sizeof(ImitBook));
+    }
     sync();
     const float* ms = a.mass_scale ? a.mass_scale + (size_t)e * NB : nullptr;
     float mu = a.friction ? a.friction[e] : a.p.friction;
@@ -2009,6 +2042,16 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
     unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * HE_STAMP_SLOTS : nullptr;
     unsigned long long t_prev = __builtin_readcyclecounter();
     for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev, s == 0, s == a.substeps - 1);
+    // ---- fused imitation (he_env_step): the reference samples depend only on the env's motion
+    // bookkeeping (read into LDS at the kernel's start), so their loads are issued here and land
+    // behind the final kinematics and stores
+    ImitRaw iraw;
+    if (a.fused && lane < GROUP) {
+        ImitBook bk;
+        static_assert(sizeof(ImitBook) <= sizeof(L.imbook), "ImitBook fits its LDS words");
+        __builtin_memcpy(&bk, L.imbook, sizeof(ImitBook));
+        iraw = imitation_frames_load(a.im, lane, bk);  // loads only: the blends wait for the epilogue
+    }
     // ---- outputs: generalized state, FK rigid-body state, forces
     kinematics<false>(L, m, lane, a.p, a.substeps > 0);
     STAMP(13);
@@ -2020,22 +2063,28 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         a.dof_state[((size_t)e * ND + d) * 2 + 1] = L.u0[6 + d];
         a.dof_force[(size_t)e * ND + d] = L.dforce[d];
     }
-    for (int t = lane; t < NB * 13; t += W) {
-        int b = t / 13, c = t - 13 * b;
-        float v;
-        if (c < 3) v = L.pw[b][c];
-        else if (c < 7) v = L.qw[b][c - 3];
-        else if (c < 10) {
-            f3 w = f3{L.V[b][0], L.V[b][1], L.V[b][2]};
-            f3 r = f3{L.pw[b][0] - L.root_pos[0], L.pw[b][1] - L.root_pos[1], L.pw[b][2] - L.root_pos[2]};
-            f3 vv = f3{L.V[b][3], L.V[b][4], L.V[b][5]} + cross3(w, r);
-            v = c == 7 ? vv.x : (c == 8 ? vv.y : vv.z);
-        } else v = L.V[b][c - 10];
-        a.rb_state[(size_t)e * NB * 13 + t] = v;
+    // rigid-body rows, lane = body (the fused epilogue reads its body from the same registers)
+    SimBody sb = body_row(L, lane < NB ? lane : 0);
+    if (lane < NB) {
+        float* rb = a.rb_state + ((size_t)e * NB + lane) * 13;
+        rb[0] = sb.pos.x; rb[1] = sb.pos.y; rb[2] = sb.pos.z;
+        rb[3] = sb.rot.x; rb[4] = sb.rot.y; rb[5] = sb.rot.z; rb[6] = sb.rot.w;
+        rb[7] = sb.vel.x; rb[8] = sb.vel.y; rb[9] = sb.vel.z;
+        rb[10] = sb.ang.x; rb[11] = sb.ang.y; rb[12] = sb.ang.z;
     }
     for (int t = lane; t < NB * 3; t += W) a.contact_forces[(size_t)e * NB * 3 + t] = L.cf[t / 3][t % 3];
     if (lane == 0 && a.num_contacts) a.num_contacts[e] = L.nc;
     if (lane == 0 && a.dropped) a.dropped[e] = L.ncand - L.nc;
+    if (a.fused && lane < GROUP) {
+        // he_env_step: the imitation step of this env on lanes 0..31 (lane = body), after every
+        // physics store above has landed (a fused reset overwrites those rows)
+        __threadfence_block();
+        float pw = 0.0f;
+        if (a.im.p.use_power_reward && lane < NB - 1)  // the joint's |tau . qdot| (humanoid_phc.py:1297-1305)
+            pw = power_term(&L.dforce[3 * lane], &L.u0[6 + 3 * lane], 1);
+        imitation_finish<false>(a.im, e, e, lane, lane == 0, imitation_frames_blend(iraw), sb, pw);
+    }
+    STAMP(24);
     if (a.cache) {  // signature (the root pose just written), slot count, keys, impulses
         float* cw = a.cache + (size_t)e * HE_CACHE_WORDS;
         const int nwc = a.p.warm_start ? L.nwc : 0;

@@ -31,7 +31,7 @@ HE_SYMBOLS = (
     "he_set_dof_targets_indexed", "he_set_env_properties", "he_simulate", "he_set_pd_params", "he_step_actions",
     "he_refresh", "he_load_motions", "he_imitation_step", "he_motion_state", "he_reset_envs", "he_env_step",
     "he_imitation_reset_step", "he_set_debug_stamps", "he_hash_uniform", "he_ingest_clips", "he_set_eval",
-    "he_set_amp", "he_amp_observations",
+    "he_set_amp", "he_amp_observations", "he_set_fused_step",
     # include/humanoid_rollout.h
     "he_rollout_store", "he_rollout_order", "he_rollout_gather", "he_gae", "he_gae_minibatch", "he_episode_step",
 )
@@ -69,6 +69,7 @@ def load_library(path: Optional[str] = None):
         "he_set_debug_stamps": [V, V],
         "he_set_eval": [V, V],
         "he_set_amp": [V, V],
+        "he_set_fused_step": [V, I],
         "he_amp_observations": [I, V, V, V, V, V, V, V, V, V],
         "he_rollout_store": [V, V, I, C.c_int64, V, V, C.c_int64, C.c_int32, V],
         "he_rollout_order": [V, C.c_int64, V, I, V],
@@ -362,6 +363,10 @@ class Engine:
                                     C.c_uint64(seed), C.c_uint64(step_index), C.c_void_p(obs.data_ptr()),
                                     C.c_void_p(rew.data_ptr()), C.c_void_p(reward_raw.data_ptr()),
                                     C.c_void_p(reset.data_ptr()), C.c_void_p(terminate.data_ptr()), self.stream))
+
+    def set_fused_step(self, enable: bool):
+        """he_set_fused_step: env_step as one launch (default) or as step_actions + imitation_reset_step."""
+        _check(self.lib.he_set_fused_step(self.h, int(bool(enable))))
 
     def imitation_reset_step(self, params, em, obs, rew, reward_raw, reset, terminate, seed: int, step_index: int):
         _check(self.lib.he_imitation_reset_step(self.h, C.byref(params), C.byref(em), C.c_uint64(seed),

@@ -242,6 +242,12 @@ int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion*
                 float* obs, float* rew, float* reward_raw, uint8_t* reset, uint8_t* terminate,
                 void* stream);
 
+/* he_env_step as ONE launch (the imitation step in the physics kernel's epilogue) or as two
+ * (he_step_actions + he_imitation_reset_step): enable 1 / 0, or -1 = auto (the default: one launch
+ * up to 2048 envs, where launch and tail latency dominate). Eval recording always takes two. Both
+ * forms give the same results bit for bit (tests/test_gpu_parity.py). */
+int he_set_fused_step(he_engine* h, int enable);
+
 /* Second half of he_env_step on its own (after he_step_actions): reward/reset/obs with the device
  * reset of flagged envs. he_env_step == he_step_actions + he_imitation_reset_step. */
 int he_imitation_reset_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, uint64_t seed,

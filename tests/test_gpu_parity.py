@@ -511,14 +511,17 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
     assert n_reset > 0, "test should exercise the device reset path"
 
 
-def test_env_step_single_call_equals_two_calls(he_model, model, golden):
-    """he_env_step is exactly he_step_actions followed by he_imitation_reset_step."""
+@pytest.mark.parametrize("fused", [1, 0])
+def test_env_step_single_call_equals_two_calls(he_model, model, golden, fused):
+    """he_env_step -- as one launch (the imitation step in the physics kernel's epilogue) and as two
+    -- is exactly he_step_actions followed by he_imitation_reset_step, bit for bit."""
     from humanoid_amd.model import pd_action_offset_scale
     g = golden("env_step")
     n = 24
     outs = []
     for single in (True, False):
         eng = make_engine(he_model, n)
+        eng.set_fused_step(fused)
         eng.load_motions(tables_from_golden(g))
         off, sc = pd_action_offset_scale(model)
         eng.set_pd_params(off, sc, None)

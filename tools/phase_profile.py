@@ -19,7 +19,7 @@ PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba"
           "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write",
           "terrain: geometry", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
           "self: segments", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
-          "free: prefetch + row loads", "free: L^-1 levels"]  # slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
+          "free: prefetch + row loads", "free: L^-1 levels", "fused imitation"]  # slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
 
 
 def main():
@@ -29,13 +29,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--max-contacts", type=int, default=20)
+    ap.add_argument("--fused", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import torch
     import bench
     from humanoid_amd.model import load_default_model
     bargs = argparse.Namespace(config=args.config, num_envs=args.num_envs, clips=128, seed=0,
-                               max_contacts=args.max_contacts)
+                               max_contacts=args.max_contacts, fused=args.fused)
     model = load_default_model()
     ro = bench.Rollout(bargs, model, 0, 0)
     for _ in range(args.warmup):
