@@ -1,0 +1,134 @@
+"""The physics invariants of tests/test_physics_invariants.py held by the HIP engine itself, at the
+bench's size (4096 envs) where the oracle is too slow to follow every env:
+* free fall from rest (drives off): the discrete semi-implicit parabola, in float32;
+* free flight with the drives off and no damping: linear momentum gains exactly M g t and angular
+  momentum about the CoM drifts at first order (measured with the oracle's momentum function on the
+  engine's states);
+* configs[1] PD stand-still at full size: after a 5 s settle every env stands still, its feet on
+  the plane within the Baumgarte steady state;
+* joint angles never leave |q| <= pi under saturated random actions (the joint-angle limit rows).
+"""
+import numpy as np
+import pytest
+
+from humanoid_amd import _abi
+from oracle import oracle as O
+
+import cases
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+G = 9.81
+
+
+def _engine(he_model, n, **sim):
+    from humanoid_amd.engine import Engine
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+    return Engine(he_model, n, device=0, sim_params=_abi.default_sim_params(**sim))
+
+
+def _load(eng, root, dof, targets=None):
+    n = root.shape[0]
+    eng.root_states.copy_(torch.as_tensor(root, device="cuda:0"))
+    eng.dof_state.copy_(torch.as_tensor(dof.reshape(n * 69, 2), device="cuda:0"))
+    if targets is None:
+        eng.dof_targets.zero_()
+    else:
+        eng.dof_targets.copy_(torch.as_tensor(targets, device="cuda:0"))
+
+
+def test_gpu_free_fall_is_the_discrete_parabola(he_model):
+    n = 4096
+    rng = np.random.default_rng(0)
+    root, dof = cases.random_state(n, rng, height=(6.0, 7.0), vel=0.0)
+    dof[..., 1] = 0.0
+    eng = _engine(he_model, n, self_collision=0, kp_scale=0.0, kd_scale=0.0, angular_damping=0.0, joint_limits=0)
+    _load(eng, root, dof)
+    steps = 20
+    for _ in range(steps):
+        eng.simulate(2)
+    torch.cuda.synchronize()
+    r = eng.root_states.cpu().numpy()
+    k = 2 * steps
+    dt = 1.0 / 60.0
+    assert (eng.num_contacts.cpu().numpy() == 0).all()
+    np.testing.assert_allclose(r[:, 2], root[:, 2] - G * dt * dt * k * (k + 1) / 2, atol=2e-5)
+    np.testing.assert_allclose(r[:, 9], -G * dt * k, atol=2e-5)
+    np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0], dof[..., 0], atol=2e-6)
+
+
+def test_gpu_free_flight_momentum(he_model, model):
+    """Drives off, no damping, gravity on, 1 s: P - M g t and L_com stay within the oracle's own
+    first-order drift bounds (tests/test_physics_invariants.py)."""
+    n = 1024
+    rng = np.random.default_rng(1)
+    root, dof = cases.random_state(n, rng, height=(9.0, 10.0), vel=0.5, ang=0.5)
+    # no limits: a free joint may spin up to pi in 1 s of undriven flight (its limit row would act)
+    sim = dict(self_collision=0, kp_scale=0.0, kd_scale=0.0, angular_damping=0.0, joint_limits=0)
+    eng = _engine(he_model, n, **sim)
+    _load(eng, root, dof)
+    sp = _abi.default_sim_params(**sim)
+    me0 = O.momentum_energy(he_model, sp, root, dof)
+    for _ in range(30):
+        eng.simulate(2)
+    torch.cuda.synchronize()
+    assert (eng.num_contacts.cpu().numpy() == 0).all()
+    r = eng.root_states.cpu().numpy()
+    d = eng.dof_state.view(n, 69, 2).cpu().numpy()
+    me1 = O.momentum_energy(he_model, sp, r, d)
+    M = float(np.sum(model.mass))
+
+    def l_com(me, rr, dd):
+        c = cases.center_of_mass(model, O.forward_kinematics(he_model, rr, dd))
+        return me[:, 3:6] - np.cross(c, me[:, :3])
+
+    P = np.abs(me0[:, :3]).max()
+    L = np.abs(l_com(me0, root, dof)).max()
+    dP = np.abs(me1[:, :3] - (me0[:, :3] + M * np.array([0, 0, -G]) * 1.0)).max()
+    dL = np.abs(l_com(me1, r, d) - l_com(me0, root, dof)).max()
+    assert dP < 0.03 * P and dL < 0.1 * L, (dP, P, dL, L)
+
+
+def test_gpu_full_size_stand_still(he_model, model):
+    """configs[1] at 4096 envs: 5 s to settle, then 2 s of standing still; feet on the plane."""
+    n = 4096
+    rng = np.random.default_rng(4)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    eng = _engine(he_model, n)
+    _load(eng, root, dof)
+    for _ in range(150):
+        eng.simulate(2)
+    torch.cuda.synchronize()
+    r1 = eng.root_states.cpu().numpy().copy()
+    for _ in range(60):
+        eng.simulate(2)
+    torch.cuda.synchronize()
+    r = eng.root_states.cpu().numpy()
+    d = eng.dof_state.view(n, 69, 2).cpu().numpy()
+    assert np.abs(r[:, :3] - r1[:, :3]).max() < 2e-4
+    assert np.abs(r[:, 7:]).max() < 1e-3 and np.abs(d[..., 1]).max() < 1e-3
+    assert (eng.num_contacts.cpu().numpy() == 16).all() and (eng.dropped_contacts.cpu().numpy() == 0).all()
+    gaps = cases.ground_gaps(model, eng.rb_state.view(n, 24, 13).cpu().numpy())
+    assert gaps.min() > -2e-3 and gaps.min() < 0.02
+
+
+def test_gpu_joint_angles_stay_inside_pi(he_model, model):
+    """Saturated random actions (the PD scale x U(-1, 1): knee-y targets up to +-5 rad) on 4096
+    standing envs for 2 s: no joint's rotation angle reaches pi (the limit rows hold it at pi - 0.02)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    n = 4096
+    rng = np.random.default_rng(8)
+    off, sc = pd_action_offset_scale(model)
+    eng = _engine(he_model, n)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    _load(eng, root, dof)
+    worst = 0.0
+    for _ in range(60):
+        a = rng.uniform(-1.0, 1.0, (n, 69)).astype(np.float32)
+        eng.dof_targets.copy_(torch.as_tensor(off + sc * a, device="cuda:0"))
+        eng.simulate(2)
+        q = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3)
+        worst = max(worst, float(q.norm(dim=-1).max()))
+    assert worst < np.pi, worst
+    assert torch.isfinite(eng.root_states).all()

@@ -38,7 +38,8 @@ def _run(he_model, root, dof, targets, steps, substeps=2, **sim):
 
 
 def _drives_off(**kw):
-    sim = dict(self_collision=0, kp_scale=0.0, kd_scale=0.0, angular_damping=0.0)
+    # joint limits off: an undriven joint may spin up to pi in a long flight, where its limit row acts
+    sim = dict(self_collision=0, kp_scale=0.0, kd_scale=0.0, angular_damping=0.0, joint_limits=0)
     sim.update(kw)
     return sim
 
