@@ -131,6 +131,8 @@ int he_set_model(he_engine* h, const he_model* model) {
     PhysTopo topo{};
     he_build_topo(*model, topo);
     if (topo.nnz > HE_NNZ_MAX) return fail("he_set_model: mass-matrix pattern too large (%d)", topo.nnz);
+    if (topo.num_boxes > HE_MAX_BOXES)
+        return fail("he_set_model: %d box geoms (the kernel's corner lanes hold at most %d)", topo.num_boxes, HE_MAX_BOXES);
     if (!h->d_model) HE_CHECK(dalloc(&h->d_model, 1));
     if (!h->d_topo) HE_CHECK(dalloc(&h->d_topo, 1));
     HE_CHECK(hipMemcpy(h->d_model, model, sizeof(he_model), hipMemcpyHostToDevice));

@@ -50,6 +50,7 @@ struct BodyTopo {
     uint32_t jump4[NB];      // byte k: 2^k-th ancestor of body b (0xFF: none), for pointer jumping
     int16_t pack_start[NG];  // packed-row offset of dof i (smpl::kPackStart)
     int8_t dof_depth[NG];    // depth of dof i in the dof tree (smpl::kDofNanc - 1)
+    int8_t cbody[W];         // corner lanes: the box body of lane 24 + 8k + c (PhysTopo::corner_body)
 };
 
 struct Lds {
@@ -297,6 +298,11 @@ HE_DEV int wave_prefix(bool flag, int lane, int& total) {
     return __popcll(below);
 }
 
+// the value of lane ^ S (S < 32): ds_swizzle in bitmask mode (and 0x1F, xor S)
+template <int S>
+HE_DEV float swizzle_xor(float v) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (S << 10)));
+}
 HE_DEV void store_contact(Lds& L, int slot, int b0, int b1, f3 x, f3 n, float gap, float mu) {
     L.cb0[slot] = b0;
     L.cb1[slot] = b1;
@@ -1352,7 +1358,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     int2 prs[ROUNDS];
     const int npairs = m.num_pairs;
     {
-        const int b = lane < NB ? lane : 0;
+        // body lanes their own geom, corner lanes their box's
+        const int cb = L.T.cbody[lane];
+        const int b = lane < NB ? lane : (cb >= 0 ? cb : 0);
         const float* g = m.geom_params[b];
 #pragma unroll
         for (int i = 0; i < 10; ++i) gv[i] = g[i];
@@ -1411,17 +1419,24 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     int nc = nlim;
     int terr_all = 0, self_all = 0;
-    // -- terrain candidates of the lane's body: one path for every geometry type
+    // -- terrain candidates, one per lane-slot: a body lane (lane < 24) takes its sphere's centre or
+    // its capsule's end points, a corner lane (lane 24 + 8k + c, he_topo.h corner_body) corner c of
+    // the k-th box. Geometry (every lane, of its geometry body tb_):
     //  self segment P0-P1, radius rs: sphere P0 = P1 = centre; capsule from / to; box the capsule
     //    proxy along its longest axis (radius geom_radius)
-    //  terrain candidates, radius rt: sphere the centre; capsule from, to; box the 8 corners around
-    //    its centre Pc (world centre +- the world half-axes, which are 0 for the others)
-    const int tb_ = lane < NB ? lane : 0;
+    //  terrain points, radius rt: sphere the centre; capsule from, to; box corner c around its
+    //    centre Pc (world centre +- the world half-axes)
+    static_assert(NB % 8 == 0 && NB + 8 * HE_MAX_BOXES <= W, "corner lanes: 8-lane groups above the body lanes");
+    constexpr int kPts = 2;  // terrain points per lane
+    const int cbody = L.T.cbody[lane];
+    const bool corner = lane >= NB && cbody >= 0;
+    const int tb_ = lane < NB ? lane : (corner ? cbody : 0);
+    const int cc = lane & 7;  // a corner lane's corner index
     const bool isS = gt == HE_GEOM_SPHERE, isC = gt == HE_GEOM_CAPSULE, isB = !isS && !isC;
-    float cd[8];
-    f3 cxs[8], cns[8];
-    bool cand[8];
-    int rank[8];
+    float cd[kPts];
+    f3 cxs[kPts], cns[kPts];
+    bool cand[kPts];
+    int rank[kPts];
     int myn = 0, base = 0;
     auto terrain_candidates = [&]() {
         const f4 bq = isB ? f4{gv[6], gv[7], gv[8], gv[9]} : f4{0.f, 0.f, 0.f, 1.f};
@@ -1430,8 +1445,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         if (gv[4] > emax) { ax = 1; emax = gv[4]; }
         if (gv[5] > emax) { ax = 2; emax = gv[5]; }
         const float half = fmaxf(emax - grad, 0.f);
-        // rotations as matrices (the box's local frame and the body's world rotation): six
-        // mat-vecs instead of ten quaternion applications
+        // rotations as matrices (the box's local frame and the body's world rotation): mat-vecs
+        // instead of quaternion applications
         f3 bc0, bc1, bc2, wc0, wc1, wc2;
         qcols(bq, bc0, bc1, bc2);
         qcols(f4{L.qw[tb_][0], L.qw[tb_][1], L.qw[tb_][2], L.qw[tb_][3]}, wc0, wc1, wc2);
@@ -1443,7 +1458,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const float rs = isS ? gv[3] : (isC ? gv[6] : grad);
         const float rt = isS ? gv[3] : (isC ? gv[6] : 0.f);
         auto rot = [&](f3 v) { return (wc0 * v.x + wc1 * v.y) + wc2 * v.z; };
-        const f3 P0 = pwb + rot(l0), P1 = pwb + rot(l1), Pc = pwb + rot(ctr);
+        const f3 P0 = pwb + rot(l0), P1 = pwb + rot(l1);
         if (self_col && lane < NB) {
             // world segments (the Ib scratch is dead after the subtree sums), and the bounding
             // sphere about the segment midpoint for the pair cull as one 16-byte record
@@ -1452,45 +1467,43 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const f3 mid = (P0 + P1) * 0.5f;
             L.bsph[lane] = make_float4(mid.x, mid.y, mid.z, 0.5f * norm3(P1 - P0) + rs);
         }
-        const f3 ex = rot(bc0 * (isB ? gv[3] : 0.f));
-        const f3 ey = rot(bc1 * (isB ? gv[4] : 0.f));
-        const f3 ez = rot(bc2 * (isB ? gv[5] : 0.f));
-        const f3 base0 = isB ? Pc : P0;
-        const int ncand = lane < NB ? (isS ? 1 : (isC ? 2 : 8)) : 0;
+        // a corner lane's point: ((Pc +- ex) +- ey) +- ez, signs by the bits of c
+        f3 X0 = P0;
+        if (corner) {
+            const f3 Pc = pwb + rot(ctr);
+            const f3 ex = rot(bc0 * gv[3]), ey = rot(bc1 * gv[4]), ez = rot(bc2 * gv[5]);
+            X0 = ((Pc + ((cc & 1) ? ex : ex * -1.f)) + ((cc & 2) ? ey : ey * -1.f)) + ((cc & 4) ? ez : ez * -1.f);
+        }
+        const int npts = lane < NB ? (isS ? 1 : (isC ? 2 : 0)) : (corner ? 1 : 0);
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) {
-            const f3 bs = (ci == 1 && isC) ? P1 : base0;
-            const f3 x = ((bs + ((ci & 1) ? ex : ex * -1.f)) + ((ci & 2) ? ey : ey * -1.f)) + ((ci & 4) ? ez : ez * -1.f);
+        for (int ci = 0; ci < kPts; ++ci) {
+            const f3 x = ci == 0 ? X0 : P1;
             cd[ci] = terrain_dist(ter, x, cns[ci]) - rt;
             cxs[ci] = x - cns[ci] * rt;
-            cand[ci] = ci < ncand && cd[ci] < off;
+            cand[ci] = ci < npts && cd[ci] < off;
         }
-        // rank among this body's candidates: box corners by depth, ties (and sphere / capsule end
-        // points, keyed 0) by index; non-candidates keyed +inf never go first. With rank[k]
-        // starting at k, one comparison per unordered pair i < j moves both ranks:
-        // rank[k] = #{i < k : key_i <= key_k} + #{j > k : key_j < key_k} (vector ops only)
-        float key[8];
-#pragma unroll
-        for (int ci = 0; ci < 8; ++ci) { rank[ci] = ci; key[ci] = cand[ci] ? (isB ? cd[ci] : 0.f) : __builtin_inff(); }
-#pragma unroll
-        for (int ci = 0; ci < 8; ++ci)
-#pragma unroll
-            for (int cj = ci + 1; cj < 8; ++cj) {
-                const int c = key[cj] < key[ci] ? 1 : 0;  // j goes first
-                rank[ci] += c;
-                rank[cj] -= c;
-            }
-        // the kept candidates (a box's 4 deepest corners) take the body's slots in candidate index
-        // order, so that resting contacts keep their slots from one substep to the next (the
-        // warm start then maps impulses one to one); rank[] becomes that slot offset
-        myn = 0;
-#pragma unroll
-        for (int ci = 0; ci < 8; ++ci) {
-            const bool kept = cand[ci] && rank[ci] < 4;
-            rank[ci] = kept ? myn : 8;
-            myn += kept ? 1 : 0;
-        }
-        // exclusive prefix of myn (0..4) over the lanes: three bit ballots, v_mbcnt per bit
+        // a box keeps its 4 deepest corners (ties by index): a corner lane's rank among the 8 lanes
+        // of its group, keys through xor swizzles (non-candidates keyed +inf never go first)
+        const float key = corner && cand[0] ? cd[0] : __builtin_inff();
+        int r = 0;
+        auto beat = [&](float kj, int sx) { r += (kj < key || (kj == key && (cc ^ sx) < cc)) ? 1 : 0; };
+        beat(swizzle_xor<1>(key), 1);
+        beat(swizzle_xor<2>(key), 2);
+        beat(swizzle_xor<3>(key), 3);
+        beat(swizzle_xor<4>(key), 4);
+        beat(swizzle_xor<5>(key), 5);
+        beat(swizzle_xor<6>(key), 6);
+        beat(swizzle_xor<7>(key), 7);
+        const bool kept0 = cand[0] && (!corner || r < 4), kept1 = cand[1];
+        // the kept points take the body's slots in point index order (box corners by corner index),
+        // so that resting contacts keep their slots from one substep to the next (the warm start then
+        // maps impulses one to one); rank[] becomes that slot offset within the body
+        const uint64_t kb = __ballot(corner && kept0);
+        const uint64_t bxm = __ballot(lane < NB && isB);
+        const int kbox = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bxm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bxm, 0u));
+        const uint32_t grp = (uint32_t)(kb >> (corner ? (lane & ~7) : (NB + 8 * (kbox < HE_MAX_BOXES ? kbox : 0)))) & 0xFFu;
+        myn = lane < NB ? (isB ? __popc(grp) : (kept0 ? 1 : 0) + (kept1 ? 1 : 0)) : 0;
+        // exclusive prefix of myn (0..4) over the body lanes: three bit ballots, v_mbcnt per bit
         base = 0;
         int total = 0;
 #pragma unroll
@@ -1499,20 +1512,27 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             base += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << k;
             total += __popcll(bm) << k;
         }
+        // a corner lane starts from its box body's base
+        const int bbase = __builtin_amdgcn_ds_bpermute(4 * tb_, base);
+        if (corner) base = bbase;
+        rank[0] = kept0 ? (corner ? __popc(grp & ((1u << cc) - 1u)) : 0) : 8;
+        rank[1] = kept1 ? (kept0 ? 1 : 0) : 8;
         return total;
     };
+    // the contact key's sub-index: the point's index on its body (a box's corner index)
+    auto sub_of = [&](int ci) { return corner ? cc : ci; };
     {
         terr_all = terrain_candidates();
         STAMP(16);
         // candidate k = base + rank (in slot order): its gap for the reduction, its slot nlim + k
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) {
+        for (int ci = 0; ci < kPts; ++ci) {
             if (cand[ci] && rank[ci] < 4) {
                 const int k = base + rank[ci];
                 if (k < kCand) gl[k] = cd[ci];
                 if (nlim + k < maxc) {
                     store_contact(L, nlim + k, tb_, -1, cxs[ci], cns[ci], cd[ci], mu);
-                    L.ckey[nlim + k] = tb_ | (1 << 8) | (ci << 16);
+                    L.ckey[nlim + k] = tb_ | (1 << 8) | (sub_of(ci) << 16);
                 }
             }
         }
@@ -1627,13 +1647,13 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         auto is_kept = [&](int k) { return k < 2 * W && ((km[k >= W ? 1 : 0] >> (k & (W - 1))) & 1ull); };
         terrain_candidates();
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) {
+        for (int ci = 0; ci < kPts; ++ci) {
             if (cand[ci] && rank[ci] < 4) {
                 const int k = base + rank[ci];
                 if (is_kept(k)) {
                     const int slot = nlim + before(k);
                     store_contact(L, slot, tb_, -1, cxs[ci], cns[ci], cd[ci], mu);
-                    L.ckey[slot] = tb_ | (1 << 8) | (ci << 16);
+                    L.ckey[slot] = tb_ | (1 << 8) | (sub_of(ci) << 16);
                 }
             }
         }
@@ -1986,6 +2006,7 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         L.T.jump4[lane] = kJump4.v[lane < NB ? lane : 0];
         for (int c = 0; c < 3; ++c) L.T.local_pos[lane][c] = m.local_pos[lane][c];
     }
+    L.T.cbody[lane] = a.topo->corner_body[lane];
     for (int i = lane; i < NG; i += W) {  // per-dof tree tables (constant memory -> LDS once)
         L.T.pack_start[i] = (int16_t)smpl::kPackStart[i];
         L.T.dof_depth[i] = (int8_t)(smpl::kDofNanc[i] - 1);

@@ -8,6 +8,7 @@
 #define HE_MAX_CHAIN 30    // longest root->dof chain: 6 root dofs + 8 bodies x 3
 #define HE_NNZ_MAX 1280    // packed lower-triangular sparse mass matrix (1221 for SMPL)
 #define HE_MAX_TRI 435     // pairs (i,j), j<=i<29 of one elimination step
+#define HE_MAX_BOXES 5     // box geoms: one 8-lane corner group each in lanes 24..63 (SMPL: 4)
 
 struct PhysTopo {
     int32_t nnz;
@@ -27,6 +28,8 @@ struct PhysTopo {
     uint8_t tri_i[HE_MAX_TRI], tri_j[HE_MAX_TRI];
     uint8_t ent_row[HE_NNZ_MAX];          // packed entry -> row of the sparse mass matrix
     int8_t body_last_dof[HE_NUM_BODIES];  // chain(body_last_dof[b]) = all dofs on b's chain
+    int32_t num_boxes;
+    int8_t corner_body[64];  // lane 24 + 8k + c: corner c of the k-th box geom's body (-1: none)
 };
 
 #ifdef __cplusplus
@@ -83,6 +86,14 @@ static inline void he_build_topo(const he_model& m, PhysTopo& t) {
     int p = 0;
     for (int i = 0; i < 29 && p < HE_MAX_TRI; ++i)
         for (int j = 0; j <= i && p < HE_MAX_TRI; ++j) { t.tri_i[p] = (uint8_t)i; t.tri_j[p] = (uint8_t)j; ++p; }
+    t.num_boxes = 0;
+    for (int l = 0; l < 64; ++l) t.corner_body[l] = -1;
+    for (int b = 0; b < HE_NUM_BODIES; ++b)
+        if (m.geom_type[b] == HE_GEOM_BOX) {
+            if (t.num_boxes < HE_MAX_BOXES)
+                for (int c = 0; c < 8; ++c) t.corner_body[HE_NUM_BODIES + 8 * t.num_boxes + c] = (int8_t)b;
+            ++t.num_boxes;
+        }
 }
 #endif
 
