@@ -543,3 +543,19 @@ def test_env_step_single_call_equals_two_calls(he_model, model, golden, fused):
         outs.append([b.cpu().numpy() for b in bufs] + [eng.rb_state.cpu().numpy()])
     for x, y in zip(*outs):
         np.testing.assert_array_equal(x, y)
+
+
+def test_model_with_more_boxes_than_corner_lanes_is_refused(he_model):
+    """Box corners take 8-lane groups above the 24 body lanes (he_topo.h HE_MAX_BOXES = 5): a model
+    with a sixth box geom is refused at he_set_model with the reason, not simulated wrong."""
+    from humanoid_amd.engine import Engine, EngineError
+    from humanoid_amd.model import GEOM_BOX
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+    m = type(he_model).from_buffer_copy(he_model)
+    boxes = [b for b in range(24) if m.geom_type[b] == GEOM_BOX]
+    assert len(boxes) == 4  # SMPL: ankles and toes
+    for b in (0, 13):  # two more bodies become boxes
+        m.geom_type[b] = GEOM_BOX
+    with pytest.raises(EngineError, match="box geoms"):
+        Engine(m, 4, device=0)
