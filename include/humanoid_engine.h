@@ -136,7 +136,9 @@ int he_device_count(int* count);
 
 /* gymapi.acquire_gym + create_sim (isaacgym_env.py:48-50): bind a HIP device, copy params. */
 int he_create(const he_sim_params* params, int device, he_engine** out);
-/* gym.load_asset (humanoid_phc.py:216); the host parses the MJCF into the blob. */
+/* gym.load_asset (humanoid_phc.py:216); the host parses the MJCF into the blob. Fails (with the
+ * reason in he_last_error) on a topology other than 24 bodies / 69 dofs in DFS order, more than
+ * HE_MAX_PAIRS self pairs or more than 5 box geoms (the kernel's corner lanes; SMPL has 4). */
 int he_set_model(he_engine* h, const he_model* model);
 /* create_env/create_actor x N + prepare_sim (humanoid_phc.py:264-326, :74): allocates the state
  * tensors, places actors at (start_xy, 0.89) with identity rotation (humanoid_phc.py:340-347). */
