@@ -1419,6 +1419,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     int nc = nlim;
     int terr_all = 0, self_all = 0;
+    STAMP(14);
     // -- terrain candidates, one per lane-slot: a body lane (lane < 24) takes its sphere's centre or
     // its capsule's end points, a corner lane (lane 24 + 8k + c, he_topo.h corner_body) corner c of
     // the k-th box. Geometry (every lane, of its geometry body tb_):
@@ -1459,6 +1460,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const float rt = isS ? gv[3] : (isC ? gv[6] : 0.f);
         auto rot = [&](f3 v) { return (wc0 * v.x + wc1 * v.y) + wc2 * v.z; };
         const f3 P0 = pwb + rot(l0), P1 = pwb + rot(l1);
+        STAMP(18);
         if (self_col && lane < NB) {
             // world segments (the Ib scratch is dead after the subtree sums), and the bounding
             // sphere about the segment midpoint for the pair cull as one 16-byte record

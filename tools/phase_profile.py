@@ -17,8 +17,8 @@ os.environ.setdefault("HE_ENGINE_LIB", os.path.join(ROOT, "humanoid_amd", "libhu
 
 PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba", "ltdl factor", "free solve",
           "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write",
-          "terrain: geometry", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
-          "self: segments", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
+          "contact: limit slots", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
+          "terrain: geometry (to P0/P1)", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
           "free: prefetch + row loads", "free: L^-1 levels", "fused imitation"]  # slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
 
 
