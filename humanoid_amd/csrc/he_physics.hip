@@ -126,7 +126,8 @@ HE_DEV void sync() {
 HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
 
 // optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
-// s_memtime deltas per phase into stamps[block * HE_STAMP_SLOTS + phase]
+// s_memtime deltas per phase into stamps[block * HE_STAMP_SLOTS + phase] with a no-return vector
+// atomic add (a load-add-store would put one global round trip into every phase it opens)
 #ifndef HE_PHASE_STAMPS
 #define HE_PHASE_STAMPS 0  // diagnostic twin library only (build.py PHASES_LIB)
 #endif
@@ -139,7 +140,8 @@ HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
     do {                                                                      \
         if (stamps && lane == 0) {                                            \
             unsigned long long _t = __builtin_readcyclecounter();             \
-            stamps[id] += _t - t_prev;                                        \
+            __hip_atomic_fetch_add(stamps + (id), _t - t_prev, __ATOMIC_RELAXED, \
+                                   __HIP_MEMORY_SCOPE_AGENT);                 \
             t_prev = _t;                                                      \
         }                                                                     \
     } while (0)
