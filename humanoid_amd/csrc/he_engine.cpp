@@ -121,6 +121,15 @@ int he_set_model(he_engine* h, const he_model* model) {
     if (model->parents[0] != -1) return fail("he_set_model: body 0 must be the root");
     for (int b = 1; b < HE_NUM_BODIES; ++b)
         if (model->parents[b] < 0 || model->parents[b] >= b) return fail("he_set_model: bodies must be in DFS order");
+    for (int b = 0; b < HE_NUM_BODIES; ++b)
+        if (model->geom_type[b] != HE_GEOM_SPHERE && model->geom_type[b] != HE_GEOM_CAPSULE && model->geom_type[b] != HE_GEOM_BOX)
+            return fail("he_set_model: body %d has geom type %d (sphere 0, capsule 1, box 2)", b, model->geom_type[b]);
+    // every check before the engine changes: a refused model leaves the previous one in place
+    PhysTopo topo{};
+    he_build_topo(*model, topo);
+    if (topo.nnz > HE_NNZ_MAX) return fail("he_set_model: mass-matrix pattern too large (%d)", topo.nnz);
+    if (topo.num_boxes > HE_MAX_BOXES)
+        return fail("he_set_model: %d box geoms (the kernel's corner lanes hold at most %d)", topo.num_boxes, HE_MAX_BOXES);
     HE_CHECK(hipSetDevice(h->device));
     h->model = *model;
     // the kernel holds every joint's rotation angle below pi - 0.02 (the exp-map branch cut); dof
@@ -128,11 +137,6 @@ int he_set_model(he_engine* h, const he_model* model) {
     h->component_limits = false;
     for (int d = 0; d < HE_NUM_DOF; ++d)
         if (std::fabs(model->dof_lower[d]) < 3.1215f || std::fabs(model->dof_upper[d]) < 3.1215f) h->component_limits = true;
-    PhysTopo topo{};
-    he_build_topo(*model, topo);
-    if (topo.nnz > HE_NNZ_MAX) return fail("he_set_model: mass-matrix pattern too large (%d)", topo.nnz);
-    if (topo.num_boxes > HE_MAX_BOXES)
-        return fail("he_set_model: %d box geoms (the kernel's corner lanes hold at most %d)", topo.num_boxes, HE_MAX_BOXES);
     if (!h->d_model) HE_CHECK(dalloc(&h->d_model, 1));
     if (!h->d_topo) HE_CHECK(dalloc(&h->d_topo, 1));
     HE_CHECK(hipMemcpy(h->d_model, model, sizeof(he_model), hipMemcpyHostToDevice));

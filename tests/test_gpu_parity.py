@@ -559,3 +559,7 @@ def test_model_with_more_boxes_than_corner_lanes_is_refused(he_model):
         m.geom_type[b] = GEOM_BOX
     with pytest.raises(EngineError, match="box geoms"):
         Engine(m, 4, device=0)
+    m = type(he_model).from_buffer_copy(he_model)
+    m.geom_type[5] = 7
+    with pytest.raises(EngineError, match="geom type 7"):
+        Engine(m, 4, device=0)
