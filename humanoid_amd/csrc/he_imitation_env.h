@@ -368,7 +368,9 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
     f3 root_pos = f3{bcast0(s.pos.x), bcast0(s.pos.y), bcast0(s.pos.z)};
     f4 root_rot = f4{bcast0(s.rot.x), bcast0(s.rot.y), bcast0(s.rot.z), bcast0(s.rot.w)};
     float h = calc_heading(root_rot);
-    f4 hinv = heading_quat(-h), hq = heading_quat(h);
+    // quat_from_angle_axis(+-h, z): sinf is odd and cosf even (both evaluate |x| and restore the
+    // sign), so the heading rotation is the inverse's z negated, bit for bit
+    const f4 hinv = heading_quat(-h), hq = f4{0.f, 0.f, -hinv.z, hinv.w};
     if (act) write_obs(a.obs + (size_t)e * HE_OBS_DIM, b, s, root_pos, hinv, hq, r2);
 }
 
