@@ -483,10 +483,11 @@ class PHCPufferEnv:
         else:
             self.actions[:] = actions.clamp(-1, 1) if self.cfg.clip_actions else actions
         e = self.env
-        e.engine.step_actions(self.actions, 2)
         e._attach_eval()
-        e.engine.imitation_reset_step(e._params, e._em, e.obs_buf, e.rew_buf, e.reward_raw, e._reset_u8, e._term_u8,
-                                      seed=self.cfg.seed, step_index=self.tick)
+        # physics + reward / reset / observation: one launch up to 2048 envs (he_set_fused_step auto),
+        # two above, or with eval recording attached; bit-identical either way
+        e.engine.env_step(e._params, e._em, self.actions, e.obs_buf, e.rew_buf, e.reward_raw, e._reset_u8, e._term_u8,
+                          seed=self.cfg.seed, step_index=self.tick)
         e._obs_noise()
         # the step's returned copies and the episode bookkeeping (env.py:120-160) in one launch
         rew = torch.empty_like(self.rewards)
