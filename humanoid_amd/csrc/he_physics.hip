@@ -205,10 +205,7 @@ HE_DEV f3 pqlog(f4 q) {
 // wraps at |q_b| = pi, so the MJCF's +-180 / +-720 deg ranges hold the rotation angle at
 // pi - kLimitGuard; the speculative row is emitted within limit_margin + dt * (closing rate).
 constexpr float kLimitGuard = 0.02f;
-HE_DEV bool angle_row(const Lds& L, int b, const he_sim_params& p, float& gap, f3& dir) {
-    const int d = 3 * (b - 1);
-    const f3 th = f3{L.q[d], L.q[d + 1], L.q[d + 2]};
-    const f3 u = f3{L.u0[6 + d], L.u0[7 + d], L.u0[8 + d]};
+HE_DEV bool angle_row(f3 th, f3 u, const he_sim_params& p, float& gap, f3& dir) {
     const float t = __builtin_amdgcn_sqrtf(dot3(th, th));
     dir = th * __builtin_amdgcn_rcpf(fmaxf(t, 1e-30f));
     gap = (3.14159265358979f - kLimitGuard) - t;
@@ -221,6 +218,51 @@ HE_DEV bool angle_row(const Lds& L, int b, const he_sim_params& p, float& gap, f
 // forces until this substep's friction-basis pass, which runs after the limit slots are stored.
 HE_DEV float* limit_rows(Lds& L) { return &L.ct1[0][0]; }
 static_assert(4 * (NB - 1) <= 6 * MAXC, "the limit rows fit the ct1 / ct2 arrays");
+// Backstop when the limit rows lose (oracle/he_oracle_physics.c limit_clamp): a limit against a
+// deep self contact has no solution, and a joint near 100 rad/s can cross the margin in one
+// substep. The new exp map nv is unwrapped against the old one qo (a rotation that crossed pi
+// comes back from the log on the far side, axis flipped, which would reverse the joint's PD error
+// and spin it), then held at pi - kLimitGuard / 2 with the outward rate q^ . w removed. Returns
+// whether it acted (nv and w changed).
+HE_DEV bool limit_clamp(f3 qo, f3& nv, float (&w)[3]) {
+    constexpr float kTwoPi = 6.28318530717959f;
+    constexpr float cap = 3.14159265358979f - 0.5f * kLimitGuard;
+    // a joint inside the cap that started more than 1.7 rad from pi (100 rad/s x 1/60 s) can
+    // neither be past the cap nor have crossed pi: the common case, one branch
+    if (dot3(nv, nv) <= cap * cap && dot3(qo, qo) < 2.07f) return false;
+    const float t0 = sqrtf(dot3(nv, nv));
+    if (!(t0 >= 1e-12f)) return false;
+    f3 dir = nv * (1.0f / t0);
+    float t = t0;
+    const f3 a = nv - qo;
+    const f3 f = dir * -(kTwoPi - t0) - qo;
+    if (dot3(f, f) < dot3(a, a)) {
+        t = kTwoPi - t0;
+        dir = dir * -1.f;
+    }
+    if (t <= cap) return false;
+    nv = dir * cap;
+    const float out = dir.x * w[0] + dir.y * w[1] + dir.z * w[2];
+    if (out > 0.f) { w[0] -= out * dir.x; w[1] -= out * dir.y; w[2] -= out * dir.z; }
+    return true;
+}
+
+// The next substep's limit rows from joint b's exp map th and velocity u (lane = body b; every
+// lane calls, the root and lanes >= NB with on = false): which rows are emitted, their gap and
+// direction, read by the drive terms (a joint on its limit cannot give way) and by the contact
+// phase (the limit slots). Evaluated where q and u are set -- the state load, then each
+// integration but the last -- so no substep re-reads them for it.
+HE_DEV void limit_detect(Lds& L, int lane, bool joint, f3 th, f3 u, const he_sim_params& sp) {
+    float lg = 0.f;
+    f3 ld = f3{0.f, 0.f, 0.f};
+    const bool on = joint && angle_row(th, u, sp, lg, ld);
+    const uint64_t bm = __ballot(on);
+    if (on) {
+        float* lr = limit_rows(L) + 4 * (lane - 1);
+        lr[0] = lg; lr[1] = -ld.x; lr[2] = -ld.y; lr[3] = -ld.z;  // the row is -q^
+    }
+    if (lane == 0) L.limmask = (uint32_t)bm;
+}
 
 // terrain constants of the env, read once per contact phase (slope normal, step field)
 struct Terrain {
@@ -1054,20 +1096,6 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         }
         if (act)
             for (int x = 0; x < 6; ++x) L.Acc[b][x] = A[x];
-        // joint-angle limits of this substep (lane = body b >= 1): which rows are emitted, their
-        // gap and direction (LimitRows), read by the drive terms (a joint on its limit cannot give
-        // way) and by the contact phase (the limit slots)
-        if (sp.joint_limits) {
-            float lg = 0.f;
-            f3 ld = f3{0.f, 0.f, 0.f};
-            const bool on = act && b > 0 && angle_row(L, b, sp, lg, ld);
-            const uint64_t bm = __ballot(on);
-            if (on) {
-                float* lr = limit_rows(L) + 4 * (b - 1);
-                lr[0] = lg; lr[1] = -ld.x; lr[2] = -ld.y; lr[3] = -ld.z;  // the row is -q^
-            }
-            if (lane == 0) L.limmask = (uint32_t)bm;
-        }
     }
     sync();
 #if HE_KIN_AXES_FLAT
@@ -1961,6 +1989,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     // damping, the angular-velocity clamp and the semi-implicit position update in one pass per
     // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
     // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
+    f3 lim_th = f3{0.f, 0.f, 0.f}, lim_u = f3{0.f, 0.f, 0.f};  // the joint's new q and u
     if (lane < NB) {
         const bool root = lane == 0;
         const int d0 = root ? 0 : 6 + 3 * (lane - 1);
@@ -1982,13 +2011,22 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int c = 0; c < 3; ++c) L.root_pos[c] += dt * L.uf[3 + c];
             L.root_q[0] = nq.x; L.root_q[1] = nq.y; L.root_q[2] = nq.z; L.root_q[3] = nq.w;
         } else {
-            const f3 nv = pqlog(nq);
+            const f3 qo = f3{L.q[d], L.q[d + 1], L.q[d + 2]};
+            f3 nv = pqlog(nq);
+            f4 nql = nq;
+            if (p.joint_limits && limit_clamp(qo, nv, w)) {  // rare: the limit rows lost
+                L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
+                nql = pqexp(nv);
+            }
             L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
             if (HE_KIN_QCACHE) {
-                L.qloc[lane][0] = nq.x; L.qloc[lane][1] = nq.y; L.qloc[lane][2] = nq.z; L.qloc[lane][3] = nq.w;
+                L.qloc[lane][0] = nql.x; L.qloc[lane][1] = nql.y; L.qloc[lane][2] = nql.z; L.qloc[lane][3] = nql.w;
             }
+            lim_th = nv;
+            lim_u = f3{w[0], w[1], w[2]};
         }
     }
+    if (p.joint_limits && !last) limit_detect(L, lane, lane >= 1 && lane < NB, lim_th, lim_u, p);
     sync();
     STAMP(12);
 }
@@ -2061,6 +2099,12 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         __builtin_memcpy(L.imbook, &bk, sizeof(ImitBook));
     }
     sync();
+    if (a.p.joint_limits) {  // the first substep's limit rows, from the loaded state
+        const bool joint = lane >= 1 && lane < NB;
+        const int d = 3 * (joint ? lane - 1 : 0);
+        limit_detect(L, lane, joint, f3{L.q[d], L.q[d + 1], L.q[d + 2]}, f3{L.u0[6 + d], L.u0[7 + d], L.u0[8 + d]}, a.p);
+        sync();
+    }
     const float* ms = a.mass_scale ? a.mass_scale + (size_t)e * NB : nullptr;
     float mu = a.friction ? a.friction[e] : a.p.friction;
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;

@@ -6,7 +6,8 @@ bench's size (4096 envs) where the oracle is too slow to follow every env:
   engine's states);
 * configs[1] PD stand-still at full size: after a 5 s settle every env stands still, its feet on
   the plane within the Baumgarte steady state;
-* joint angles never leave |q| <= pi under saturated random actions (the joint-angle limit rows).
+* joint angles never wrap past pi under saturated random actions (limit rows + the integration's
+  backstop).
 """
 import numpy as np
 import pytest
@@ -126,9 +127,14 @@ def test_gpu_full_size_stand_still(he_model, model):
     assert gaps.min() > -2e-3 and gaps.min() < 0.02
 
 
-def test_gpu_joint_angles_stay_inside_pi(he_model, model):
-    """Saturated random actions (the PD scale x U(-1, 1): knee-y targets up to +-5 rad) on 4096
-    standing envs for 2 s: no joint's rotation angle reaches pi (the limit rows hold it at pi - 0.02)."""
+def test_gpu_joint_angles_never_wrap(he_model, model):
+    """Saturated random actions (the PD scale x U(-1, 1): targets past pi on every joint, knee-y up
+    to +-5 rad) on 4096 standing envs, one substep per launch: no joint's exp map ever passes
+    pi - 0.01 or comes back from the log on the far side of pi. The limit rows alone do not
+    guarantee it in this regime (a knee folded against a deep self contact has no solution, and
+    joints reach the 100 rad/s cap), so the integration's backstop (limit_clamp) is what this pins.
+    The regime itself is violent: 500 N m on every joint spins light links at the cap and the
+    bodies fly; finiteness is asserted, not plausibility."""
     from humanoid_amd.model import pd_action_offset_scale
     n = 4096
     rng = np.random.default_rng(8)
@@ -136,12 +142,19 @@ def test_gpu_joint_angles_stay_inside_pi(he_model, model):
     eng = _engine(he_model, n)
     root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
     _load(eng, root, dof)
-    worst = 0.0
-    for _ in range(60):
+    cap = np.pi - 0.01
+    worst, flips = 0.0, 0
+    for _ in range(30):
         a = rng.uniform(-1.0, 1.0, (n, 69)).astype(np.float32)
         eng.dof_targets.copy_(torch.as_tensor(off + sc * a, device="cuda:0"))
-        eng.simulate(2)
-        q = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3)
-        worst = max(worst, float(q.norm(dim=-1).max()))
-    assert worst < np.pi, worst
-    assert torch.isfinite(eng.root_states).all()
+        for _sub in range(2):
+            q0 = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3).clone()
+            eng.simulate(1)
+            q1 = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3)
+            t1 = q1.norm(dim=-1, keepdim=True)
+            far = -q1 / t1.clamp_min(1e-12) * (2 * np.pi - t1)  # the same rotation past pi
+            flips += int(((far - q0).norm(dim=-1) < (q1 - q0).norm(dim=-1)).sum())
+            worst = max(worst, float(t1.max()))
+    assert worst <= cap + 1e-5, worst
+    assert flips == 0, flips
+    assert torch.isfinite(eng.root_states).all() and torch.isfinite(eng.dof_state).all()

@@ -563,3 +563,29 @@ def test_model_with_more_boxes_than_corner_lanes_is_refused(he_model):
     m.geom_type[5] = 7
     with pytest.raises(EngineError, match="geom type 7"):
         Engine(m, 4, device=0)
+
+
+def test_limit_backstop_matches_oracle(he_model, model):
+    """The integration's limit backstop (limit_clamp) on the GPU: joints 5 mrad inside the limit
+    moving outward at 60 rad/s with rows that cannot act (no sweeps), and the same with the rows
+    (which then hold first); both as the oracle, the clamped joints at pi - 0.01 on their side."""
+    n = 16
+    rng = np.random.default_rng(3)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    root[:, 2] += 1.5
+    axis = rng.standard_normal((n, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    j = rng.integers(0, 23, n)
+    for e in range(n):
+        dof[e, 3 * j[e]:3 * j[e] + 3, 0] = (axis[e] * (np.pi - 0.025)).astype(np.float32)
+        dof[e, 3 * j[e]:3 * j[e] + 3, 1] = (axis[e] * 60.0).astype(np.float32)
+    targets = np.zeros((n, 69), np.float32)
+    sim = dict(self_collision=0, kp_scale=0.0, kd_scale=0.0)
+    eng, _ = _physics_compare(he_model, root, dof, targets, substeps=1, steps=1, max_skip=0.0,
+                              solver_iterations=0, warm_start=0, **sim)
+    q = eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0].reshape(n, 23, 3)
+    t = np.linalg.norm(q[np.arange(n), j].astype(np.float64), axis=1)
+    np.testing.assert_allclose(t, np.pi - 0.01, atol=2e-6)
+    assert ((q[np.arange(n), j] * axis).sum(1) > 0).all()
+    # with the rows (one policy step: 60 rad/s joints spread a 1e-4 m difference within ~3 steps)
+    _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, max_skip=0.0, **sim)

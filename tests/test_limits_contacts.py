@@ -145,3 +145,43 @@ def test_cache_signature_invalidates_on_external_write(he_model, model):
     O.physics_step(he_model, sp, r3, d3, targets, 2, cache=O.new_cache(2))
     np.testing.assert_array_equal(r2[1], r3[1])
     np.testing.assert_array_equal(d2[1], d3[1])
+
+
+def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
+    """A joint 5 mrad inside its limit with 60 rad/s outward (one substep covers 1 rad) and rows that
+    cannot act (no solver sweeps: they stand for a limit against a contact it cannot win): the
+    integration's backstop (limit_clamp) keeps the rotation angle at pi - 0.01 on the same side of
+    pi, with the outward rate removed; joints inside the limit are left alone. With the sweeps the
+    row alone holds it at pi - 0.02."""
+    rng = np.random.default_rng(3)
+    n = 4
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    root[:, 2] += 1.5
+    axis = rng.standard_normal((n, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    j = 10  # Neck's joint (body 11): a light link
+    dof[:, 3 * j:3 * j + 3, 0] = (axis * (np.pi - 0.025)).astype(np.float32)
+    dof[:, 3 * j:3 * j + 3, 1] = (axis * 60.0).astype(np.float32)
+    sp = _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0, warm_start=0)
+    r, d = root.copy(), dof.copy()
+    O.physics_step(he_model, sp, r, d, np.zeros((n, 69), np.float32), 1)
+    q = d[:, 3 * j:3 * j + 3, 0].astype(np.float64)
+    u = d[:, 3 * j:3 * j + 3, 1].astype(np.float64)
+    t = np.linalg.norm(q, axis=1)
+    np.testing.assert_allclose(t, np.pi - 0.01, atol=1e-6)
+    assert ((q * axis).sum(1) > 0).all()  # not wrapped to the far side
+    assert ((u * q).sum(1) / t <= 1e-6).all()  # no outward rate left
+    # the other joints equal a run without limits (the backstop acts only past pi - 0.01)
+    r2, d2 = root.copy(), dof.copy()
+    O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0,
+                                                     warm_start=0, joint_limits=0),
+                   r2, d2, np.zeros((n, 69), np.float32), 1)
+    others = [k for k in range(23) if k != j]
+    qs = d[:, :, 0].reshape(n, 23, 3)[:, others]
+    np.testing.assert_array_equal(qs, d2[:, :, 0].reshape(n, 23, 3)[:, others])
+    # with the sweeps, the limit row holds it first, at pi - 0.02
+    r3, d3 = root.copy(), dof.copy()
+    O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0), r3, d3,
+                   np.zeros((n, 69), np.float32), 1)
+    t3 = np.linalg.norm(d3[:, 3 * j:3 * j + 3, 0].astype(np.float64), axis=1)
+    assert (t3 < np.pi - 0.015).all() and (t3 > np.pi - 0.03).all()
