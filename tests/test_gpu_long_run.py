@@ -57,6 +57,9 @@ def test_long_run_tracking_configs2(model):
 
 
 def test_long_run_saturated_actions_dr_terrain(model):
+    """Saturated actions are the violent regime of DESIGN §5 (500 N m drives spin light links at the
+    100 rad/s cap and bodies fly): asserted is what must hold even there -- finite state, no joint
+    past the limit backstop, capacity, reward range, flat-plane envs above the plane."""
     ro = _rollout("dr", model, seed=3)
     rng = np.random.default_rng(5)
     worst = 0.0
