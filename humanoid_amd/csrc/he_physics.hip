@@ -220,23 +220,22 @@ HE_DEV float* limit_rows(Lds& L) { return &L.ct1[0][0]; }
 static_assert(4 * (NB - 1) <= 6 * MAXC, "the limit rows fit the ct1 / ct2 arrays");
 // Backstop when the limit rows lose (oracle/he_oracle_physics.c limit_clamp): a limit against a
 // deep self contact has no solution, and a joint near 100 rad/s can cross the margin in one
-// substep. The new exp map nv is unwrapped against the old one qo (a rotation that crossed pi
-// comes back from the log on the far side, axis flipped, which would reverse the joint's PD error
-// and spin it), then held at pi - kLimitGuard / 2 with the outward rate q^ . w removed. Returns
-// whether it acted (nv and w changed).
-HE_DEV bool limit_clamp(f3 qo, f3& nv, float (&w)[3]) {
+// substep. nq = exp(q_old) (x) exp(dt w) before the log (exp(q_old) has w >= 0: the kinematics'
+// and this function's qloc): its scalar part is negative when the rotation went past pi this
+// substep, and the log then comes back on the far side with the axis flipped, which would reverse
+// the joint's PD error and spin it. The angle is continued past pi instead, then held at
+// pi - kLimitGuard / 2 on the joint's side with the outward rate q^ . w removed. Returns whether it
+// acted (nv and w changed).
+HE_DEV bool limit_clamp(f4 nq, f3& nv, float (&w)[3]) {
     constexpr float kTwoPi = 6.28318530717959f;
     constexpr float cap = 3.14159265358979f - 0.5f * kLimitGuard;
-    // a joint inside the cap that started more than 1.7 rad from pi (100 rad/s x 1/60 s) can
-    // neither be past the cap nor have crossed pi: the common case, one branch
-    if (dot3(nv, nv) <= cap * cap && dot3(qo, qo) < 2.07f) return false;
+    constexpr float kWcap = 0.00499997917f;  // cos(cap / 2)
+    if (nq.w >= kWcap) return false;         // inside the cap, not crossed: the common case
     const float t0 = sqrtf(dot3(nv, nv));
     if (!(t0 >= 1e-12f)) return false;
     f3 dir = nv * (1.0f / t0);
     float t = t0;
-    const f3 a = nv - qo;
-    const f3 f = dir * -(kTwoPi - t0) - qo;
-    if (dot3(f, f) < dot3(a, a)) {
+    if (nq.w < 0.f) {
         t = kTwoPi - t0;
         dir = dir * -1.f;
     }
@@ -2011,10 +2010,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int c = 0; c < 3; ++c) L.root_pos[c] += dt * L.uf[3 + c];
             L.root_q[0] = nq.x; L.root_q[1] = nq.y; L.root_q[2] = nq.z; L.root_q[3] = nq.w;
         } else {
-            const f3 qo = f3{L.q[d], L.q[d + 1], L.q[d + 2]};
             f3 nv = pqlog(nq);
             f4 nql = nq;
-            if (p.joint_limits && limit_clamp(qo, nv, w)) {  // rare: the limit rows lost
+            if (p.joint_limits && limit_clamp(nq, nv, w)) {  // rare: the limit rows lost
                 L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
                 nql = pqexp(nv);
             }

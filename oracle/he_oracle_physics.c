@@ -359,21 +359,18 @@ static void jr_inv_row(const R* th, int c, R* row) {
 #define LIMIT_PI_GUARD 0.02
 /* Backstop when the limit rows lose (a limit against a deep self contact has no solution, and a
  * joint near 100 rad/s can cross the margin in one substep): the rotation angle never passes
- * pi - LIMIT_PI_GUARD / 2. The new exp map is first unwrapped against the old one (a rotation
- * that crossed pi comes back from the log on the far side, axis flipped, which would reverse the
- * joint's PD error and spin it), then held at that angle with the outward rate q^ . u removed. */
-static void limit_clamp(const R* qold, R* qv, R* u) {
+ * pi - LIMIT_PI_GUARD / 2. nq = exp(q_old) (x) exp(dt u) before the log: its scalar part is
+ * cos(angle / 2), negative when the rotation went past pi this substep (exp(q_old) has w >= 0 and
+ * one substep turns by less than pi), in which case the log comes back on the far side with the
+ * axis flipped -- that would reverse the joint's PD error and spin it. The angle is continued past
+ * pi instead, then held at the cap on the joint's side with the outward rate q^ . u removed. */
+static void limit_clamp(const R* nq, R* qv, R* u) {
     const R cap = M_PI - 0.5 * LIMIT_PI_GUARD;
+    if (nq[3] >= cos(0.5 * cap)) return; /* inside the cap, not crossed: the common case */
     R t = sqrt(dot3(qv, qv));
     if (t < 1e-12) return;
     R dir[3] = {qv[0] / t, qv[1] / t, qv[2] / t};
-    R d_near = 0, d_far = 0;  /* distance of the log and of its continuation past pi to the old q */
-    for (int c = 0; c < 3; ++c) {
-        R a = qv[c] - qold[c], f = -dir[c] * (2 * M_PI - t) - qold[c];
-        d_near += a * a;
-        d_far += f * f;
-    }
-    if (d_far < d_near) {
+    if (nq[3] < 0) {
         t = 2 * M_PI - t;
         for (int c = 0; c < 3; ++c) dir[c] = -dir[c];
     }
@@ -840,13 +837,12 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     for (int b = 1; b < NB; ++b) {
         R* qv = &s->q[3 * (b - 1)];
         R ql[4], dq[4], nq[4], dw[3] = {dt * s->u[3 * (b - 1)], dt * s->u[3 * (b - 1) + 1], dt * s->u[3 * (b - 1) + 2]};
-        const R qold[3] = {qv[0], qv[1], qv[2]};
         qexp(qv, ql);
         qexp(dw, dq);
         qmul(ql, dq, nq);
         qnormalize(nq);
         qlog(nq, qv);
-        if (p->joint_limits) limit_clamp(qold, qv, &s->u[3 * (b - 1)]);
+        if (p->joint_limits) limit_clamp(nq, qv, &s->u[3 * (b - 1)]);
     }
 }
 
