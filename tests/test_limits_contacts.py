@@ -185,3 +185,25 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
                    np.zeros((n, 69), np.float32), 1)
     t3 = np.linalg.norm(d3[:, 3 * j:3 * j + 3, 0].astype(np.float64), axis=1)
     assert (t3 < np.pi - 0.015).all() and (t3 > np.pi - 0.03).all()
+
+
+def test_moderate_random_actions_stay_physical(he_model, model):
+    """DESIGN §5's boundary of the violent regime, as a regression guard: random actions
+    U(-0.5, 0.5) of the PD scale on standing bodies for 2 s keep every root below 10 m/s and
+    no joint past the limit (the saturated U(-1, 1) regime spins light links at the 100 rad/s cap
+    and throws bodies at 10^2 m/s in the same equations)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    n = 64
+    rng = np.random.default_rng(8)
+    off, sc = pd_action_offset_scale(model)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    sp = _abi.default_sim_params()
+    cache = O.new_cache(n)
+    vmax = 0.0
+    for _ in range(60):
+        a = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+        O.physics_step(he_model, sp, root, dof, (off + sc * a).astype(np.float32), 2, cache=cache)
+        vmax = max(vmax, float(np.linalg.norm(root[:, 7:10], axis=1).max()))
+    q = np.linalg.norm(dof[..., 0].reshape(n, 23, 3), axis=-1)
+    assert vmax < 10.0, vmax
+    assert q.max() < np.pi - 0.01
