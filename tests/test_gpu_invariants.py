@@ -158,3 +158,26 @@ def test_gpu_joint_angles_never_wrap(he_model, model):
     assert worst <= cap + 1e-5, worst
     assert flips == 0, flips
     assert torch.isfinite(eng.root_states).all() and torch.isfinite(eng.dof_state).all()
+
+
+def test_gpu_moderate_random_actions_stay_physical(he_model, model):
+    """The engine side of tests/test_limits_contacts.py::test_moderate_random_actions_stay_physical
+    at full size: U(-0.25, 0.25) random actions on 4096 standing envs for 2 s keep every root below
+    10 m/s and every joint inside the limit (at U(-0.5, 0.5) 6 of 4096 envs already run
+    away, profiles/r02/action_regimes.json)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    n = 4096
+    rng = np.random.default_rng(8)
+    off, sc = pd_action_offset_scale(model)
+    eng = _engine(he_model, n)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    _load(eng, root, dof)
+    vmax = 0.0
+    for _ in range(60):
+        a = rng.uniform(-0.25, 0.25, (n, 69)).astype(np.float32)
+        eng.dof_targets.copy_(torch.as_tensor(off + sc * a, device="cuda:0"))
+        eng.simulate(2)
+        vmax = max(vmax, float(eng.root_states[:, 7:10].norm(dim=1).max()))
+    q = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3).norm(dim=-1)
+    assert vmax < 10.0, vmax
+    assert float(q.max()) < np.pi - 0.01

@@ -201,7 +201,7 @@ def test_moderate_random_actions_stay_physical(he_model, model):
     cache = O.new_cache(n)
     vmax = 0.0
     for _ in range(60):
-        a = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+        a = rng.uniform(-0.25, 0.25, (n, 69)).astype(np.float32)
         O.physics_step(he_model, sp, root, dof, (off + sc * a).astype(np.float32), 2, cache=cache)
         vmax = max(vmax, float(np.linalg.norm(root[:, 7:10], axis=1).max()))
     q = np.linalg.norm(dof[..., 0].reshape(n, 23, 3), axis=-1)
