@@ -20,9 +20,10 @@ SOURCES = [
     ("he_imitation.hip", ["-ffp-contract=off"]),
     # no SLP vectorisation: the compiler's own packed-FP32 pairing costs more moves than it saves;
     # the elimination issues its v_pk_fma_f32 explicitly (he_regla.h)
-    # iterative-ilp scheduling: +1% on the bench workload against the default (A/B, r01)
+    # max-ilp scheduling: +1.0% against iterative-ilp (r02 A/B, 3 of 3 passes, bit-identical results),
+    # which was +1% against the default (r01); iterative-minreg -4%
     ("he_physics.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize",
-                        "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]),
+                        "-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
     ("he_ingest.hip", []),
     ("he_rollout.hip", ["-ffp-contract=off"]),  # GAE: the Cython module's float32 rounding
     ("he_engine.cpp", ["-x", "hip"]),
