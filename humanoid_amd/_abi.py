@@ -39,6 +39,7 @@ class HeSimParams(C.Structure):
         ("max_contacts", C.c_int32), ("kp_scale", C.c_float), ("kd_scale", C.c_float), ("terrain", C.c_int32),
         ("terrain_slope", C.c_float), ("step_height", C.c_float), ("step_length", C.c_float),
         ("joint_limits", C.c_int32), ("limit_margin", C.c_float), ("warm_start", C.c_int32), ("solver_tolerance", C.c_float),
+        ("bias_predictor", C.c_int32),
     ]
 
 
@@ -114,6 +115,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.limit_margin = 0.1
     p.warm_start = 1
     p.solver_tolerance = 0.0
+    p.bias_predictor = 0
     for k, v in kw.items():
         setattr(p, k, v)
     return p

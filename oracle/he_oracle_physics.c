@@ -573,6 +573,47 @@ typedef struct warm_cache {
 } warm_cache;
 
 /* one substep; updates s in place */
+/* Velocity-dependent + gravity bias at the velocities of state sv (the bias predictor,
+ * he_sim_params.bias_predictor): the same RNEA as the substep's, with sv's body velocities. */
+static void bias_at(const he_model* m, const topo* t, const he_sim_params* p, const env_state* sv, const kin* k,
+                    const sinertia* I, R* bias) {
+    static __thread kin kv;
+    kinematics(m, t, sv, &kv);
+    R Aacc[NB][6], F[NB][6];
+    Aacc[0][0] = Aacc[0][1] = Aacc[0][2] = 0;
+    {
+        R vxw[3];
+        cross3(sv->root_v, sv->root_w, vxw);
+        for (int c = 0; c < 3; ++c) Aacc[0][3 + c] = vxw[c] - p->gravity[c];
+    }
+    for (int b = 1; b < NB; ++b) {
+        int pb = m->parents[b];
+        for (int i = 0; i < 6; ++i) Aacc[b][i] = Aacc[pb][i];
+        for (int c = 0; c < 3; ++c) {
+            R cr[6];
+            crm(kv.V[b], k->S[t->body_dof0[b] + c], cr);
+            R uu = sv->u[3 * (b - 1) + c];
+            for (int i = 0; i < 6; ++i) Aacc[b][i] += cr[i] * uu;
+        }
+    }
+    for (int b = 0; b < NB; ++b) {
+        R IA[6], IV[6], x[6];
+        si_apply(&I[b], Aacc[b], IA);
+        si_apply(&I[b], kv.V[b], IV);
+        crf(kv.V[b], IV, x);
+        for (int i = 0; i < 6; ++i) F[b][i] = IA[i] + x[i];
+    }
+    for (int b = NB - 1; b > 0; --b) {
+        int pb = m->parents[b];
+        for (int i = 0; i < 6; ++i) F[pb][i] += F[b][i];
+    }
+    for (int i = 0; i < NG; ++i) {
+        const R* S = k->S[i];
+        const R* f = F[t->dof_body[i]];
+        bias[i] = S[0] * f[0] + S[1] * f[1] + S[2] * f[2] + S[3] * f[3] + S[4] * f[4] + S[5] * f[5];
+    }
+}
+
 static void substep(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
                     R mu, int terrain_kind, step_out* out, warm_cache* ws) {
     static __thread kin k;
@@ -681,6 +722,21 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     for (int c = 0; c < 3; ++c) { u0[c] = s->root_w[c]; u0[3 + c] = s->root_v[c]; }
     for (int d = 0; d < ND; ++d) u0[6 + d] = s->u[d];
     for (int i = 0; i < NG; ++i) uf[i] = u0[i] + du[i];
+    if (p->bias_predictor) {
+        /* The bias (Coriolis, gyroscopic) is explicit: taken at u0, it lets stiff drives on light
+         * links pump energy at dt = 1/60 (the runaway regime). Predictor: the bias
+         * again at the free velocity, and the free velocity corrected through the same factor. */
+        env_state sv = *s;
+        for (int c = 0; c < 3; ++c) { sv.root_w[c] = uf[c]; sv.root_v[c] = uf[3 + c]; }
+        for (int d = 0; d < ND; ++d) sv.u[d] = uf[6 + d];
+        R b2[NG], dc[NG];
+        bias_at(m, t, p, &sv, &k, I, b2);
+        for (int i = 0; i < NG; ++i) dc[i] = dt * (bias[i] - b2[i]);
+        ltdl_solve_LT(H, t->dof_parent, dc);
+        for (int i = 0; i < NG; ++i) dc[i] /= H[i][i];
+        ltdl_solve_L(H, t->dof_parent, dc);
+        for (int i = 0; i < NG; ++i) uf[i] += dc[i];
+    }
     /* contacts */
     int total = 0;
     int nc = gen_contacts(m, p, &k, s, terrain_kind, mu, cs, &total);

@@ -589,3 +589,13 @@ def test_limit_backstop_matches_oracle(he_model, model):
     assert ((q[np.arange(n), j] * axis).sum(1) > 0).all()
     # with the rows (one policy step: 60 rad/s joints spread a 1e-4 m difference within ~3 steps)
     _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, max_skip=0.0, **sim)
+
+
+def test_bias_predictor_refused_until_the_kernel_has_it(he_model):
+    """he_sim_params.bias_predictor is the oracle's: the engine refuses it at
+    he_create with the reason rather than silently stepping without it."""
+    from humanoid_amd.engine import Engine, EngineError
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+    with pytest.raises(EngineError, match="bias_predictor"):
+        Engine(he_model, 4, device=0, sim_params=_abi.default_sim_params(bias_predictor=1))

@@ -194,3 +194,51 @@ def test_penetration_within_contact_offset(he_model, model):
         gaps = cases.ground_gaps(model, out["rb_state"])
         assert gaps.min() > -2e-3, gaps.min()
         assert gaps.min() < sp.contact_offset  # bodies rest on the plane
+
+
+def _internal_ke(he_model, model, sp, root, dof):
+    me = O.momentum_energy(he_model, sp, root, dof)
+    M = float(np.sum(model.mass))
+    return me[:, 6] - 0.5 * (me[:, :3] ** 2).sum(1) / M
+
+
+def test_bias_predictor_tames_the_runaway(he_model, model):
+    """DESIGN §5's runaway regime, on the oracle: airborne bodies (no contact) under random targets
+    U(+-0.5) of the PD scale renewed every step gain internal kinetic energy without bound at the
+    configured 1/60 s substep (the velocity-dependent bias is explicit); with the bias predictor
+    (he_sim_params.bias_predictor: the bias again at the free velocity, one more solve) it stays at
+    the drives' level. The same runs at U(+-0.25) are clean either way."""
+    from humanoid_amd.model import pd_action_offset_scale
+    off, sc = pd_action_offset_scale(model)
+    n = 48
+    res = {}
+    for pred in (0, 1):
+        rng = np.random.default_rng(8)
+        root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+        root[:, 2] += 200.0
+        sp = _abi.default_sim_params(self_collision=0, bias_predictor=pred)
+        cache = O.new_cache(n)
+        for _ in range(90):
+            a = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+            O.physics_step(he_model, sp, root, dof, (off + sc * a).astype(np.float32), 2, cache=cache)
+        res[pred] = float(np.median(_internal_ke(he_model, model, sp, root, dof)))
+    assert res[0] > 5e3, res  # the defect, pinned so the kernel port can be checked against it
+    assert res[1] < 1e3, res
+
+
+def test_bias_predictor_keeps_standing_bodies_grounded(he_model, model):
+    """Standing bodies under U(+-0.75) random actions for 2 s: with the predictor no root exceeds
+    20 m/s (without it, most envs run away: profiles/r02/action_regimes.json)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    off, sc = pd_action_offset_scale(model)
+    n = 48
+    rng = np.random.default_rng(8)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    sp = _abi.default_sim_params(bias_predictor=1)
+    cache = O.new_cache(n)
+    vmax = 0.0
+    for _ in range(60):
+        a = rng.uniform(-0.75, 0.75, (n, 69)).astype(np.float32)
+        O.physics_step(he_model, sp, root, dof, (off + sc * a).astype(np.float32), 2, cache=cache)
+        vmax = max(vmax, float(np.linalg.norm(root[:, 7:10], axis=1).max()))
+    assert vmax < 20.0, vmax
