@@ -105,8 +105,6 @@ int he_create(const he_sim_params* params, int device, he_engine** out) {
     if (params->max_contacts < 1 || params->max_contacts > HE_MAX_CONTACTS)
         return fail("he_create: max_contacts must be in [1, %d]", HE_MAX_CONTACTS);
     if (params->dt <= 0.f) return fail("he_create: dt must be positive");
-    if (params->bias_predictor)
-        return fail("he_create: bias_predictor is implemented in the CPU oracle only (the kernel follows in round 3)");
     he_engine* h = new he_engine();
     h->device = device;
     h->params = *params;

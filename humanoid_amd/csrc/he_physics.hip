@@ -1172,6 +1172,88 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
     }
 }
 
+// ---------------------------------------------------------------------------------- bias predictor
+// he_sim_params.bias_predictor (oracle/he_oracle_physics.c: substep, bias_at): the velocity-dependent
+// bias (Coriolis, gyroscopic; gravity cancels) again at the free velocity uf, and the free velocity
+// corrected through the same factor: yh += D^-1/2 L^-T dt (bias(u0) - bias(uf)). Runs between the
+// factorisation and the contact phase, with the factor in Lp and the first bias's subtree forces
+// in F. Scratch: uf, V (the final kinematics rewrites it), Acc (the contact phase's scratch after),
+// Ib (own inertias, stored by the force pass).
+HE_DEV void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p) {
+    using namespace regla;
+    const float dt = p.dt;
+    {  // uf = u0 + L^-1 D^-1/2 yh
+        float r1[regla::kRowRegs], r2[regla::kRowRegs];
+        load_rows(L, T, lane, r1, r2);
+        float t1 = L.yh[lane] * L.sDinv[lane];
+        float t2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
+        solve_L(r1, r2, lane, t1, t2);
+        L.uf[lane] = L.u0[lane] + t1;
+        if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + t2;
+    }
+    sync();
+    const bool bl = lane < NB;
+    const int b = bl ? lane : 0;
+    if (bl) {  // joint velocities S_b uf_b (the root's S are the unit axes) -> Acc
+        float vj[6];
+        if (b == 0) {
+            for (int x = 0; x < 6; ++x) vj[x] = L.uf[x];
+        } else {
+            const int d0 = T.dof0[b];
+            for (int x = 0; x < 6; ++x)
+                vj[x] = L.S[d0][x] * L.uf[d0] + L.S[d0 + 1][x] * L.uf[d0 + 1] + L.S[d0 + 2][x] * L.uf[d0 + 2];
+        }
+        for (int x = 0; x < 6; ++x) L.Acc[b][x] = vj[x];
+    }
+    sync();
+    float V[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (bl) {  // body velocities: the chain's joint velocities summed, root first
+        for (int k = 0; k <= T.depth[b]; ++k) {
+            const int a = T.chain[b][k];
+            for (int x = 0; x < 6; ++x) V[x] += L.Acc[a][x];
+        }
+        for (int x = 0; x < 6; ++x) L.V[b][x] = V[x];
+    }
+    sync();
+    float Fb[6];
+    if (bl) {  // RNEA body force at uf: a_b = a_0 + sum over the chain (root excluded) of V_a x S_a uf_a
+        const f3 vxw = cross3(f3{L.uf[3], L.uf[4], L.uf[5]}, f3{L.uf[0], L.uf[1], L.uf[2]});
+        float A[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
+        for (int k = 1; k <= T.depth[b]; ++k) {
+            const int a = T.chain[b][k];
+            float cr[6];
+            crm(L.V[a], L.Acc[a], cr);
+            for (int x = 0; x < 6; ++x) A[x] += cr[x];
+        }
+        float IA[6], IV[6], X[6];
+        si_apply(L.Ib[b], A, IA);
+        si_apply(L.Ib[b], V, IV);
+        crf(V, IV, X);
+        for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
+    }
+    sync();
+    if (bl)
+        for (int x = 0; x < 6; ++x) L.Acc[b][x] = Fb[x];
+    sync();
+    // lane = dof (then dofs 64..74 on lanes 0..10): dc_i = dt (S_i . F_b(u0) - S_i . F_b(uf)) with the
+    // subtree sums of the new body forces
+    auto corr = [&](int i) {
+        const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
+        const uint32_t sm = T.sub_mask[bi];
+        float fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int d = 0; d < NB; ++d)
+            if ((sm >> d) & 1u)
+                for (int x = 0; x < 6; ++x) fs[x] += L.Acc[d][x];
+        return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], fs));
+    };
+    float c1 = corr(lane);
+    float c2 = lane < NH ? corr(64 + lane) : 0.f;
+    regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+    L.yh[lane] += c1 * L.sDinv[lane];
+    if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
+    sync();
+}
+
 // ---------------------------------------------------------------------------------- fused imitation
 // he_env_step's imitation step (reward / reset / observations + the device reset of flagged envs)
 // as the physics kernel's epilogue, from the post-step state in LDS: the same code as the stand-alone
@@ -1255,6 +1337,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float* o10 = L.Ic[b];  // own inertia; the subtree sums accumulate in place
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
+        if (p.bias_predictor)  // the body's own inertia for the predictor's second RNEA (Ib is free until
+            for (int x = 0; x < 10; ++x) L.Ib[b][x] = o10[x];  // the contact phase's segments)
         float IA[6], IV[6], X[6];
         si_apply(o10, L.Acc[b], IA);
         si_apply(o10, L.V[b], IV);
@@ -1378,6 +1462,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     sync();
     STAMP(5);
+#if HE_ONE_SWEEP
+    if (p.bias_predictor) bias_predictor(L, T, lane, p);
+#else
+#error "the bias predictor is implemented on the one-sweep path (HE_ONE_SWEEP=1)"
+#endif
     // the contact phase's model reads (geometry of the lane's body, self-collision pair indices)
     // depend on nothing computed here: issued now, they land behind the free-velocity sweep
     constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;

@@ -368,6 +368,28 @@ __device__ __forceinline__ void solve_L_gather(const float (&r1)[kRowRegs], cons
     }
 }
 
+// ---------------------------------------------------------------- y <- L^-T y, one vector
+// Lane j holds y_j (and y_{64+j} in y2). The elimination's forward substitution replayed from the
+// stored factor: pivots in kElimOrder (deepest first, so every descendant of K is final before K
+// is read), each ancestor j of K taking y_j -= L[K][j] y_K with L[K][j] = Lp[kPackStart[K] + depth(j)].
+// Used by the bias predictor's correction, once per substep (not on the factor's latency chain).
+template <int J>
+__device__ __forceinline__ void solve_LT_vec(const float* Lp, int dj, int dj2, float& yl, float& y2) {
+    if constexpr (J < NG) {
+        constexpr int K = kElimOrder[J];
+        if constexpr (kDofNanc[K] - 1 > 0) {
+            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
+            if (lanes<lo>()) yl = yl - Lp[kPackStart[K] + dj] * yk;
+            if constexpr (K > 64) {
+                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+                if (lanes<hi>()) y2 = y2 - Lp[kPackStart[K] + dj2] * yk;
+            }
+        }
+        solve_LT_vec<J + 1>(Lp, dj, dj2, yl, y2);
+    }
+}
+
 // ---------------------------------------------------------------- grouped elimination
 // Consecutive steps of kElimOrder whose dofs are mutually independent (neither is an ancestor of
 // the other: different branches) touch disjoint pivots and rows, so a group of them runs as one

@@ -81,8 +81,8 @@ typedef struct he_sim_params {
     float solver_tolerance;          /* m/s: stop the sweeps once no row's velocity moves by more
                                         (|d lambda_r| A_rr) in a sweep; 0 = always solver_iterations */
     int32_t bias_predictor;          /* 1: the velocity-dependent bias re-evaluated at the free
-                                        velocity, one more solve; the CPU oracle has
-                                        it, he_create refuses it until the kernel does (round 3) */
+                                        velocity, one more solve; off by default
+                                        (the reference's PhysX bias is explicit) */
 } he_sim_params;
 
 /* Per-env solver warm-start cache (f32 words; HE_BUF_CONTACT_CACHE), written at the end of every

@@ -591,11 +591,58 @@ def test_limit_backstop_matches_oracle(he_model, model):
     _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, max_skip=0.0, **sim)
 
 
-def test_bias_predictor_refused_until_the_kernel_has_it(he_model):
-    """he_sim_params.bias_predictor is the oracle's: the engine refuses it at
-    he_create with the reason rather than silently stepping without it."""
-    from humanoid_amd.engine import Engine, EngineError
-    if not torch.cuda.is_available():
-        pytest.fail("GPU test run without a visible GPU")
-    with pytest.raises(EngineError, match="bias_predictor"):
-        Engine(he_model, 4, device=0, sim_params=_abi.default_sim_params(bias_predictor=1))
+def test_bias_predictor_airborne_matches_oracle(he_model):
+    """he_sim_params.bias_predictor on the GPU (he_physics.hip: bias_predictor; the bias again at the
+    free velocity, one more L^-1 / L^-T pass through the same factor) against the oracle's
+    (he_oracle_physics.c: substep), airborne actuated bodies, one policy step."""
+    rng = np.random.default_rng(21)
+    root, dof = cases.random_state(64, rng, height=(3.0, 4.0))
+    targets = rng.uniform(-0.5, 0.5, (64, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, self_collision=0, bias_predictor=1, max_skip=0.0,
+                     max_widened=0.0)
+
+
+def test_bias_predictor_trajectories_match_oracle(he_model, model):
+    """The predictor's joint-angle and CoM trajectories at 1e-4 over 10 policy steps: airborne with
+    self collision, and the PD stand-still on the plane (contacts, warm start)."""
+    rng = np.random.default_rng(22)
+    root, dof = cases.random_state(32, rng, height=(6.0, 7.0), ang=0.4, vel=0.5)
+    targets = rng.uniform(-0.5, 0.5, (32, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, steps=10, bias_predictor=1, max_skip=0.0, max_widened=0.01)
+    root, dof = cases.standing_state(model, 32, rng, xy_jitter=1.0)
+    _physics_compare(he_model, root, dof, np.zeros((32, 69), np.float32), steps=10, bias_predictor=1,
+                     max_skip=0.0, max_widened=0.05)
+
+
+def test_bias_predictor_tames_the_runaway_on_gpu(he_model, model):
+    """DESIGN §5's runaway regime through the engine: airborne bodies under random targets U(+-0.5)
+    of the PD scale renewed every policy step for 3 s. Without the predictor the median internal
+    kinetic energy runs away (> 5e3 J, as the oracle's CPU test pins); with it, it stays at the
+    drives' level (< 1e3 J)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    _require_gpu()
+    off, sc = pd_action_offset_scale(model)
+    n = 256
+    M = float(np.sum(model.mass))
+    res = {}
+    for pred in (0, 1):
+        rng = np.random.default_rng(8)
+        root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+        root[:, 2] += 200.0
+        eng = make_engine(he_model, n, self_collision=0, bias_predictor=pred)
+        eng.root_states.copy_(cu(root))
+        eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
+        for _ in range(90):
+            a = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+            eng.dof_targets.copy_(cu((off + sc * a).astype(np.float32)))
+            eng.simulate(2)
+        torch.cuda.synchronize()
+        rg = eng.root_states.cpu().numpy()
+        dg = eng.dof_state.view(n, 69, 2).cpu().numpy()
+        assert np.isfinite(rg).all() and np.isfinite(dg).all()
+        me = O.momentum_energy(eng.he_model, _abi.default_sim_params(self_collision=0), rg, dg)
+        res[pred] = float(np.median(me[:, 6] - 0.5 * (me[:, :3] ** 2).sum(1) / M))
+        del eng
+    print(f"median internal KE after 3 s: {res}")
+    assert res[0] > 5e3, res
+    assert res[1] < 1e3, res
