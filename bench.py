@@ -46,6 +46,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=20)
+    ap.add_argument("--bias-predictor", action="store_true",
+                    help="he_sim_params.bias_predictor on (off by default, as the reference's explicit bias)")
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
@@ -130,7 +132,8 @@ class Rollout:
         self.fused = bool(getattr(args, "fused", False))
         n = args.num_envs
         tables, actions, rng = build_workload(args, model, rank)
-        sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0)
+        sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0,
+                                      bias_predictor=int(getattr(args, "bias_predictor", False)))
         self.eng = Engine(model, n, device=device_index, sim_params=sim, start_xy=rng.uniform(-1, 1, (n, 2)))
         dev = self.eng.device
         self.eng.load_motions(tables)
@@ -261,7 +264,8 @@ def cpu_baseline(args, model):
     tables, actions, rng = build_workload(a, model, 0)
     n = a.num_envs
     hm = _abi.make_model(model)
-    sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0)
+    sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0,
+                                      bias_predictor=int(getattr(args, "bias_predictor", False)))
     mt = O.MotionTables.from_tables(tables)
     p = _abi.imitation_params()
     off, sc = pd_action_offset_scale(model)
@@ -428,7 +432,7 @@ def main():
                                     "imitation": "configs[2]: 4096 humanoids over 128 synthetic clips, full PHC reward",
                                     "dr": "configs[4]: 4096 envs, mass/friction randomisation + 3 terrains"}[args.config],
                        "num_envs_per_gpu": n, "substeps": 2, "sim_dt": 1 / 60, "max_contacts": args.max_contacts,
-                       "parallelism": f"replicas{world}"},
+                       "bias_predictor": int(args.bias_predictor), "parallelism": f"replicas{world}"},
             # the physics kernel is bound by the latency of its per-env serial chains (elimination,
             # Gauss-Seidel sweeps, triangular solves) at 2 waves / SIMD, not by HBM or the matrix
             # cores: priced against the FP32 vector / matrix peak with the canonical dense-equivalent

@@ -100,6 +100,12 @@ struct Lds {
 #ifndef HE_ONE_SWEEP
 #define HE_ONE_SWEEP 1
 #endif
+#ifndef HE_PRED_LEVELS  // the predictor's subtree sums by body levels (1) or per dof lane (0)
+#define HE_PRED_LEVELS 0
+#endif
+#ifndef HE_BIAS_PREDICTOR  // 0: the predictor compiled out (diagnostic A/B of its code's cost when off)
+#define HE_BIAS_PREDICTOR 1
+#endif
 #ifndef HE_FAC_PIPE
 #define HE_FAC_PIPE 1
 #endif
@@ -1179,7 +1185,17 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // factorisation and the contact phase, with the factor in Lp and the first bias's subtree forces
 // in F. Scratch: uf, V (the final kinematics rewrites it), Acc (the contact phase's scratch after),
 // Ib (own inertias, stored by the force pass).
-HE_DEV void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p) {
+#ifndef HE_PRED_NOINLINE  // diagnostic: the predictor as a called function (its own register allocation)
+#define HE_PRED_NOINLINE 0
+#endif
+#if HE_PRED_NOINLINE
+#define HE_PRED_FN __device__ __attribute__((noinline))
+#else
+#define HE_PRED_FN HE_DEV
+#endif
+HE_PRED_FN void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, unsigned long long* stamps,
+                               unsigned long long& t_prev) {
+    (void)stamps; (void)t_prev;
     using namespace regla;
     const float dt = p.dt;
     {  // uf = u0 + L^-1 D^-1/2 yh
@@ -1192,6 +1208,7 @@ HE_DEV void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_par
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + t2;
     }
     sync();
+    STAMP(25);
     const bool bl = lane < NB;
     const int b = bl ? lane : 0;
     if (bl) {  // joint velocities S_b uf_b (the root's S are the unit axes) -> Acc
@@ -1235,8 +1252,18 @@ HE_DEV void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_par
     if (bl)
         for (int x = 0; x < 6; ++x) L.Acc[b][x] = Fb[x];
     sync();
+    STAMP(26);
+#if HE_PRED_LEVELS
+    // subtree sums of the new body forces, in place by body levels (as the first bias's)
+    subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.Acc[0][0], nullptr, lane);
+    auto corr = [&](int i) {
+        const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
+        return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], L.Acc[bi]));
+    };
+#else
     // lane = dof (then dofs 64..74 on lanes 0..10): dc_i = dt (S_i . F_b(u0) - S_i . F_b(uf)) with the
-    // subtree sums of the new body forces
+    // subtree sums of the new body forces (the level-parallel sums measured 2 VGPRs over the
+    // kernel's 2-waves budget)
     auto corr = [&](int i) {
         const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
         const uint32_t sm = T.sub_mask[bi];
@@ -1246,12 +1273,15 @@ HE_DEV void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_par
                 for (int x = 0; x < 6; ++x) fs[x] += L.Acc[d][x];
         return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], fs));
     };
+#endif
     float c1 = corr(lane);
     float c2 = lane < NH ? corr(64 + lane) : 0.f;
+    STAMP(27);
     regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
     L.yh[lane] += c1 * L.sDinv[lane];
     if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
     sync();
+    STAMP(28);
 }
 
 // ---------------------------------------------------------------------------------- fused imitation
@@ -1337,7 +1367,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float* o10 = L.Ic[b];  // own inertia; the subtree sums accumulate in place
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
-        if (p.bias_predictor)  // the body's own inertia for the predictor's second RNEA (Ib is free until
+        if (HE_BIAS_PREDICTOR && p.bias_predictor)  // the body's own inertia for the predictor's second RNEA (Ib is free until
             for (int x = 0; x < 10; ++x) L.Ib[b][x] = o10[x];  // the contact phase's segments)
         float IA[6], IV[6], X[6];
         si_apply(o10, L.Acc[b], IA);
@@ -1463,7 +1493,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     sync();
     STAMP(5);
 #if HE_ONE_SWEEP
-    if (p.bias_predictor) bias_predictor(L, T, lane, p);
+    if (HE_BIAS_PREDICTOR && p.bias_predictor) bias_predictor(L, T, lane, p, stamps, t_prev);
 #else
 #error "the bias predictor is implemented on the one-sweep path (HE_ONE_SWEEP=1)"
 #endif
