@@ -646,3 +646,30 @@ def test_bias_predictor_tames_the_runaway_on_gpu(he_model, model):
     print(f"median internal KE after 3 s: {res}")
     assert res[0] > 5e3, res
     assert res[1] < 1e3, res
+
+
+def test_bias_predictor_keeps_standing_bodies_grounded_on_gpu(he_model, model):
+    """Standing bodies on the plane under U(+-0.75) random actions for 2 s through the engine: with
+    the predictor no root exceeds 20 m/s (the oracle's CPU test, at 256 envs); without it most envs
+    run away (profiles/r02/action_regimes.json), printed for the record."""
+    from humanoid_amd.model import pd_action_offset_scale
+    _require_gpu()
+    off, sc = pd_action_offset_scale(model)
+    n = 256
+    vmax = {}
+    for pred in (0, 1):
+        rng = np.random.default_rng(8)
+        root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+        eng = make_engine(he_model, n, bias_predictor=pred)
+        eng.root_states.copy_(cu(root))
+        eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
+        v = np.zeros(n)
+        for _ in range(60):
+            a = rng.uniform(-0.75, 0.75, (n, 69)).astype(np.float32)
+            eng.dof_targets.copy_(cu((off + sc * a).astype(np.float32)))
+            eng.simulate(2)
+            v = np.maximum(v, torch.linalg.norm(eng.root_states[:, 7:10], dim=1).cpu().numpy())
+        vmax[pred] = v
+        del eng
+    print(f"envs over 20 m/s: without {int((vmax[0] > 20).sum())}/{n}, with {int((vmax[1] > 20).sum())}/{n}")
+    assert np.isfinite(vmax[1]).all() and vmax[1].max() < 20.0, vmax[1].max()
