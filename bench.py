@@ -243,6 +243,25 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
                                   "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x steps"}}
 
 
+def predictor_leg(args, model, device_index, steps=50, warmup=10):
+    """The bench workload with he_sim_params.bias_predictor on (the velocity-dependent
+    bias again at the free velocity, one more solve; off by default), timed the same way."""
+    import torch
+    a = argparse.Namespace(**vars(args))
+    a.bias_predictor = True
+    ro = Rollout(a, model, device_index, 0)
+    for _ in range(warmup):
+        ro.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ro.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": round(a.num_envs * steps / dt, 1), "unit": "env-steps/s", "steps": steps,
+            "workload": "the bench workload with he_sim_params.bias_predictor = 1"}
+
+
 def cpu_model_name():
     try:
         for line in open("/proc/cpuinfo"):
@@ -447,6 +466,11 @@ def main():
                                      "unit": "GB/s", "frac": round(imit_gbs / HBM_PEAK_GBS, 5),
                                      "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic}},
         }
+        if not args.no_tracking and world == 1 and not getattr(args, "bias_predictor", False):
+            try:
+                line["bias_predictor_on"] = predictor_leg(args, model, local)
+            except Exception as exc:  # report, never fake
+                line["bias_predictor_on"] = {"value": None, "error": repr(exc)}
         if not args.no_tracking and world == 1 and args.num_envs == 4096:
             try:
                 line["tracking_configs2"] = tracking_leg(args, model, local)
