@@ -673,3 +673,24 @@ def test_bias_predictor_keeps_standing_bodies_grounded_on_gpu(he_model, model):
         del eng
     print(f"envs over 20 m/s: without {int((vmax[0] > 20).sum())}/{n}, with {int((vmax[1] > 20).sum())}/{n}")
     assert np.isfinite(vmax[1]).all() and vmax[1].max() < 20.0, vmax[1].max()
+
+
+def test_bias_predictor_contact_rich_and_terrain_match_oracle(he_model, model):
+    """The predictor under contact: near-ground tumbling and lying bodies (one step), and the
+    config-5 mass / friction / terrain randomisation (3 steps), against the oracle with it on, under
+    the same bars as the tests without it."""
+    rng = np.random.default_rng(23)
+    root, dof = cases.random_state(64, rng, height=(0.85, 1.0), ang=0.8, vel=0.5)
+    r2, d2 = cases.lying_state(32, rng)
+    root = np.concatenate([root, r2])
+    dof = np.concatenate([dof, d2])
+    targets = rng.uniform(-0.5, 0.5, (96, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, bias_predictor=1)
+    n = 48
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
+    root[:, 2] += 0.1
+    ms = rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32)
+    fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
+    tk = (np.arange(n) % 3).astype(np.int32)
+    _physics_compare(he_model, root, dof, np.zeros((n, 69), np.float32), steps=3, env_props=(ms, fr, tk),
+                     max_widened=0.08, bias_predictor=1)
