@@ -24,12 +24,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-EV_EVERY = 10                  # timed steps between sampled kernel-duration event triples
+EV_STEPS = 60                  # kernel-duration pass after the timed region: events on every step
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak (spec)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 # SURVEY.md §8(d) canonical algorithmic counts per env-step
-PHYS_FLOP_PER_ENV_STEP = 1_309_278          # dense-equivalent physics, 2 substeps, n_c = 8
-FUSED_FLOP_PER_ENV_STEP = PHYS_FLOP_PER_ENV_STEP + 30_000  # + the imitation step (≈0.03 MFLOP)
+PHYS_FLOP_PER_SUBSTEP = 654_639            # dense-equivalent physics per physics step, n_c = 8
+# SURVEY's 1,309,278 FLOP/env-step counts 2 physics steps; the engine runs gym.simulate() x 2 with
+# SimParams.substeps = 2 (Isaac Gym's default), i.e. 4 physics steps of 1/120 s per env-step
+IMIT_FLOP_PER_ENV_STEP = 30_000             # the imitation step (≈0.03 MFLOP)
 IMIT_BYTES_PER_ENV_STEP = 13_200            # fused imitation kernel share of the 16.0 KB/env-step
 
 
@@ -46,8 +48,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=20)
-    ap.add_argument("--bias-predictor", action="store_true",
-                    help="he_sim_params.bias_predictor on (off by default, as the reference's explicit bias)")
+    ap.add_argument("--scheme", choices=["default", "r02"], default="default",
+                    help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 4 sweeps, "
+                         "link world angular-velocity clamp; r02 = round 2's energy-unstable scheme (2 x 1/60 s, "
+                         "explicit bias, 8 sweeps), for the cost comparison only (DESIGN §5)")
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
@@ -133,7 +137,7 @@ class Rollout:
         n = args.num_envs
         tables, actions, rng = build_workload(args, model, rank)
         sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0,
-                                      bias_predictor=int(getattr(args, "bias_predictor", False)))
+                                      **scheme_params(args))
         self.eng = Engine(model, n, device=device_index, sim_params=sim, start_xy=rng.uniform(-1, 1, (n, 2)))
         dev = self.eng.device
         self.eng.load_motions(tables)
@@ -243,12 +247,25 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
                                   "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x steps"}}
 
 
-def predictor_leg(args, model, device_index, steps=50, warmup=10):
-    """The bench workload with he_sim_params.bias_predictor on (the velocity-dependent
-    bias again at the free velocity, one more solve; off by default), timed the same way."""
+def sim_substeps(args):
+    """Physics steps per gym.simulate() of the run's scheme (he_sim_params.substeps)."""
+    from humanoid_amd import _abi
+    return int(scheme_params(args).get("substeps", _abi.default_sim_params().substeps))
+
+
+def scheme_params(args):
+    """he_sim_params overrides of the --scheme."""
+    if getattr(args, "scheme", "default") == "r02":
+        return dict(substeps=1, bias_midpoint=0, solver_iterations=8, max_angular_velocity=1e9)
+    return {}
+
+
+def scheme_leg(args, model, device_index, scheme="r02", steps=50, warmup=10):
+    """The bench workload under another physics scheme, timed the same way: the cost of the
+    energy-stable default against round 2's scheme (2 x 1/60 s, explicit bias, 8 sweeps)."""
     import torch
     a = argparse.Namespace(**vars(args))
-    a.bias_predictor = True
+    a.scheme = scheme
     ro = Rollout(a, model, device_index, 0)
     for _ in range(warmup):
         ro.step()
@@ -259,7 +276,7 @@ def predictor_leg(args, model, device_index, steps=50, warmup=10):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"value": round(a.num_envs * steps / dt, 1), "unit": "env-steps/s", "steps": steps,
-            "workload": "the bench workload with he_sim_params.bias_predictor = 1"}
+            "workload": f"the bench workload under --scheme {scheme}: " + str(scheme_params(a))}
 
 
 def cpu_model_name():
@@ -270,6 +287,22 @@ def cpu_model_name():
     except OSError:
         pass
     return None
+
+
+def host_cores():
+    """The CPU cores this process may use: its affinity mask (os.sched_getaffinity) capped by the
+    cgroup CPU quota (cpu.max, cgroup v2), which is how a shared GPU host grants its share; the
+    CPU baseline runs one OpenMP thread per granted core."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    return {"affinity": aff, "cgroup_quota": quota, "granted": min(aff, quota) if quota else aff}
 
 
 def cpu_baseline(args, model):
@@ -284,7 +317,7 @@ def cpu_baseline(args, model):
     n = a.num_envs
     hm = _abi.make_model(model)
     sim = _abi.default_sim_params(max_contacts=args.max_contacts, terrain=1 if args.config == "dr" else 0,
-                                      bias_predictor=int(getattr(args, "bias_predictor", False)))
+                                  **scheme_params(args))
     mt = O.MotionTables.from_tables(tables)
     p = _abi.imitation_params()
     off, sc = pd_action_offset_scale(model)
@@ -304,6 +337,8 @@ def cpu_baseline(args, model):
         fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
         tk = (np.arange(n) % 3).astype(np.int32)
     cache = O.new_cache(n)  # the engine's warm start
+    cores = host_cores()
+    threads = O.set_threads(cores["granted"])
     t0 = time.perf_counter()
     for step in range(a.cpu_steps):
         out = O.physics_step(hm, sim, st["root_states"], st["dof_state"], tgt, 2, mass_scale=ms, friction=fr,
@@ -318,9 +353,8 @@ def cpu_baseline(args, model):
             ph = np.array([O.hash_uniform(0, step, int(e)) for e in ids], np.float32)
             O.reset_envs(p, mt, ids, ph, np.arange(n), st)
     dt = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": n * a.cpu_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model_name(), "nproc": os.cpu_count(),
+            "cpu_model": cpu_model_name(), "nproc": os.cpu_count(), "host_cores": cores,
             "sample": f"{n} envs x {a.cpu_steps} policy steps of the C oracle (fp64 physics + imitation + resets), "
                       f"OpenMP over envs ({threads} threads), {dt:.1f} s"}
 
@@ -356,33 +390,37 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    # kernel durations: HIP events around the two launches of every EV_EVERY-th timed step (an event
-    # pair costs ~3 us of stream time per step, 3.7% of the step if recorded on every step)
-    sampled = list(range(0, args.steps, EV_EVERY))
-    evs = {k: tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for k in sampled}
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ro.step(evs.get(k))
+        ro.step()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     nc = ro.eng.num_contacts.cpu().numpy()
     dropped = ro.eng.dropped_contacts.cpu().numpy()
-    step_ms = float(np.mean([e[0].elapsed_time(e[2]) for e in evs.values()]))
-    phys_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs.values()]))
-    imit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs.values()]))
-    # the two kernels apart (unfused form, a short sampled pass after the timed region), for the
-    # physics kernel's own roofline and the imitation kernel's HBM share
+    # kernel durations: a pass of EV_STEPS further steps (untimed, the same workload continuing) with
+    # HIP events around the launches of EVERY step, on the engine's stream (torch's current stream);
+    # the medians are the per-launch figures (compare the rocprofv3 averages of the same command)
+    def kernel_pass(steps):
+        ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(steps)]
+        for e in ev:
+            ro.step(e)
+        torch.cuda.synchronize()
+        return (np.array([e[0].elapsed_time(e[1]) for e in ev]), np.array([e[1].elapsed_time(e[2]) for e in ev]),
+                np.array([e[0].elapsed_time(e[2]) for e in ev]))
+    first, second, whole = kernel_pass(EV_STEPS)
+    step_ms = float(np.median(whole))
+    phys_ms, imit_ms = float(np.median(first)), float(np.median(second))
+    kernel_samples = {"steps": EV_STEPS, "statistic": "median", "first_launch_ms": {
+        "median": round(phys_ms, 5), "mean": round(float(first.mean()), 5), "max": round(float(first.max()), 5)}}
+    # the two kernels apart (unfused form), for the physics kernel's own roofline and the imitation
+    # kernel's HBM share
     split = None
     if ro.fused:
         ro.set_fused(False)
-        sev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(10)]
-        for k in range(20):
-            ro.step(sev[k // 2] if k % 2 else None)
-        torch.cuda.synchronize()
-        split = (float(np.mean([e[0].elapsed_time(e[1]) for e in sev])),
-                 float(np.mean([e[1].elapsed_time(e[2]) for e in sev])))
+        a1, a2, _ = kernel_pass(EV_STEPS // 2)
+        split = (float(np.median(a1)), float(np.median(a2)))
         ro.set_fused(True)
     if world > 1:
         t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
@@ -395,7 +433,8 @@ def main():
         if split is not None:  # fused: the one launch is the dominant kernel
             fused_ms = step_ms
             phys_ms, imit_ms = split
-        phys_tflops = PHYS_FLOP_PER_ENV_STEP * n / (phys_ms * 1e-3) / 1e12
+        phys_flop = PHYS_FLOP_PER_SUBSTEP * 2 * sim_substeps(args)  # per env-step: 2 simulate() x substeps
+        phys_tflops = phys_flop * n / (phys_ms * 1e-3) / 1e12
         imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
         traffic = imit_traffic = mfma = None
         mfile = os.path.join(ROOT, "profiles", "pmc_mfma.json")  # rocprofv3 SQ counters of the bench
@@ -423,14 +462,15 @@ def main():
         # measured matrix-core busy share (rocprofv3 SQ counters)
         phys_roof = {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                     "kernel": "physics_kernel (fp32 VALU + MFMA; canonical 1.309 MFLOP/env-step, SURVEY §8d)",
+                     "kernel": f"physics_kernel (fp32 VALU + MFMA; SURVEY §8d canonical 0.6546 MFLOP per physics step "
+                               f"x {2 * sim_substeps(args)} physics steps per env-step)",
                      "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma}
         if split is not None:  # the fused launch (physics + the imitation epilogue) is the dominant kernel
-            f_tflops = FUSED_FLOP_PER_ENV_STEP * n / (fused_ms * 1e-3) / 1e12
+            f_tflops = (phys_flop + IMIT_FLOP_PER_ENV_STEP) * n / (fused_ms * 1e-3) / 1e12
             roof = {"bound": "latency", "achieved": round(f_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(f_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
                     "kernel": "physics_kernel, fused he_env_step (physics + imitation epilogue; canonical "
-                              "1.309 + 0.03 MFLOP/env-step, SURVEY §8d)",
+                              "physics + 0.03 MFLOP/env-step, SURVEY §8d)",
                     "avg_launch_ms": round(fused_ms, 4), "mfma_util": mfma}
         else:
             roof = phys_roof
@@ -450,13 +490,15 @@ def main():
             "config": {"workload": {"standstill": "configs[1]: 4096 SMPL-neutral humanoids, PD stand-still, zero ref motion",
                                     "imitation": "configs[2]: 4096 humanoids over 128 synthetic clips, full PHC reward",
                                     "dr": "configs[4]: 4096 envs, mass/friction randomisation + 3 terrains"}[args.config],
-                       "num_envs_per_gpu": n, "substeps": 2, "sim_dt": 1 / 60, "max_contacts": args.max_contacts,
-                       "bias_predictor": int(args.bias_predictor), "parallelism": f"replicas{world}"},
+                       "num_envs_per_gpu": n, "simulate_calls": 2, "substeps_per_simulate": int(sim_substeps(args)),
+                       "sim_dt": 1 / 60, "max_contacts": args.max_contacts,
+                       "scheme": args.scheme, "parallelism": f"replicas{world}"},
             # the physics kernel is bound by the latency of its per-env serial chains (elimination,
             # Gauss-Seidel sweeps, triangular solves) at 2 waves / SIMD, not by HBM or the matrix
             # cores: priced against the FP32 vector / matrix peak with the canonical dense-equivalent
             # flop count; mfma_util is the measured matrix-core busy share (rocprofv3 SQ counters)
             "roofline": roof,
+            "kernel_timing": kernel_samples,
             "contacts": {"slots_mean": round(float(nc.mean()), 3), "slots_max": int(nc.max()),
                          "capacity": args.max_contacts, "envs_dropping": int((dropped > 0).sum()),
                          "dropped_mean": round(float(dropped.mean()), 4)},
@@ -466,11 +508,11 @@ def main():
                                      "unit": "GB/s", "frac": round(imit_gbs / HBM_PEAK_GBS, 5),
                                      "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic}},
         }
-        if not args.no_tracking and world == 1 and not getattr(args, "bias_predictor", False):
+        if not args.no_tracking and world == 1 and args.scheme == "default":
             try:
-                line["bias_predictor_on"] = predictor_leg(args, model, local)
+                line["r02_scheme"] = scheme_leg(args, model, local)
             except Exception as exc:  # report, never fake
-                line["bias_predictor_on"] = {"value": None, "error": repr(exc)}
+                line["r02_scheme"] = {"value": None, "error": repr(exc)}
         if not args.no_tracking and world == 1 and args.num_envs == 4096:
             try:
                 line["tracking_configs2"] = tracking_leg(args, model, local)

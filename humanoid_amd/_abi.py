@@ -39,7 +39,7 @@ class HeSimParams(C.Structure):
         ("max_contacts", C.c_int32), ("kp_scale", C.c_float), ("kd_scale", C.c_float), ("terrain", C.c_int32),
         ("terrain_slope", C.c_float), ("step_height", C.c_float), ("step_length", C.c_float),
         ("joint_limits", C.c_int32), ("limit_margin", C.c_float), ("warm_start", C.c_int32), ("solver_tolerance", C.c_float),
-        ("bias_predictor", C.c_int32),
+        ("bias_midpoint", C.c_int32), ("substeps", C.c_int32), ("max_joint_velocity", C.c_float),
     ]
 
 
@@ -102,7 +102,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.max_depenetration_velocity = 10.0
     p.angular_damping = 0.01
     p.max_angular_velocity = 100.0
-    p.solver_iterations = 8
+    p.solver_iterations = 4  # physx.num_position_iterations (isaacgym_env.py:17)
     p.self_collision = 1
     p.max_contacts = 20
     p.kp_scale = 1.0
@@ -115,7 +115,9 @@ def default_sim_params(**kw) -> HeSimParams:
     p.limit_margin = 0.1
     p.warm_start = 1
     p.solver_tolerance = 0.0
-    p.bias_predictor = 0
+    p.bias_midpoint = 1  # explicit bias pumps energy under per-step random targets
+    p.substeps = 2  # gymapi.SimParams.substeps default (not set by isaacgym_env.py:6-35)
+    p.max_joint_velocity = 100.0  # PhysX articulation joint maxJointVelocity default
     for k, v in kw.items():
         setattr(p, k, v)
     return p

@@ -105,6 +105,9 @@ int he_create(const he_sim_params* params, int device, he_engine** out) {
     if (params->max_contacts < 1 || params->max_contacts > HE_MAX_CONTACTS)
         return fail("he_create: max_contacts must be in [1, %d]", HE_MAX_CONTACTS);
     if (params->dt <= 0.f) return fail("he_create: dt must be positive");
+    if (params->substeps < 1 || params->substeps > 16) return fail("he_create: substeps must be in [1, 16]");
+    if (!(params->max_joint_velocity > 0.f) || !(params->max_angular_velocity > 0.f))
+        return fail("he_create: max_joint_velocity and max_angular_velocity must be positive");
     he_engine* h = new he_engine();
     h->device = device;
     h->params = *params;
@@ -285,9 +288,11 @@ int he_set_pd_params(he_engine* h, const float* host_offset, const float* host_s
 }
 
 namespace {
-static PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
+// num_simulate gym.simulate() calls = num_simulate x SimParams.substeps physics steps of dt / substeps
+static PhysArgs phys_args(he_engine* h, int num_simulate, const float* actions) {
     PhysArgs a{};
     a.p = h->params;
+    a.p.dt = h->params.dt / (float)h->params.substeps;
     a.model = h->d_model;
     a.topo = h->d_topo;
     a.root_states = h->root;
@@ -308,28 +313,28 @@ static PhysArgs phys_args(he_engine* h, int substeps, const float* actions) {
     a.friction = h->friction;
     a.terrain_kind = h->terrain_kind;
     a.num_envs = h->num_envs;
-    a.substeps = substeps;
+    a.substeps = num_simulate * h->params.substeps;
     a.stamps = h->stamps;
     return a;
 }
 }  // namespace
 
-int he_simulate(he_engine* h, int substeps, void* stream) {
+int he_simulate(he_engine* h, int num_simulate, void* stream) {
     if (!h || !h->num_envs) return fail("he_simulate: no envs");
     if (h->params.joint_limits && h->component_limits)
         return fail("he_simulate: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
-    if (substeps < 1) return fail("he_simulate: substeps must be >= 1");
-    HE_CHECK(launch_physics(phys_args(h, substeps, nullptr), (hipStream_t)stream));
+    if (num_simulate < 1) return fail("he_simulate: num_simulate must be >= 1");
+    HE_CHECK(launch_physics(phys_args(h, num_simulate, nullptr), (hipStream_t)stream));
     return 0;
 }
 
-int he_step_actions(he_engine* h, const float* actions, int substeps, void* stream) {
+int he_step_actions(he_engine* h, const float* actions, int num_simulate, void* stream) {
     if (!h || !h->num_envs || !actions) return fail("he_step_actions: bad arguments");
     if (!h->has_pd) return fail("he_step_actions: call he_set_pd_params first");
     if (h->params.joint_limits && h->component_limits)
         return fail("he_step_actions: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
-    if (substeps < 1) return fail("he_step_actions: substeps must be >= 1");
-    HE_CHECK(launch_physics(phys_args(h, substeps, actions), (hipStream_t)stream));
+    if (num_simulate < 1) return fail("he_step_actions: num_simulate must be >= 1");
+    HE_CHECK(launch_physics(phys_args(h, num_simulate, actions), (hipStream_t)stream));
     return 0;
 }
 
@@ -554,7 +559,7 @@ int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motio
 }
 
 int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em, const float* actions,
-                int substeps, uint64_t seed, uint64_t step_index, float* obs, float* rew, float* reward_raw,
+                int num_simulate, uint64_t seed, uint64_t step_index, float* obs, float* rew, float* reward_raw,
                 uint8_t* reset, uint8_t* terminate, void* stream) {
     if (!h || !h->num_envs || !actions) return fail("he_env_step: bad arguments");
     // auto: one launch while the envs fit one round of waves on the chip (2 per SIMD: launch and
@@ -563,13 +568,13 @@ int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion*
     // 4096 envs: 0.218 against 0.209 ms per step)
     const bool fused = h->fused_step == 1 || (h->fused_step < 0 && h->num_envs <= 2048);
     if (h->has_eval || !fused) {  // eval recording lives in the stand-alone imitation kernel
-        if (he_step_actions(h, actions, substeps, stream)) return 1;
+        if (he_step_actions(h, actions, num_simulate, stream)) return 1;
         return he_imitation_reset_step(h, p, em, seed, step_index, obs, rew, reward_raw, reset, terminate, stream);
     }
     // one launch: actions -> PD targets -> physics -> the imitation step with the device reset of
     // flagged envs in the physics kernel's epilogue (the same results as the two launches)
     if (!h->has_pd) return fail("he_env_step: call he_set_pd_params first");
-    if (substeps < 1) return fail("he_env_step: substeps must be >= 1");
+    if (num_simulate < 1) return fail("he_env_step: num_simulate must be >= 1");
     if (h->params.joint_limits && h->component_limits)
         return fail("he_env_step: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
     ImitArgs a;
@@ -580,7 +585,7 @@ int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion*
     a.mode = 1;
     a.seed = seed;
     a.step = step_index;
-    PhysArgs pa = phys_args(h, substeps, actions);
+    PhysArgs pa = phys_args(h, num_simulate, actions);
     pa.fused = 1;
     pa.im = a;
     HE_CHECK(launch_physics(pa, (hipStream_t)stream));

@@ -314,7 +314,7 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
         bool fallen = false;
         if (p.enable_early_termination) {
             bool inset = act && ((p.reset_body_mask >> b) & 1);
-            float dist = norm3(s.pos - r.pos);
+            float dist = norm3_im(s.pos - r.pos);  // no contraction in either TU (torch rounding)
             if (p.eval_mode) {
                 float sum = group_sum(inset ? dist : 0.0f);
                 float cnt = group_sum(inset ? 1.0f : 0.0f);

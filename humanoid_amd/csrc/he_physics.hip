@@ -100,10 +100,10 @@ struct Lds {
 #ifndef HE_ONE_SWEEP
 #define HE_ONE_SWEEP 1
 #endif
-#ifndef HE_PRED_LEVELS  // the predictor's subtree sums by body levels (1) or per dof lane (0)
+#ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
 #define HE_PRED_LEVELS 0
 #endif
-#ifndef HE_BIAS_PREDICTOR  // 0: the predictor compiled out (diagnostic A/B of its code's cost when off)
+#ifndef HE_BIAS_PREDICTOR  // 0: the midpoint bias compiled out (diagnostic A/B of its code's cost when off)
 #define HE_BIAS_PREDICTOR 1
 #endif
 #ifndef HE_FAC_PIPE
@@ -1178,13 +1178,14 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
     }
 }
 
-// ---------------------------------------------------------------------------------- bias predictor
-// he_sim_params.bias_predictor (oracle/he_oracle_physics.c: substep, bias_at): the velocity-dependent
-// bias (Coriolis, gyroscopic; gravity cancels) again at the free velocity uf, and the free velocity
-// corrected through the same factor: yh += D^-1/2 L^-T dt (bias(u0) - bias(uf)). Runs between the
-// factorisation and the contact phase, with the factor in Lp and the first bias's subtree forces
-// in F. Scratch: uf, V (the final kinematics rewrites it), Acc (the contact phase's scratch after),
-// Ib (own inertias, stored by the force pass).
+// ---------------------------------------------------------------------------------- midpoint bias
+// he_sim_params.bias_midpoint (oracle/he_oracle_physics.c: substep, bias_at): the velocity-dependent
+// bias (Coriolis, gyroscopic; gravity cancels) again at the midpoint velocity um = (u0 + uf) / 2 of
+// the explicit step, and the free velocity corrected through the same factor:
+// yh += D^-1/2 L^-T dt (bias(u0) - bias(um)). Runs between the factorisation and the contact phase,
+// with the factor in Lp and the first bias's subtree forces in F. Scratch: uf (holds um), V (the
+// final kinematics rewrites it), Acc (the contact phase's scratch after), Ib (own inertias, stored
+// by the force pass).
 #ifndef HE_PRED_NOINLINE  // diagnostic: the predictor as a called function (its own register allocation)
 #define HE_PRED_NOINLINE 0
 #endif
@@ -1193,19 +1194,19 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 #else
 #define HE_PRED_FN HE_DEV
 #endif
-HE_PRED_FN void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, unsigned long long* stamps,
+HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, unsigned long long* stamps,
                                unsigned long long& t_prev) {
     (void)stamps; (void)t_prev;
     using namespace regla;
     const float dt = p.dt;
-    {  // uf = u0 + L^-1 D^-1/2 yh
+    {  // um = u0 + (L^-1 D^-1/2 yh) / 2, the midpoint of u0 and the explicit free velocity
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
         load_rows(L, T, lane, r1, r2);
         float t1 = L.yh[lane] * L.sDinv[lane];
         float t2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
         solve_L(r1, r2, lane, t1, t2);
-        L.uf[lane] = L.u0[lane] + t1;
-        if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + t2;
+        L.uf[lane] = L.u0[lane] + 0.5f * t1;
+        if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + 0.5f * t2;
     }
     sync();
     STAMP(25);
@@ -1233,7 +1234,7 @@ HE_PRED_FN void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim
     }
     sync();
     float Fb[6];
-    if (bl) {  // RNEA body force at uf: a_b = a_0 + sum over the chain (root excluded) of V_a x S_a uf_a
+    if (bl) {  // RNEA body force at um: a_b = a_0 + sum over the chain (root excluded) of V_a x S_a uf_a
         const f3 vxw = cross3(f3{L.uf[3], L.uf[4], L.uf[5]}, f3{L.uf[0], L.uf[1], L.uf[2]});
         float A[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
         for (int k = 1; k <= T.depth[b]; ++k) {
@@ -1261,7 +1262,7 @@ HE_PRED_FN void bias_predictor(Lds& L, const BodyTopo& T, int lane, const he_sim
         return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], L.Acc[bi]));
     };
 #else
-    // lane = dof (then dofs 64..74 on lanes 0..10): dc_i = dt (S_i . F_b(u0) - S_i . F_b(uf)) with the
+    // lane = dof (then dofs 64..74 on lanes 0..10): dc_i = dt (S_i . F_b(u0) - S_i . F_b(um)) with the
     // subtree sums of the new body forces (the level-parallel sums measured 2 VGPRs over the
     // kernel's 2-waves budget)
     auto corr = [&](int i) {
@@ -1367,7 +1368,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float* o10 = L.Ic[b];  // own inertia; the subtree sums accumulate in place
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
-        if (HE_BIAS_PREDICTOR && p.bias_predictor)  // the body's own inertia for the predictor's second RNEA (Ib is free until
+        if (HE_BIAS_PREDICTOR && p.bias_midpoint)  // the body's own inertia for the midpoint's second RNEA (Ib is free until
             for (int x = 0; x < 10; ++x) L.Ib[b][x] = o10[x];  // the contact phase's segments)
         float IA[6], IV[6], X[6];
         si_apply(o10, L.Acc[b], IA);
@@ -1493,9 +1494,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     sync();
     STAMP(5);
 #if HE_ONE_SWEEP
-    if (HE_BIAS_PREDICTOR && p.bias_predictor) bias_predictor(L, T, lane, p, stamps, t_prev);
+    if (HE_BIAS_PREDICTOR && p.bias_midpoint) bias_midpoint(L, T, lane, p, stamps, t_prev);
 #else
-#error "the bias predictor is implemented on the one-sweep path (HE_ONE_SWEEP=1)"
+#error "the midpoint bias is implemented on the one-sweep path (HE_ONE_SWEEP=1)"
 #endif
     // the contact phase's model reads (geometry of the lane's body, self-collision pair indices)
     // depend on nothing computed here: issued now, they land behind the free-velocity sweep
@@ -2013,7 +2014,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // the solve's impulses and keys: the next solve's warm start and the reported forces
         L.lam[lane] = lane < nr ? lamv : 0.f;
         if (lane < nc) L.wckey[lane] = L.ckey[lane];
-        if (lane == 0) L.nwc = nc;
+        if (lane == 0) L.nwc = p.warm_start ? nc : 0;  // warm_start 0: every substep's solve is cold
         sync();
         STAMP(10);
         // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
@@ -2104,19 +2105,50 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
         sync();
     }
-    // damping, the angular-velocity clamp and the semi-implicit position update in one pass per
+    // damping, the angular-velocity clamps and the semi-implicit position update in one pass per
     // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
     // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
     f3 lim_th = f3{0.f, 0.f, 0.f}, lim_u = f3{0.f, 0.f, 0.f};  // the joint's new q and u
-    if (lane < NB) {
-        const bool root = lane == 0;
-        const int d0 = root ? 0 : 6 + 3 * (lane - 1);
-        float w[3] = {L.uf[d0] * damp, L.uf[d0 + 1] * damp, L.uf[d0 + 2] * damp};
-        float nrm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        if (nrm > p.max_angular_velocity) {
-            float s = p.max_angular_velocity / nrm;
+    const bool bl = lane < NB;
+    const bool root = lane == 0;
+    const int d0 = root ? 0 : 6 + 3 * ((bl ? lane : 1) - 1);
+    float w[3] = {L.uf[d0] * damp, L.uf[d0 + 1] * damp, L.uf[d0 + 2] * damp};
+    {
+        // the joint's relative rate: PhysX articulation joint maxJointVelocity
+        const float nrm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        if (!root && nrm > p.max_joint_velocity) {
+            const float s = p.max_joint_velocity / nrm;
             w[0] *= s; w[1] *= s; w[2] *= s;
         }
+        // the link's WORLD angular velocity (asset max_angular_velocity, PxRigidBody): w_b = w_parent +
+        // R_b u_b summed along the chain (Acc is scratch here), clamped link by link; the joint rates
+        // are then re-derived, u_b = R_b^T (w'_b - w'_parent) (oracle: the same pass)
+        const f4 qb = bl ? f4{L.qw[lane][0], L.qw[lane][1], L.qw[lane][2], L.qw[lane][3]} : f4{0.f, 0.f, 0.f, 1.f};
+        const f3 wr = root ? f3{w[0], w[1], w[2]} : qapply(qb, f3{w[0], w[1], w[2]});
+        if (bl) { L.Acc[lane][0] = wr.x; L.Acc[lane][1] = wr.y; L.Acc[lane][2] = wr.z; }
+        sync();
+        f3 wo = f3{0.f, 0.f, 0.f};
+        if (bl)
+            for (int k = 0; k <= T.depth[lane]; ++k) {
+                const int a = T.chain[lane][k];
+                wo = wo + f3{L.Acc[a][0], L.Acc[a][1], L.Acc[a][2]};
+            }
+        const float wmax = p.max_angular_velocity;
+        const float wn2 = dot3(wo, wo);
+        const bool over = bl && wn2 > wmax * wmax;
+        if (__ballot(over) != 0ull) {  // rare (wave-uniform branch)
+            const f3 wc = over ? wo * (wmax * __builtin_amdgcn_rsqf(wn2)) : wo;
+            if (bl) { L.Acc[lane][3] = wc.x; L.Acc[lane][4] = wc.y; L.Acc[lane][5] = wc.z; }
+            sync();
+            if (bl) {
+                const int pb = root ? 0 : T.chain[lane][T.depth[lane] - 1];
+                const f3 rel = root ? wc : wc - f3{L.Acc[pb][3], L.Acc[pb][4], L.Acc[pb][5]};
+                const f3 ub = root ? rel : qapply(qconj(qb), rel);
+                w[0] = ub.x; w[1] = ub.y; w[2] = ub.z;
+            }
+        }
+    }
+    if (bl) {
         L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
         const int d = root ? 0 : 3 * (lane - 1);
         const f3 dtw = f3{dt * w[0], dt * w[1], dt * w[2]};

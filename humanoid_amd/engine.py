@@ -253,8 +253,9 @@ class Engine:
                                               vp(terrain_kind, torch.int32)))
 
     # ------------------------------------------------------------------ stepping
-    def simulate(self, substeps: int = 2):
-        _check(self.lib.he_simulate(self.h, int(substeps), self.stream))
+    def simulate(self, num_simulate: int = 2):
+        """gym.simulate() x num_simulate (control_freq_inv), each he_sim_params.substeps physics steps."""
+        _check(self.lib.he_simulate(self.h, int(num_simulate), self.stream))
 
     def set_pd_params(self, offset, scale, frozen_mask=None, clip_actions=True):
         off = np.ascontiguousarray(offset, np.float32)
@@ -263,10 +264,10 @@ class Engine:
         _check(self.lib.he_set_pd_params(self.h, off.ctypes.data_as(C.c_void_p), sc.ctypes.data_as(C.c_void_p),
                                          None if fz is None else fz.ctypes.data_as(C.c_void_p), int(bool(clip_actions))))
 
-    def step_actions(self, actions, substeps: int = 2):
+    def step_actions(self, actions, num_simulate: int = 2):
         import torch
         a = self._contig(actions, torch.float32)
-        _check(self.lib.he_step_actions(self.h, C.c_void_p(a.data_ptr()), int(substeps), self.stream))
+        _check(self.lib.he_step_actions(self.h, C.c_void_p(a.data_ptr()), int(num_simulate), self.stream))
 
     # ------------------------------------------------------------------ motion library
     def load_motions(self, tables):
@@ -356,17 +357,19 @@ class Engine:
                                       C.c_void_p(reset.data_ptr()), C.c_void_p(terminate.data_ptr()), self.stream))
 
     def env_step(self, params, em, actions, obs, rew, reward_raw, reset, terminate, seed: int, step_index: int,
-                 substeps: int = 2):
+                 num_simulate: int = 2):
         import torch
         a = self._contig(actions, torch.float32)
-        _check(self.lib.he_env_step(self.h, C.byref(params), C.byref(em), C.c_void_p(a.data_ptr()), int(substeps),
+        _check(self.lib.he_env_step(self.h, C.byref(params), C.byref(em), C.c_void_p(a.data_ptr()), int(num_simulate),
                                     C.c_uint64(seed), C.c_uint64(step_index), C.c_void_p(obs.data_ptr()),
                                     C.c_void_p(rew.data_ptr()), C.c_void_p(reward_raw.data_ptr()),
                                     C.c_void_p(reset.data_ptr()), C.c_void_p(terminate.data_ptr()), self.stream))
 
-    def set_fused_step(self, enable: bool):
-        """he_set_fused_step: env_step as one launch (default) or as step_actions + imitation_reset_step."""
-        _check(self.lib.he_set_fused_step(self.h, int(bool(enable))))
+    def set_fused_step(self, enable):
+        """he_set_fused_step: env_step as one launch (True / 1), as step_actions + imitation_reset_step
+        (False / 0), or None / -1 = auto (the engine default: one launch up to 2048 envs)."""
+        mode = -1 if enable is None or (not isinstance(enable, bool) and int(enable) < 0) else int(bool(enable))
+        _check(self.lib.he_set_fused_step(self.h, mode))
 
     def imitation_reset_step(self, params, em, obs, rew, reward_raw, reset, terminate, seed: int, step_index: int):
         _check(self.lib.he_imitation_reset_step(self.h, C.byref(params), C.byref(em), C.c_uint64(seed),

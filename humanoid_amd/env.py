@@ -234,14 +234,21 @@ class HumanoidPHC:
         """_sample_ref_state (humanoid_phc.py:848-855): motion time 0 for Start and in test mode."""
         return self.cfg.state_init == "Start" or self.flag_test
 
-    def _obs_noise(self):
-        """humanoid_phc.py:956: obs + N(0, obs_noise_std) while training (not in test mode)."""
+    def _obs_noise(self, env_ids=None):
+        """humanoid_phc.py:956-959: obs + N(0, obs_noise_std) while training (not in test mode), on the
+        rows just computed: every row after a step, only the reset rows after a partial reset
+        (obs_buf[env_ids] = obs)."""
         import torch
         if self.cfg.add_obs_noise and not self.flag_test:
             if not hasattr(self, "_noise_gen"):  # its own stream: the reset phases stay the same
                 self._noise_gen = torch.Generator(device=self.device).manual_seed(self.cfg.seed + 7919)
-            self.obs_buf.add_(torch.randn(self.obs_buf.shape, device=self.device, generator=self._noise_gen)
-                              * self.cfg.obs_noise_std)
+            if env_ids is None:
+                self.obs_buf.add_(torch.randn(self.obs_buf.shape, device=self.device, generator=self._noise_gen)
+                                  * self.cfg.obs_noise_std)
+            else:
+                ids = env_ids.to(device=self.device, dtype=torch.long)
+                self.obs_buf[ids] += torch.randn((len(ids), self.obs_buf.shape[1]), device=self.device,
+                                                 generator=self._noise_gen) * self.cfg.obs_noise_std
 
     def _update_params(self):
         r = dataclasses.asdict(self.cfg.reward)
@@ -284,7 +291,7 @@ class HumanoidPHC:
             phases = torch.rand(len(env_ids), device=self.device, generator=self._gen)
         self.engine.reset_envs(self._params, self._em, env_ids.to(torch.int32), phases, self.obs_buf,
                                self._reset_u8, self._term_u8)
-        self._obs_noise()
+        self._obs_noise(env_ids)
 
     def reset(self, env_ids=None):
         safe_reset = env_ids is None or len(env_ids) == self.cfg.num_envs

@@ -84,7 +84,7 @@ class PhysXParams:
 class SimParams:
     def __init__(self):
         self.dt = 1.0 / 60.0
-        self.substeps = 1
+        self.substeps = 2  # Isaac Gym's default; the reference leaves it (isaacgym_env.py:6-35)
         self.up_axis = UP_AXIS_Z
         self.gravity = Vec3(0.0, 0.0, -9.81)
         self.use_gpu_pipeline = True
@@ -308,7 +308,8 @@ class Gym:
         params = _abi.default_sim_params(
             dt=sp.dt, contact_offset=px.contact_offset, max_depenetration_velocity=px.max_depenetration_velocity,
             angular_damping=o.angular_damping, max_angular_velocity=o.max_angular_velocity,
-            friction=plane.static_friction, self_collision=int(bool(sim.self_collision)))
+            friction=plane.static_friction, self_collision=int(bool(sim.self_collision)), substeps=int(sp.substeps),
+            solver_iterations=int(px.num_position_iterations))
         params.gravity[:] = (sp.gravity.x, sp.gravity.y, sp.gravity.z)
         n = len(sim.envs)
         xy = np.array([p[0][:2] for p in sim.start_poses], np.float32)

@@ -80,9 +80,17 @@ typedef struct he_sim_params {
     int32_t warm_start;              /* 1: the solver starts from the previous solve's impulses */
     float solver_tolerance;          /* m/s: stop the sweeps once no row's velocity moves by more
                                         (|d lambda_r| A_rr) in a sweep; 0 = always solver_iterations */
-    int32_t bias_predictor;          /* 1: the velocity-dependent bias re-evaluated at the free
-                                        velocity, one more solve; off by default
-                                        (the reference's PhysX bias is explicit) */
+    int32_t bias_midpoint;           /* 1 (default): the velocity-dependent bias (Coriolis,
+                                        gyroscopic) evaluated at the midpoint velocity (u0 + uf) / 2
+                                        of the explicit step, one more solve through the same factor
+                                        (explicit at dt 1/120 pumps energy under
+                                        per-step random targets); 0: explicit, at u0 */
+    int32_t substeps;                /* gymapi.SimParams.substeps (Isaac Gym default 2; the reference
+                                        leaves it, isaacgym_env.py:6-35): each simulate() advances dt
+                                        in `substeps` physics steps of dt / substeps */
+    float max_joint_velocity;        /* rad/s, per joint relative rate (PhysX articulation joint
+                                        maxJointVelocity, default 100); max_angular_velocity above
+                                        clamps each link's WORLD angular velocity (PxRigidBody) */
 } he_sim_params;
 
 /* Per-env solver warm-start cache (f32 words; HE_BUF_CONTACT_CACHE), written at the end of every
@@ -168,15 +176,17 @@ int he_set_dof_targets_indexed(he_engine* h, const float* src, const int32_t* id
 int he_set_env_properties(he_engine* h, const float* mass_scale, const float* friction,
                           const int32_t* terrain_kind);
 
-/* gym.simulate x substeps + fetch_results (humanoid_phc.py:131-134): articulated rigid-body step
- * with implicit PD drives, ground + self contacts and a PGS contact solve; updates every state
- * buffer (root, dof, rigid-body, contact force, dof force). One kernel launch. */
-int he_simulate(he_engine* h, int substeps, void* stream);
+/* gym.simulate x num_simulate + fetch_results (humanoid_phc.py:131-134; num_simulate =
+ * control_freq_inv = 2 per policy step): articulated rigid-body step with implicit PD drives,
+ * ground + self contacts and a PGS contact solve, num_simulate x he_sim_params.substeps physics
+ * steps of dt / substeps; updates every state buffer (root, dof, rigid-body, contact force, dof
+ * force). One kernel launch. */
+int he_simulate(he_engine* h, int num_simulate, void* stream);
 /* action -> PD target (humanoid_phc.py:1218-1228, freeze hand/toe :116-125) fused into the step:
  * target = offset + scale*clip(a,-1,1) (frozen dofs 0), then he_simulate. */
 int he_set_pd_params(he_engine* h, const float* host_offset, const float* host_scale,
                      const int32_t* host_frozen_mask, int clip_actions);
-int he_step_actions(he_engine* h, const float* actions, int substeps, void* stream);
+int he_step_actions(he_engine* h, const float* actions, int num_simulate, void* stream);
 /* refresh_*_tensor (humanoid_phc.py:782-789): buffers are the live engine state, nothing to copy;
  * kept for API parity (no FK recompute: rigid-body rows written by the caller after a reset stay,
  * as the reference relies on, humanoid_phc.py:922-931). */
@@ -243,7 +253,7 @@ int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motio
  * physics -> reward/reset/obs -> device reset of flagged envs (phases from a counter-based hash
  * of (seed, step, env)) -> obs for reset envs. */
 int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion* em,
-                const float* actions, int substeps, uint64_t seed, uint64_t step_index,
+                const float* actions, int num_simulate, uint64_t seed, uint64_t step_index,
                 float* obs, float* rew, float* reward_raw, uint8_t* reset, uint8_t* terminate,
                 void* stream);
 

@@ -542,3 +542,9 @@ void ho_amp_obs(int n, int num_joints, const int32_t* joints, int num_key, const
         }
     }
 }
+
+/* OpenMP thread count of the oracle's parallel loops (bench.py cpu_baseline: the cores the host
+ * grants this process) */
+#include <omp.h>
+void ho_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
+int ho_get_threads(void) { return omp_get_max_threads(); }

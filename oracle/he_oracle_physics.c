@@ -573,8 +573,8 @@ typedef struct warm_cache {
 } warm_cache;
 
 /* one substep; updates s in place */
-/* Velocity-dependent + gravity bias at the velocities of state sv (the bias predictor,
- * he_sim_params.bias_predictor): the same RNEA as the substep's, with sv's body velocities. */
+/* Velocity-dependent + gravity bias at the velocities of state sv (the midpoint bias,
+ * he_sim_params.bias_midpoint): the same RNEA as the substep's, with sv's body velocities. */
 static void bias_at(const he_model* m, const topo* t, const he_sim_params* p, const env_state* sv, const kin* k,
                     const sinertia* I, R* bias) {
     static __thread kin kv;
@@ -722,13 +722,18 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     for (int c = 0; c < 3; ++c) { u0[c] = s->root_w[c]; u0[3 + c] = s->root_v[c]; }
     for (int d = 0; d < ND; ++d) u0[6 + d] = s->u[d];
     for (int i = 0; i < NG; ++i) uf[i] = u0[i] + du[i];
-    if (p->bias_predictor) {
-        /* The bias (Coriolis, gyroscopic) is explicit: taken at u0, it lets stiff drives on light
-         * links pump energy at dt = 1/60 (the runaway regime). Predictor: the bias
-         * again at the free velocity, and the free velocity corrected through the same factor. */
+    if (p->bias_midpoint) {
+        /* The velocity-dependent bias (Coriolis, gyroscopic) taken at u0 alone is explicit: at
+         * 1/120 s, stiff drives on light links under per-step random targets pump energy without
+         * bound. It is taken again at the midpoint velocity um = (u0 + uf) / 2 of the
+         * explicit step, and the free velocity corrected through the same factor:
+         * uf += H^-1 dt (bias(u0) - bias(um)). One fixed-point pass of the implicit midpoint rule
+         * (bias at (u0 + u+) / 2), which conserves the quadratic invariants of a free rigid body. */
         env_state sv = *s;
-        for (int c = 0; c < 3; ++c) { sv.root_w[c] = uf[c]; sv.root_v[c] = uf[3 + c]; }
-        for (int d = 0; d < ND; ++d) sv.u[d] = uf[6 + d];
+        R um[NG];
+        for (int i = 0; i < NG; ++i) um[i] = 0.5 * (u0[i] + uf[i]);
+        for (int c = 0; c < 3; ++c) { sv.root_w[c] = um[c]; sv.root_v[c] = um[3 + c]; }
+        for (int d = 0; d < ND; ++d) sv.u[d] = um[6 + d];
         R b2[NG], dc[NG];
         bias_at(m, t, p, &sv, &k, I, b2);
         for (int i = 0; i < NG; ++i) dc[i] = dt * (bias[i] - b2[i]);
@@ -873,11 +878,40 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     R damp = 1.0 / (1.0 + dt * p->angular_damping);
     for (int c = 0; c < 3; ++c) unew[c] *= damp;
     for (int d = 0; d < ND; ++d) unew[6 + d] *= damp;
-    R wmax = p->max_angular_velocity;
-    for (int b = 0; b < NB; ++b) {
-        R* w = b == 0 ? &unew[0] : &unew[6 + 3 * (b - 1)];
+    /* PhysX articulation joint maxJointVelocity (default 100 rad/s): each joint's relative rate */
+    const R jmax = p->max_joint_velocity;
+    for (int b = 1; b < NB; ++b) {
+        R* w = &unew[6 + 3 * (b - 1)];
         R nrm = sqrt(dot3(w, w));
-        if (nrm > wmax) { R sc = wmax / nrm; w[0] *= sc; w[1] *= sc; w[2] *= sc; }
+        if (nrm > jmax) { R sc = jmax / nrm; w[0] *= sc; w[1] *= sc; w[2] *= sc; }
+    }
+    /* max_angular_velocity (asset option, humanoid_phc.py:213; PxRigidBody maxAngularVelocity):
+     * each link's WORLD angular velocity w_b = w_parent + R_b u_b, clamped link by link; the
+     * joint rates are then re-derived from the clamped world rates, u_b = R_b^T (w'_b - w'_parent) */
+    {
+        const R wmax = p->max_angular_velocity;
+        R wo[NB][3], wc[NB][3];
+        int any = 0;
+        for (int c = 0; c < 3; ++c) wo[0][c] = unew[c];
+        for (int b = 1; b < NB; ++b) {
+            R r[3];
+            matvec(k.Rw[b], &unew[6 + 3 * (b - 1)], r);
+            for (int c = 0; c < 3; ++c) wo[b][c] = wo[m->parents[b]][c] + r[c];
+        }
+        for (int b = 0; b < NB; ++b) {
+            R nrm = sqrt(dot3(wo[b], wo[b])), sc = 1;
+            if (nrm > wmax) { sc = wmax / nrm; any = 1; }
+            for (int c = 0; c < 3; ++c) wc[b][c] = wo[b][c] * sc;
+        }
+        if (any) {
+            for (int c = 0; c < 3; ++c) unew[c] = wc[0][c];
+            for (int b = 1; b < NB; ++b) {
+                const R* wp = wc[m->parents[b]];
+                R rel[3] = {wc[b][0] - wp[0], wc[b][1] - wp[1], wc[b][2] - wp[2]};
+                R* u = &unew[6 + 3 * (b - 1)];
+                for (int c = 0; c < 3; ++c) u[c] = k.Rw[b][0][c] * rel[0] + k.Rw[b][1][c] * rel[1] + k.Rw[b][2][c] * rel[2];
+            }
+        }
     }
     /* write velocities + semi-implicit position update */
     for (int c = 0; c < 3; ++c) { s->root_w[c] = unew[c]; s->root_v[c] = unew[3 + c]; }
@@ -917,18 +951,24 @@ static void write_rb(const he_model* m, const topo* t, const env_state* s, float
     }
 }
 
-/* gym.simulate x substeps for n envs. root_states [N,13], dof_state [N,69,2] (in/out),
+/* gym.simulate x num_simulate for n envs: num_simulate x p->substeps physics steps of
+ * p->dt / p->substeps (gymapi.SimParams.substeps, Isaac Gym default 2). root_states [N,13], dof_state [N,69,2] (in/out),
  * targets [N,69]; outputs rb_state [N,24,13], contact_forces [N,24,3], dof_force [N,69],
  * num_contacts [N] (nullable). mass_scale [N,24], friction [N], terrain_kind [N] nullable.
  * cache [N,HE_CACHE_WORDS] (in/out, nullable: cold solves), dropped [N], residual [N] and
  * sweeps [N] (out, nullable): contacts past the capacity, the solve's residual and its sweep count,
  * all of the last substep. */
 void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* root_states, float* dof_state,
-                     const float* targets, int substeps, float* rb_state, float* contact_forces, float* dof_force,
+                     const float* targets, int num_simulate, float* rb_state, float* contact_forces, float* dof_force,
                      int32_t* num_contacts, const float* mass_scale, const float* friction, const int32_t* terrain_kind,
                      float* cache, int32_t* dropped, float* residual, int32_t* sweeps) {
     topo t;
     build_topo(m, &t);
+    he_sim_params ps = *p; /* the physics step's parameters: dt / substeps */
+    const int nsub = p->substeps > 0 ? p->substeps : 1;
+    ps.dt = p->dt / nsub;
+    const int substeps = num_simulate * nsub;
+    p = &ps;
 #pragma omp parallel for schedule(dynamic, 4)
     for (int e = 0; e < n; ++e) {
         env_state s;

@@ -39,6 +39,12 @@ def lib():
     return _lib
 
 
+def set_threads(n):
+    """OpenMP threads of the oracle's parallel loops; returns the count in effect."""
+    lib().ho_set_threads(int(n))
+    return int(lib().ho_get_threads())
+
+
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 

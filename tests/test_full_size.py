@@ -26,6 +26,14 @@ def _rollout(config, model):
     return bench.Rollout(args, model, 0, 0)
 
 
+def _props(ro, idx):
+    """configs[4]'s per-env mass scale, friction and terrain kind of the sampled envs (oracle kwargs)."""
+    if ro.args.config != "dr":
+        return {}
+    return dict(mass_scale=ro.ms.cpu().numpy()[idx].copy(), friction=ro.fr.cpu().numpy()[idx].copy(),
+                terrain_kind=ro.tk.cpu().numpy()[idx].copy())
+
+
 def _state(ro):
     return (ro.eng.root_states.clone(), ro.eng.dof_state.clone(), ro.obs.clone(), ro.rew.clone())
 
@@ -56,7 +64,7 @@ def test_full_size_standstill_invariant(model):
     assert (ro.eng.num_contacts == 16).all()  # 4 foot/toe boxes x 4 corners
 
 
-@pytest.mark.parametrize("config", ["standstill", "imitation"])
+@pytest.mark.parametrize("config", ["standstill", "imitation", "dr"])
 def test_full_size_sample_matches_oracle(model, he_model, config):
     import cases  # noqa: F401  (tests/ on the path)
     from humanoid_amd import _abi
@@ -73,15 +81,16 @@ def test_full_size_sample_matches_oracle(model, he_model, config):
     torch.cuda.synchronize()
     tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
     from test_gpu_parity import CondStats, _cond_close, contact_keys
-    sp = _abi.default_sim_params(max_contacts=20)
+    sp = _abi.default_sim_params(max_contacts=20, terrain=1 if config == "dr" else 0)
+    props = _props(ro, idx)
     probes = []
     for seed in (123, 124, 125):  # the oracle's own sensitivity (see _cond_close)
         r_s, d_s = root.copy(), dof.copy()
         d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
-        O.physics_step(he_model, sp, r_s, d_s, tgt, 2, cache=cache.copy())
+        O.physics_step(he_model, sp, r_s, d_s, tgt, 2, cache=cache.copy(), **props)
         probes.append((r_s, d_s))
     c_o = cache.copy()
-    out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o)
+    out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o, **props)
     kg = contact_keys(ro.eng.contact_cache.cpu().numpy()[idx])
     same = np.array([a == b for a, b in zip(kg, contact_keys(c_o))])
     assert same.mean() >= 0.95
@@ -93,3 +102,59 @@ def test_full_size_sample_matches_oracle(model, he_model, config):
     _cond_close("dof vel", dg[same, :, 1], dof[same, :, 1], [d[same, :, 1] for _, d in probes], 1e-2, 1e-3, stats=st)
     print(f"widened elements {st.widened}/{st.total}: {st.by_name}")
     assert st.frac <= 0.05
+
+
+def test_full_size_dr_sample_30_steps(model, he_model):
+    """configs[4] (4096 envs: mass / friction randomisation, plane / 10 deg slope / box steps) at full
+    size: after 5 bench steps, 30 more policy steps of physics (actions 0) on all 4096 envs, and the
+    oracle on a 48-env sample from the same state and warm-start cache (its own mass scale, friction
+    and terrain). Joint angles and CoM at 1e-4 every step; envs whose contact sets ever differ are
+    excluded (at most 5%); at most 1% of the compared elements need the sensitivity widening."""
+    import cases
+    from humanoid_amd import _abi
+    from test_gpu_parity import CondStats, _cond_close, contact_keys
+    ro = _rollout("dr", model)
+    for _ in range(5):
+        ro.step()
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(12)
+    idx = np.sort(rng.choice(4096, 48, replace=False))
+    root = ro.eng.root_states.cpu().numpy()[idx].copy()
+    dof = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy()
+    c_o = ro.eng.contact_cache.cpu().numpy()[idx].copy()
+    props = _props(ro, idx)
+    sp = _abi.default_sim_params(max_contacts=20, terrain=1)
+    probes = []
+    for seed in (123, 124, 125):
+        d_s = dof.copy()
+        d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
+        probes.append([root.copy(), d_s, c_o.copy(), None])
+    zero = torch.zeros_like(ro.actions)
+    mism = np.zeros(len(idx), bool)
+    st = CondStats()
+    hist = []
+    for step in range(30):
+        ro.eng.step_actions(zero, 2)
+        tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
+        out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o, **props)
+        for k, pr in enumerate(probes):
+            if step > 0:  # rounding-level noise in every step, as the fp32 engine rounds in every step
+                pr[1][:, :, 0] += (1e-6 * np.random.default_rng(1000 * k + step).standard_normal(
+                    pr[1][:, :, 0].shape)).astype(np.float32)
+            pr[3] = O.physics_step(he_model, sp, pr[0], pr[1], tgt, 2, cache=pr[2], **props)
+        torch.cuda.synchronize()
+        mism |= np.array([a != b for a, b in zip(contact_keys(ro.eng.contact_cache.cpu().numpy()[idx]),
+                                                 contact_keys(c_o))])
+        hist.append((ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy(),
+                     ro.eng.rb_state.view(4096, 24, 13).cpu().numpy()[idx].copy(), dof.copy(),
+                     out["rb_state"].copy(), [p[1].copy() for p in probes], [p[3]["rb_state"].copy() for p in probes]))
+    ok = ~mism
+    print(f"contact-set mismatch: {mism.sum()}/{len(idx)} envs")
+    assert mism.mean() <= 0.05
+    for dg, rbg, do, rbo, dps, rbps in hist:
+        _cond_close("dof pos", dg[ok, :, 0], do[ok, :, 0], [d[ok, :, 0] for d in dps], 1e-4, stats=st)
+        com = [cases.center_of_mass(model, r[ok]) for r in rbps]
+        _cond_close("CoM", cases.center_of_mass(model, rbg[ok]), cases.center_of_mass(model, rbo[ok]), com, 1e-4,
+                    stats=st)
+    print(f"widened elements {st.widened}/{st.total} ({100 * st.frac:.2f}%): {st.by_name}")
+    assert st.frac <= 0.01

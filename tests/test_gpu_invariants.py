@@ -51,12 +51,13 @@ def test_gpu_free_fall_is_the_discrete_parabola(he_model):
         eng.simulate(2)
     torch.cuda.synchronize()
     r = eng.root_states.cpu().numpy()
-    k = 2 * steps
-    dt = 1.0 / 60.0
+    sub = eng.params.substeps  # physics steps of dt / substeps per simulate() (SimParams.substeps)
+    k = 2 * steps * sub
+    dt = 1.0 / 60.0 / sub
     assert (eng.num_contacts.cpu().numpy() == 0).all()
     np.testing.assert_allclose(r[:, 2], root[:, 2] - G * dt * dt * k * (k + 1) / 2, atol=2e-5)
     np.testing.assert_allclose(r[:, 9], -G * dt * k, atol=2e-5)
-    # in float32 the gravity bias cancels to rounding only: 40 substeps accumulate <= ~1e-4 rad
+    # in float32 the gravity bias cancels to rounding only: 80 physics steps accumulate <= ~1e-4 rad
     np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0], dof[..., 0], atol=2e-4)
 
 

@@ -251,10 +251,12 @@ def _obs_tol(oo):
     return tol
 
 
-def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=1e-4, vel_tol=1e-2, max_skip=0.02,
+def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-4, vel_tol=1e-2, max_skip=0.02,
                      max_widened=0.05, env_props=None, **sim):
-    """Engine vs oracle for `steps` policy steps from the same state, both warm-starting from their
-    own caches. Envs whose contact SETS (keys: body, partner, candidate) ever differ are excluded
+    """Engine vs oracle for `steps` policy steps (`calls` gym.simulate() each) from the same state,
+    both warm-starting from their own caches. The oracle's sensitivity probes (_cond_close) carry
+    rounding-level noise into every policy step (1e-6 rad on the joint angles, fresh each step), as
+    the fp32 engine rounds in every step, not only at the start. Envs whose contact SETS (keys: body, partner, candidate) ever differ are excluded
     (a point within rounding of the 0.02 m offset, or a tie in the deepest-first reduction), at most
     `max_skip` of them; at most `max_widened` of the compared elements may need the sensitivity
     widening (_cond_close)."""
@@ -278,11 +280,14 @@ def _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, pos_tol=
         probes.append([r_s, d_s, None, O.new_cache(n)])
     sp = _abi.default_sim_params(**sim)
     mismatch = np.zeros(n, bool)
-    for _ in range(steps):
-        eng.simulate(substeps)
-        out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, substeps, cache=c_o, **props)
-        for pr in probes:
-            pr[2] = O.physics_step(eng.he_model, sp, pr[0], pr[1], targets, substeps, cache=pr[3], **props)
+    for step in range(steps):
+        eng.simulate(calls)
+        out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, calls, cache=c_o, **props)
+        for k, pr in enumerate(probes):
+            if step > 0:  # step 0's perturbation is the initial one above
+                noise = np.random.default_rng(1000 * k + step).standard_normal(pr[1][:, :, 0].shape)
+                pr[1][:, :, 0] += (1e-6 * noise).astype(np.float32)
+            pr[2] = O.physics_step(eng.he_model, sp, pr[0], pr[1], targets, calls, cache=pr[3], **props)
         torch.cuda.synchronize()
         kg = contact_keys(eng.contact_cache.cpu().numpy())
         ko = contact_keys(c_o)
@@ -372,6 +377,16 @@ def test_physics_solver_tolerance_matches_oracle(he_model):
     _physics_compare(he_model, root, dof, targets, steps=5, solver_tolerance=1e-5)
 
 
+def test_cold_solve_matches_oracle(he_model, model):
+    """warm_start = 0 is cold in every physics step of a launch, as in the oracle (the
+    kernel used to warm-start the second physics step from the first's impulses): standing bodies
+    under random targets, 4 sweeps, 5 policy steps."""
+    rng = np.random.default_rng(14)
+    root, dof = cases.standing_state(model, 48, rng, xy_jitter=1.0)
+    targets = rng.uniform(-0.2, 0.2, (48, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, steps=5, warm_start=0, solver_iterations=4, max_skip=0.0)
+
+
 def test_physics_domain_randomised_terrain(he_model, model):
     """Config 5 extension: per-env mass scale, friction and terrain kind vs the oracle, 3 steps,
     positions and velocities."""
@@ -383,9 +398,9 @@ def test_physics_domain_randomised_terrain(he_model, model):
     fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
     tk = (np.arange(n) % 3).astype(np.int32)
     # a 0.1 m drop onto slopes and step edges (feet straddling an edge tip over): the divergent
-    # contact-set stress case; 5.7% of the elements were ill-conditioned on the r02 box
+    # contact-set stress case (0% widened on the r02 final box; bound 1%)
     _physics_compare(he_model, root, dof, np.zeros((n, 69), np.float32), steps=3, env_props=(ms, fr, tk),
-                     max_widened=0.08)
+                     max_widened=0.01)
 
 
 def test_knee_limit_matches_oracle(he_model, model):
@@ -408,10 +423,13 @@ def test_contact_overflow_counted_and_reduced(he_model):
     the oracle, keeps the same (deepest) contact set, and the settled state matches."""
     rng = np.random.default_rng(5)
     root, dof = cases.lying_state(32, rng)
+    # lowered to 0.08-0.10 m: limbs start deep in the plane, 25-40 contacts generated per env, and
+    # the overflow persists through the policy step (the oracle: 12 of 32 envs still drop contacts
+    # in the last physics step)
+    root[:, 2] = 0.08 + rng.uniform(0, 0.02, 32).astype(np.float32)
     targets = np.zeros((32, 69), np.float32)
-    # the first step: limbs start inside the plane, ~25-30 contacts per env (the overflow case)
     eng, out = _physics_compare(he_model, root, dof, targets, steps=1, max_skip=0.05, max_widened=0.05)
-    assert (out["dropped"] > 0).sum() >= 3, "the case must overflow"  # 5 of 32 envs on the box (r02)
+    assert (out["dropped"] > 0).sum() >= 8, "the case must overflow"
 
 
 def test_env_step_fused_matches_oracle(he_model, model, golden):
@@ -514,11 +532,15 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
 @pytest.mark.parametrize("fused", [1, 0])
 def test_env_step_single_call_equals_two_calls(he_model, model, golden, fused):
     """he_env_step -- as one launch (the imitation step in the physics kernel's epilogue) and as two
-    -- is exactly he_step_actions followed by he_imitation_reset_step, bit for bit."""
+    -- is exactly he_step_actions followed by he_imitation_reset_step, bit for bit: obs, reward,
+    reset / terminate flags, the state and the warm-start cache, over 12 steps of random actions
+    under which bodies fall and the device resets them (their cache signature is invalidated, so the
+    next solve is cold). The two-launch form is held to the oracle by test_env_step_fused_matches_oracle."""
     from humanoid_amd.model import pd_action_offset_scale
     g = golden("env_step")
     n = 24
     outs = []
+    n_reset = 0
     for single in (True, False):
         eng = make_engine(he_model, n)
         eng.set_fused_step(fused)
@@ -532,17 +554,31 @@ def test_env_step_single_call_equals_two_calls(he_model, model, golden, fused):
         em = eng.env_motion(torch.arange(n, device="cuda:0"), st, so, go, prog)
         bufs = [torch.zeros(n, 934, device="cuda:0"), torch.zeros(n, device="cuda:0"), torch.zeros(n, 5, device="cuda:0"),
                 torch.zeros(n, dtype=torch.uint8, device="cuda:0"), torch.zeros(n, dtype=torch.uint8, device="cuda:0")]
-        a = torch.full((n, 69), 0.3, device="cuda:0")
-        for k in range(3):
+        rng = np.random.default_rng(31)
+        trace = []
+        for k in range(12):
+            a = cu(rng.uniform(-1.0, 1.0, (n, 69)).astype(np.float32))
             if single:
                 eng.env_step(_abi.imitation_params(), em, a, *bufs, seed=7, step_index=k)
             else:
                 eng.step_actions(a, 2)
                 eng.imitation_reset_step(_abi.imitation_params(), em, *bufs, seed=7, step_index=k)
-        torch.cuda.synchronize()
-        outs.append([b.cpu().numpy() for b in bufs] + [eng.rb_state.cpu().numpy()])
-    for x, y in zip(*outs):
-        np.testing.assert_array_equal(x, y)
+            torch.cuda.synchronize()
+            rs = bufs[3].cpu().numpy().astype(bool)
+            cache = eng.contact_cache.cpu().numpy()
+            r = eng.root_states.cpu().numpy()
+            if single:
+                n_reset += int(rs.sum())
+                # a reset env's cache no longer matches its (new) root pose: the next solve is cold
+                if rs.any():
+                    assert (cache[rs, :7] != r[rs, :7]).any(axis=1).all()
+            trace.append([b.cpu().numpy() for b in bufs] + [eng.rb_state.cpu().numpy(), r, cache,
+                                                           eng.dof_state.cpu().numpy()])
+        outs.append(trace)
+    assert n_reset > 0, "the run must exercise the device reset"
+    for ta, tb in zip(*outs):
+        for x, y in zip(ta, tb):
+            np.testing.assert_array_equal(x, y)
 
 
 def test_model_with_more_boxes_than_corner_lanes_is_refused(he_model):
@@ -581,116 +617,108 @@ def test_limit_backstop_matches_oracle(he_model, model):
         dof[e, 3 * j[e]:3 * j[e] + 3, 1] = (axis[e] * 60.0).astype(np.float32)
     targets = np.zeros((n, 69), np.float32)
     sim = dict(self_collision=0, kp_scale=0.0, kd_scale=0.0)
-    eng, _ = _physics_compare(he_model, root, dof, targets, substeps=1, steps=1, max_skip=0.0,
-                              solver_iterations=0, warm_start=0, **sim)
+    eng, _ = _physics_compare(he_model, root, dof, targets, calls=1, steps=1, max_skip=0.0,
+                              solver_iterations=0, warm_start=0, substeps=1, **sim)
     q = eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0].reshape(n, 23, 3)
     t = np.linalg.norm(q[np.arange(n), j].astype(np.float64), axis=1)
     np.testing.assert_allclose(t, np.pi - 0.01, atol=2e-6)
     assert ((q[np.arange(n), j] * axis).sum(1) > 0).all()
     # with the rows (one policy step: 60 rad/s joints spread a 1e-4 m difference within ~3 steps)
-    _physics_compare(he_model, root, dof, targets, substeps=2, steps=1, max_skip=0.0, **sim)
+    _physics_compare(he_model, root, dof, targets, calls=2, steps=1, max_skip=0.0, **sim)
 
 
-def test_bias_predictor_airborne_matches_oracle(he_model):
-    """he_sim_params.bias_predictor on the GPU (he_physics.hip: bias_predictor; the bias again at the
-    free velocity, one more L^-1 / L^-T pass through the same factor) against the oracle's
-    (he_oracle_physics.c: substep), airborne actuated bodies, one policy step."""
+def test_explicit_bias_matches_oracle(he_model, model):
+    """bias_midpoint = 0 (the velocity-dependent bias explicit, at u0) on the GPU against
+    the oracle: airborne actuated bodies (one policy step) and the PD stand-still (10 steps)."""
     rng = np.random.default_rng(21)
     root, dof = cases.random_state(64, rng, height=(3.0, 4.0))
     targets = rng.uniform(-0.5, 0.5, (64, 69)).astype(np.float32)
-    _physics_compare(he_model, root, dof, targets, self_collision=0, bias_predictor=1, max_skip=0.0,
+    _physics_compare(he_model, root, dof, targets, self_collision=0, bias_midpoint=0, max_skip=0.0,
                      max_widened=0.0)
-
-
-def test_bias_predictor_trajectories_match_oracle(he_model, model):
-    """The predictor's joint-angle and CoM trajectories at 1e-4 over 10 policy steps: airborne with
-    self collision, and the PD stand-still on the plane (contacts, warm start)."""
-    rng = np.random.default_rng(22)
-    root, dof = cases.random_state(32, rng, height=(6.0, 7.0), ang=0.4, vel=0.5)
-    targets = rng.uniform(-0.5, 0.5, (32, 69)).astype(np.float32)
-    _physics_compare(he_model, root, dof, targets, steps=10, bias_predictor=1, max_skip=0.0, max_widened=0.01)
     root, dof = cases.standing_state(model, 32, rng, xy_jitter=1.0)
-    _physics_compare(he_model, root, dof, np.zeros((32, 69), np.float32), steps=10, bias_predictor=1,
+    _physics_compare(he_model, root, dof, np.zeros((32, 69), np.float32), steps=10, bias_midpoint=0,
                      max_skip=0.0, max_widened=0.05)
 
 
-def test_bias_predictor_tames_the_runaway_on_gpu(he_model, model):
-    """DESIGN §5's runaway regime through the engine: airborne bodies under random targets U(+-0.5)
-    of the PD scale renewed every policy step for 3 s. Without the predictor the median internal
-    kinetic energy runs away (> 5e3 J, as the oracle's CPU test pins); with it, it stays at the
-    drives' level (< 1e3 J)."""
+def test_world_angular_velocity_clamp_matches_oracle(he_model, model):
+    """max_angular_velocity on each link's WORLD angular velocity (PxRigidBody) and
+    max_joint_velocity on the joint rates, both active: airborne bodies spun up to 60-80 rad/s with
+    the caps lowered to 40 / 30 rad/s, one policy step, against the oracle; no link leaves the cap."""
+    rng = np.random.default_rng(24)
+    n = 64
+    root, dof = cases.random_state(n, rng, height=(3.0, 4.0), vel=0.0)
+    root[:, 10:13] = rng.normal(0, 20.0, (n, 3)).astype(np.float32)
+    dof[..., 1] = rng.normal(0, 25.0, (n, 69)).astype(np.float32)
+    targets = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+    eng, out = _physics_compare(he_model, root, dof, targets, self_collision=0, max_angular_velocity=40.0,
+                                max_joint_velocity=30.0, max_skip=0.0, max_widened=0.0)
+    rb = eng.rb_state.view(n, 24, 13).cpu().numpy()
+    w = np.linalg.norm(rb[..., 10:13].astype(np.float64), axis=-1)
+    # the rows report the state after the last integration, whose world rates use the integrated
+    # rotations: within the cap up to the rotation over one physics step
+    assert w.max() < 40.0 * 1.5, w.max()
+
+
+def _random_action_gpu(he_model, model, n, amp, steps, airborne=False, **sim):
     from humanoid_amd.model import pd_action_offset_scale
-    _require_gpu()
     off, sc = pd_action_offset_scale(model)
-    n = 256
-    M = float(np.sum(model.mass))
-    res = {}
-    for pred in (0, 1):
-        rng = np.random.default_rng(8)
-        root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
-        root[:, 2] += 200.0
-        eng = make_engine(he_model, n, self_collision=0, bias_predictor=pred)
-        eng.root_states.copy_(cu(root))
-        eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
-        for _ in range(90):
-            a = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
-            eng.dof_targets.copy_(cu((off + sc * a).astype(np.float32)))
-            eng.simulate(2)
-        torch.cuda.synchronize()
-        rg = eng.root_states.cpu().numpy()
-        dg = eng.dof_state.view(n, 69, 2).cpu().numpy()
-        assert np.isfinite(rg).all() and np.isfinite(dg).all()
-        me = O.momentum_energy(eng.he_model, _abi.default_sim_params(self_collision=0), rg, dg)
-        res[pred] = float(np.median(me[:, 6] - 0.5 * (me[:, :3] ** 2).sum(1) / M))
-        del eng
-    print(f"median internal KE after 3 s: {res}")
-    assert res[0] > 5e3, res
-    assert res[1] < 1e3, res
-
-
-def test_bias_predictor_keeps_standing_bodies_grounded_on_gpu(he_model, model):
-    """Standing bodies on the plane under U(+-0.75) random actions for 2 s through the engine: with
-    the predictor no root exceeds 20 m/s (the oracle's CPU test, at 256 envs); without it most envs
-    run away (profiles/r02/action_regimes.json), printed for the record."""
-    from humanoid_amd.model import pd_action_offset_scale
-    _require_gpu()
-    off, sc = pd_action_offset_scale(model)
-    n = 256
-    vmax = {}
-    for pred in (0, 1):
-        rng = np.random.default_rng(8)
-        root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
-        eng = make_engine(he_model, n, bias_predictor=pred)
-        eng.root_states.copy_(cu(root))
-        eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
-        v = np.zeros(n)
-        for _ in range(60):
-            a = rng.uniform(-0.75, 0.75, (n, 69)).astype(np.float32)
-            eng.dof_targets.copy_(cu((off + sc * a).astype(np.float32)))
-            eng.simulate(2)
-            v = np.maximum(v, torch.linalg.norm(eng.root_states[:, 7:10], dim=1).cpu().numpy())
-        vmax[pred] = v
-        del eng
-    print(f"envs over 20 m/s: without {int((vmax[0] > 20).sum())}/{n}, with {int((vmax[1] > 20).sum())}/{n}")
-    assert np.isfinite(vmax[1]).all() and vmax[1].max() < 20.0, vmax[1].max()
-
-
-def test_bias_predictor_contact_rich_and_terrain_match_oracle(he_model, model):
-    """The predictor under contact: near-ground tumbling and lying bodies (one step), and the
-    config-5 mass / friction / terrain randomisation (3 steps), against the oracle with it on, under
-    the same bars as the tests without it."""
-    rng = np.random.default_rng(23)
-    root, dof = cases.random_state(64, rng, height=(0.85, 1.0), ang=0.8, vel=0.5)
-    r2, d2 = cases.lying_state(32, rng)
-    root = np.concatenate([root, r2])
-    dof = np.concatenate([dof, d2])
-    targets = rng.uniform(-0.5, 0.5, (96, 69)).astype(np.float32)
-    _physics_compare(he_model, root, dof, targets, bias_predictor=1)
-    n = 48
+    rng = np.random.default_rng(8)
     root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
-    root[:, 2] += 0.1
-    ms = rng.uniform(0.8, 1.2, (n, 24)).astype(np.float32)
-    fr = rng.uniform(0.5, 1.25, n).astype(np.float32)
-    tk = (np.arange(n) % 3).astype(np.int32)
-    _physics_compare(he_model, root, dof, np.zeros((n, 69), np.float32), steps=3, env_props=(ms, fr, tk),
-                     max_widened=0.08, bias_predictor=1)
+    if airborne:
+        root[:, 2] += 200.0
+        sim.setdefault("self_collision", 0)
+    eng = make_engine(he_model, n, **sim)
+    eng.root_states.copy_(cu(root))
+    eng.dof_state.copy_(cu(dof.reshape(n * 69, 2)))
+    off_t, sc_t = cu(np.asarray(off, np.float32)), cu(np.asarray(sc, np.float32))
+    gen = torch.Generator(device="cuda:0")
+    gen.manual_seed(8)
+    vmax = torch.zeros(n, device="cuda:0")
+    for _ in range(steps):
+        a = (torch.rand(n, 69, device="cuda:0", generator=gen) * 2.0 - 1.0) * amp
+        eng.dof_targets.copy_(off_t + sc_t * a)
+        eng.simulate(2)
+        vmax = torch.maximum(vmax, torch.linalg.norm(eng.root_states[:, 7:10], dim=1))
+    torch.cuda.synchronize()
+    rg = eng.root_states.cpu().numpy()
+    dg = eng.dof_state.view(n, 69, 2).cpu().numpy()
+    assert np.isfinite(rg).all() and np.isfinite(dg).all()
+    me = O.momentum_energy(eng.he_model, _abi.default_sim_params(), rg, dg)
+    M = float(np.sum(model.mass))
+    ke = me[:, 6] - 0.5 * (me[:, :3] ** 2).sum(1) / M
+    return vmax.cpu().numpy(), ke, dg
+
+
+def test_midpoint_bias_tames_the_runaway_on_gpu(he_model, model):
+    """DESIGN §5's runaway regime through the engine: airborne bodies under random targets U(+-1) of
+    the PD scale renewed every policy step for 3 s. With the bias explicit the median internal
+    kinetic energy runs away (the oracle's CPU test: ~50 kJ); with the default midpoint bias it stays
+    at the dt-refined level (oracle ~1.0 kJ)."""
+    _require_gpu()
+    _, ke_exp, _ = _random_action_gpu(he_model, model, 256, 1.0, 90, airborne=True, bias_midpoint=0)
+    _, ke_mid, _ = _random_action_gpu(he_model, model, 256, 1.0, 90, airborne=True)
+    res = (float(np.median(ke_exp)), float(np.median(ke_mid)))
+    print(f"median internal KE after 3 s (explicit, midpoint): {res}")
+    assert res[0] > 1e4, res
+    assert res[1] < 1.5e3, res
+
+
+def test_saturated_random_actions_stay_physical_on_gpu(he_model, model):
+    """VERDICT r02 item 1 at full size: 4096 standing envs under U(+-1) random actions (new every policy
+    step) for 2 s. The median internal kinetic energy stays at the dt-refined level (oracle: 0.90 kJ;
+    1/480 s physics steps: 0.80 kJ; the explicit bias: 22 kJ with roots at 10^2 m/s) and no joint
+    passes its angle cap. Root speeds: the fastest roots are pelvises whipped by flailing legs while
+    airborne, the tail of the physics itself -- the fp64 oracle under this scheme reaches 9.5-10.7 m/s
+    over four 4096-env seeds (0-2 envs past 10 m/s), the 1/480 s refinement 8.75 m/s
+    (tools/energy_probe.py) -- so the bar is: no root past 15 m/s, at most 0.1% of envs
+    past 10 m/s."""
+    _require_gpu()
+    n = 4096
+    vmax, ke, dg = _random_action_gpu(he_model, model, n, 1.0, 60)
+    q = np.linalg.norm(dg[..., 0].reshape(n, 23, 3), axis=-1)
+    print(f"envs over 10 m/s: {int((vmax > 10).sum())}/{n}, max root speed {vmax.max():.2f} m/s, "
+          f"median internal KE {np.median(ke):.1f} J, max joint angle {q.max():.4f}")
+    assert vmax.max() < 15.0, vmax.max()
+    assert int((vmax > 10).sum()) <= n // 1000, int((vmax > 10).sum())
+    assert np.median(ke) < 1.5e3
+    assert q.max() < np.pi - 0.01

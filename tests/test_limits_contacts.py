@@ -162,7 +162,9 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
     j = 10  # Neck's joint (body 11): a light link
     dof[:, 3 * j:3 * j + 3, 0] = (axis * (np.pi - 0.025)).astype(np.float32)
     dof[:, 3 * j:3 * j + 3, 1] = (axis * 60.0).astype(np.float32)
-    sp = _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0, warm_start=0)
+    # one physics step of 1/60 s (substeps 1): the backstop's own case
+    sp = _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0, warm_start=0,
+                                 substeps=1)
     r, d = root.copy(), dof.copy()
     O.physics_step(he_model, sp, r, d, np.zeros((n, 69), np.float32), 1)
     q = d[:, 3 * j:3 * j + 3, 0].astype(np.float64)
@@ -174,24 +176,23 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
     # the other joints equal a run without limits (the backstop acts only past pi - 0.01)
     r2, d2 = root.copy(), dof.copy()
     O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0,
-                                                     warm_start=0, joint_limits=0),
+                                                     warm_start=0, joint_limits=0, substeps=1),
                    r2, d2, np.zeros((n, 69), np.float32), 1)
     others = [k for k in range(23) if k != j]
     qs = d[:, :, 0].reshape(n, 23, 3)[:, others]
     np.testing.assert_array_equal(qs, d2[:, :, 0].reshape(n, 23, 3)[:, others])
     # with the sweeps, the limit row holds it first, at pi - 0.02
     r3, d3 = root.copy(), dof.copy()
-    O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0), r3, d3,
+    O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, substeps=1), r3, d3,
                    np.zeros((n, 69), np.float32), 1)
     t3 = np.linalg.norm(d3[:, 3 * j:3 * j + 3, 0].astype(np.float64), axis=1)
     assert (t3 < np.pi - 0.015).all() and (t3 > np.pi - 0.03).all()
 
 
 def test_moderate_random_actions_stay_physical(he_model, model):
-    """DESIGN §5's boundary of the violent regime, as a regression guard: random actions
-    U(-0.5, 0.5) of the PD scale on standing bodies for 2 s keep every root below 10 m/s and
-    no joint past the limit (the saturated U(-1, 1) regime spins light links at the 100 rad/s cap
-    and throws bodies at 10^2 m/s in the same equations)."""
+    """Random actions U(-0.5, 0.5) of the PD scale on standing bodies for 2 s keep every root below
+    5 m/s (measured 5.7 max over 512 envs, tools/energy_probe.py; CoM below 4.4) and no joint past the
+    limit. The saturated U(-1, 1) case is test_physics_invariants.py::test_saturated_random_actions_stay_physical."""
     from humanoid_amd.model import pd_action_offset_scale
     n = 64
     rng = np.random.default_rng(8)
@@ -201,9 +202,9 @@ def test_moderate_random_actions_stay_physical(he_model, model):
     cache = O.new_cache(n)
     vmax = 0.0
     for _ in range(60):
-        a = rng.uniform(-0.25, 0.25, (n, 69)).astype(np.float32)
+        a = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
         O.physics_step(he_model, sp, root, dof, (off + sc * a).astype(np.float32), 2, cache=cache)
         vmax = max(vmax, float(np.linalg.norm(root[:, 7:10], axis=1).max()))
     q = np.linalg.norm(dof[..., 0].reshape(n, 23, 3), axis=-1)
-    assert vmax < 10.0, vmax
+    assert vmax < 7.0, vmax
     assert q.max() < np.pi - 0.01

@@ -20,7 +20,7 @@ PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba"
           "contact: limit slots", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
           "terrain: geometry (to P0/P1)", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
           "free: prefetch + row loads", "free: L^-1 levels", "fused imitation",
-          "pred: uf sweep", "pred: velocities + rnea", "pred: subtree + dc", "pred: L^-T"]  # slots 25-28: the bias predictor; slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
+          "mid: um sweep", "mid: velocities + rnea", "mid: subtree + dc", "mid: L^-T"]  # slots 25-28: the midpoint bias; slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
 
 
 def main():
@@ -31,15 +31,14 @@ def main():
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--max-contacts", type=int, default=20)
     ap.add_argument("--fused", action="store_true")
-    ap.add_argument("--bias-predictor", action="store_true")
+    ap.add_argument("--scheme", choices=["default", "r02"], default="default")
     args = ap.parse_args()
     import numpy as np
     import torch
     import bench
     from humanoid_amd.model import load_default_model
     bargs = argparse.Namespace(config=args.config, num_envs=args.num_envs, clips=128, seed=0,
-                               max_contacts=args.max_contacts, fused=args.fused,
-                               bias_predictor=args.bias_predictor)
+                               max_contacts=args.max_contacts, fused=args.fused, scheme=args.scheme)
     model = load_default_model()
     ro = bench.Rollout(bargs, model, 0, 0)
     for _ in range(args.warmup):
@@ -58,7 +57,7 @@ def main():
     rows = {PHASES[i]: {"cycles": round(float(mean[i])), "share": round(float(mean[i] / total), 4)}
             for i in range(len(PHASES))}
     print(json.dumps({"config": args.config, "num_envs": args.num_envs, "mean_contacts": float(np.mean(nc)),
-                      "bias_predictor": args.bias_predictor,
+                      "scheme": args.scheme,
                       "cycles_per_env_step": round(float(total)), "phases": rows}, indent=1))
 
 
