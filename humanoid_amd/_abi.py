@@ -14,7 +14,9 @@ MAX_PAIRS, MAX_CONTACTS = 256, 21
 OBS_SELF, OBS_TASK, OBS_DIM = 358, 576, 934
 
 (BUF_ROOT_STATE, BUF_DOF_STATE, BUF_RB_STATE, BUF_CONTACT_FORCE, BUF_DOF_FORCE, BUF_DOF_TARGET, BUF_NUM_CONTACTS,
- BUF_DROPPED_CONTACTS, BUF_CONTACT_CACHE) = range(9)
+ BUF_DROPPED_CONTACTS, BUF_CONTACT_CACHE, BUF_INIT_ROOT_STATE) = range(10)
+# StateInit (envs/state_init.py) -> he_imitation_params.state_init
+STATE_INIT = {"Default": 0, "Start": 1, "Random": 2, "Hybrid": 3}
 CACHE_WORDS, CACHE_KEYS, CACHE_LAMBDA = 96, 8, 32  # he_sim_params warm-start cache layout
 DTYPE_F32, DTYPE_I32 = 1, 2
 
@@ -49,7 +51,8 @@ class HeImitationParams(C.Structure):
         ("w_pos", C.c_float), ("w_rot", C.c_float), ("w_vel", C.c_float), ("w_ang_vel", C.c_float),
         ("power_coef", C.c_float), ("use_power_reward", C.c_int32), ("control_dt", C.c_float),
         ("enable_early_termination", C.c_int32), ("eval_mode", C.c_int32), ("reset_body_mask", C.c_int32),
-        ("term_dist", C.c_float * NB), ("state_init", C.c_int32), ("reserved", C.c_int32),
+        ("term_dist", C.c_float * NB), ("state_init", C.c_int32), ("hybrid_init_prob", C.c_float),
+        ("test_mode", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -125,8 +128,10 @@ def default_sim_params(**kw) -> HeSimParams:
 
 def imitation_params(reward=None, control_dt=1.0 / 30.0, use_power_reward=True, power_coef=0.0005,
                      enable_early_termination=True, eval_mode=False, termination_distance=0.25,
-                     reset_body_ids=None, state_init_start=False) -> HeImitationParams:
-    """config.py:37-50 (RewardConfig), :97-112 (EnvConfig) defaults."""
+                     reset_body_ids=None, state_init="Random", hybrid_init_prob=0.5,
+                     test_mode=False) -> HeImitationParams:
+    """config.py:37-50 (RewardConfig), :97-112, :114, :139 (EnvConfig) defaults. state_init is a
+    StateInit name (state_init.py); test_mode = flag_test (reference-state inits at motion time 0)."""
     r = dict(k_pos=100.0, k_rot=10.0, k_vel=0.1, k_ang_vel=0.1, w_pos=0.5, w_rot=0.3, w_vel=0.1, w_ang_vel=0.1)
     if reward:
         r.update({k: v for k, v in reward.items() if k in r})
@@ -144,7 +149,11 @@ def imitation_params(reward=None, control_dt=1.0 / 30.0, use_power_reward=True, 
     td = np.broadcast_to(np.asarray(termination_distance, np.float32), (NB,))
     for b in range(NB):
         p.term_dist[b] = float(td[b])
-    p.state_init = 1 if state_init_start else 0
+    if state_init not in STATE_INIT:
+        raise ValueError(f"Unsupported state initialization strategy: {state_init}")
+    p.state_init = STATE_INIT[state_init]
+    p.hybrid_init_prob = float(hybrid_init_prob)
+    p.test_mode = int(bool(test_mode))
     return p
 
 

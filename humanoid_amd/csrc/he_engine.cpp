@@ -63,6 +63,8 @@ struct he_engine {
     int32_t* num_contacts = nullptr;
     int32_t* dropped = nullptr;
     float* cache = nullptr;
+    float* init_root = nullptr;     // [N,13] HE_BUF_INIT_ROOT_STATE
+    float* d_rest = nullptr;        // [24,3] zero-pose body origins in the root frame
     bool component_limits = false;  // a dof bound inside (-pi + guard, pi - guard): not implemented
     int fused_step = -1;            // he_env_step as one launch: 1 / 0 (he_set_fused_step), -1 auto
     const float *mass_scale = nullptr, *friction = nullptr;
@@ -144,6 +146,13 @@ int he_set_model(he_engine* h, const he_model* model) {
     if (!h->d_topo) HE_CHECK(dalloc(&h->d_topo, 1));
     HE_CHECK(hipMemcpy(h->d_model, model, sizeof(he_model), hipMemcpyHostToDevice));
     HE_CHECK(hipMemcpy(h->d_topo, &topo, sizeof(PhysTopo), hipMemcpyHostToDevice));
+    // the zero pose's body origins in the root frame: every local rotation is the identity, so the
+    // joint offsets add up along the chain (the Default state init's rigid-body rows)
+    float rest[HE_NUM_BODIES][3] = {};
+    for (int b = 1; b < HE_NUM_BODIES; ++b)
+        for (int c = 0; c < 3; ++c) rest[b][c] = rest[model->parents[b]][c] + model->local_pos[b][c];
+    if (!h->d_rest) HE_CHECK(dalloc(&h->d_rest, HE_NUM_BODIES * 3));
+    HE_CHECK(hipMemcpy(h->d_rest, rest, sizeof(rest), hipMemcpyHostToDevice));
     h->has_model = true;
     return 0;
 }
@@ -174,6 +183,9 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
         r[6] = 1.f;
     }
     HE_CHECK(hipMemcpy(h->root, root.data(), root.size() * sizeof(float), hipMemcpyHostToDevice));
+    // _initial_humanoid_root_states (humanoid_phc.py:522-523): the creation poses, zero velocities
+    HE_CHECK(dalloc(&h->init_root, (size_t)N * 13));
+    HE_CHECK(hipMemcpy(h->init_root, root.data(), root.size() * sizeof(float), hipMemcpyHostToDevice));
     HE_CHECK(hipMemset(h->dof_state, 0, (size_t)N * HE_NUM_DOF * 2 * sizeof(float)));
     HE_CHECK(hipMemset(h->rb, 0, (size_t)N * HE_NUM_BODIES * 13 * sizeof(float)));
     HE_CHECK(hipMemset(h->cf, 0, (size_t)N * HE_NUM_BODIES * 3 * sizeof(float)));
@@ -190,7 +202,7 @@ int he_destroy(he_engine* h) {
     if (!h) return 0;
     hipSetDevice(h->device);
     void* ptrs[] = {h->d_model, h->d_topo, h->root, h->dof_state, h->rb, h->cf, h->dof_force, h->targets,
-                    h->num_contacts, h->dropped, h->cache, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
+                    h->num_contacts, h->dropped, h->cache, h->init_root, h->d_rest, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
                     h->m_dt, h->m_starts, h->m_nframes};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -213,6 +225,7 @@ int he_get_buffer(he_engine* h, int kind, void** dptr, int64_t* shape, int* ndim
         case HE_BUF_NUM_CONTACTS: *dptr = h->num_contacts; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
         case HE_BUF_DROPPED_CONTACTS: *dptr = h->dropped; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
         case HE_BUF_CONTACT_CACHE: *dptr = h->cache; *ndim = 2; shape[0] = N; shape[1] = HE_CACHE_WORDS; break;
+        case HE_BUF_INIT_ROOT_STATE: *dptr = h->init_root; *ndim = 2; shape[0] = N; shape[1] = 13; break;
         default: return fail("he_get_buffer: unknown buffer kind %d", kind);
     }
     return 0;
@@ -494,6 +507,12 @@ static int imit_common(he_engine* h, const he_imitation_params* p, const he_env_
     a.progress = em->progress;
     a.ev = h->eval;
     a.has_eval = h->has_eval;
+    a.init_root = h->init_root;
+    a.rest_pos = h->d_rest;
+    if (p->state_init < HE_STATE_INIT_DEFAULT || p->state_init > HE_STATE_INIT_HYBRID)
+        return fail("%s: state_init %d is not a StateInit (0 Default, 1 Start, 2 Random, 3 Hybrid)", what, p->state_init);
+    if (p->state_init == HE_STATE_INIT_HYBRID && !(p->hybrid_init_prob >= 0.f && p->hybrid_init_prob <= 1.f))
+        return fail("%s: hybrid_init_prob must be in [0, 1]", what);
     return 0;
 }
 // the AMP update that follows an imitation launch (he_set_amp)
@@ -511,6 +530,10 @@ static hipError_t amp_after(he_engine* h, const ImitArgs& ia, int mode, hipStrea
     a.mode = mode;
     a.control_dt = ia.p.control_dt;
     a.amp = h->amp;
+    a.ip = ia.p;
+    a.phases = ia.phases;
+    a.seed = ia.seed;
+    a.step = ia.step;
     return launch_amp(a, stream);
 }
 }  // namespace

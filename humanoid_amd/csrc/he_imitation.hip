@@ -308,12 +308,21 @@ __global__ void __launch_bounds__(256) amp_kernel(AmpArgs a) {
     const int e = a.env_ids ? a.env_ids[slot] : slot;
     const bool init = a.mode == 2 || (a.mode == 1 && a.reset[e]);
     if (k > 0 && !init) return;
+    // the reset's state init, from the same draw as the imitation launch's (resolve_init)
+    bool ref = true;
+    if (init) {
+        float ph;
+        ref = resolve_init(a.ip, a.mode == 2 ? a.phases[slot] : hash_uniform(a.seed, a.step, (uint32_t)e), ph);
+    }
     const bool act = lane < NB;
     const int b = act ? lane : 0;
     float* row = a.amp.amp_obs + ((size_t)e * S + k) * AMP_W;
-    float* demo = (init && a.amp.amp_obs_demo) ? a.amp.amp_obs_demo + ((size_t)e * S + k) * AMP_W : nullptr;
-    if (k == 0) {
-        if (!init && S > 1) amp_shift(row, S, lane);
+    float* demo = (init && ref && a.amp.amp_obs_demo) ? a.amp.amp_obs_demo + ((size_t)e * S + k) * AMP_W : nullptr;
+    // row 0, and for a Default init every history row (_init_amp_obs_default, humanoid_phc.py:801-803:
+    // the history is the current observation; the reference raises "Not tested yet" before it,
+    // :794-796, and the engine runs the function it left): from the simulated (or just reset) state
+    if (k == 0 || !ref) {
+        if (k == 0 && !init && S > 1) amp_shift(row, S, lane);
         // _compute_amp_observations from the simulated (or just reset) state
         const SimBody s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);
         f3 dp = f3{0.f, 0.f, 0.f}, dv = f3{0.f, 0.f, 0.f};

@@ -202,6 +202,59 @@ HE_DEV void reset_body(const ImitArgs& a, int e, int b, int64_t mid, float t, f3
     }
 }
 
+// The state init of a reset from its uniform draw u (include/humanoid_engine.h, he_sim_params'
+// StateInit block; oracle/he_oracle.c resolve_init): true = a reference-state init at phase `ph`
+// (humanoid_phc.py:694-731, 848-856), false = the initial pose (_reset_default, :688-692).
+HE_DEV bool resolve_init(const he_imitation_params& p, float u, float& ph) {
+#pragma clang fp contract(off)
+    bool ref = p.state_init != HE_STATE_INIT_DEFAULT;
+    ph = u;
+    if (p.state_init == HE_STATE_INIT_HYBRID) {  // torch.bernoulli(hybrid_init_prob) (:733-745)
+        ref = u < p.hybrid_init_prob;
+        ph = ref ? u / p.hybrid_init_prob : 0.0f;
+    }
+    if (p.state_init == HE_STATE_INIT_START || p.test_mode) ph = 0.0f;
+    return ref;
+}
+
+// _reset_default + _reset_env_tensors (humanoid_phc.py:688-692, 747-780) of body b of env e: the root
+// row of HE_BUF_INIT_ROOT_STATE, zero dof positions / velocities / targets, and the rigid-body row of
+// that pose (every local rotation the identity: the root rotation, origin root + R rest_pos[b]; the
+// velocities of the initial root state, which the reference zeroes), zero contact force.
+HE_DEV void default_reset_body(const ImitArgs& a, int e, int b) {
+#pragma clang fp contract(off)
+    const float* ir = a.init_root + (size_t)e * 13;
+    const f3 rp = f3{ir[0], ir[1], ir[2]};
+    const f4 rq = f4{ir[3], ir[4], ir[5], ir[6]};
+    const f3 v = f3{ir[7], ir[8], ir[9]}, w = f3{ir[10], ir[11], ir[12]};
+    const f3 lo = f3{a.rest_pos[3 * b], a.rest_pos[3 * b + 1], a.rest_pos[3 * b + 2]};
+    const f3 ro = qrot_ref(rq, lo);
+    const f3 pos = rp + ro;
+    const f3 vel = v + f3{w.y * ro.z - w.z * ro.y, w.z * ro.x - w.x * ro.z, w.x * ro.y - w.y * ro.x};
+    float* rb = a.rb_state + ((size_t)e * NB + b) * 13;
+    rb[0] = pos.x; rb[1] = pos.y; rb[2] = pos.z;
+    rb[3] = rq.x; rb[4] = rq.y; rb[5] = rq.z; rb[6] = rq.w;
+    rb[7] = vel.x; rb[8] = vel.y; rb[9] = vel.z;
+    rb[10] = w.x; rb[11] = w.y; rb[12] = w.z;
+    if (a.contact_forces) {
+        float* cf = a.contact_forces + ((size_t)e * NB + b) * 3;
+        cf[0] = cf[1] = cf[2] = 0.0f;
+    }
+    if (b == 0) {
+        float* rs = a.root_states + (size_t)e * 13;
+#pragma unroll
+        for (int c = 0; c < 13; ++c) rs[c] = ir[c];
+    } else {
+        const int d = 3 * (b - 1);
+        float* ds = a.dof_state + ((size_t)e * ND + d) * 2;
+        ds[0] = ds[1] = ds[2] = ds[3] = ds[4] = ds[5] = 0.0f;
+        if (a.dof_targets) {
+            float* tg = a.dof_targets + (size_t)e * ND + d;
+            tg[0] = tg[1] = tg[2] = 0.0f;
+        }
+    }
+}
+
 // eval recording (he_imitation.hip; only the stand-alone kernel instantiates EVAL = true)
 HE_DEV void eval_record(const he_eval_buffers& ev, int e, int lane, bool act, f3 p, f3 g);
 
@@ -283,7 +336,7 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
     const float t = x.t;
     const BodyRef r = x.r;
     BodyRef r2 = x.r2;
-    bool do_reset = false;
+    bool do_reset = false, ref_init = true;
     float reset_time = 0.0f;
 
     if (a.mode != 2) {
@@ -337,17 +390,29 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
         }
         if (a.mode == 1 && reset) {
             do_reset = true;
-            // Random: sample_time_interval of a hashed phase; Start (and test mode): time 0
-            // (humanoid_phc.py:848-852)
-            float ph = a.p.state_init == 1 ? 0.f : hash_uniform(a.seed, a.step, (uint32_t)e);
-            reset_time = sample_time_interval(ph, mm.len);
+            // the reset's draw: a hashed uniform, resolved by the state init (humanoid_phc.py:679-692,
+            // 733-745, 848-856)
+            float ph;
+            ref_init = resolve_init(a.p, hash_uniform(a.seed, a.step, (uint32_t)e), ph);
+            reset_time = ref_init ? sample_time_interval(ph, mm.len) : 0.0f;
         }
     } else {
         do_reset = true;
-        reset_time = sample_time_interval(a.phases[slot], mm.len);
+        float ph;
+        ref_init = resolve_init(a.p, a.phases[slot], ph);
+        reset_time = ref_init ? sample_time_interval(ph, mm.len) : 0.0f;
     }
 
-    if (do_reset) {  // the group's branch is uniform
+    if (do_reset && !ref_init) {  // _reset_default: the motion bookkeeping stays (the group is uniform)
+        if (act) default_reset_body(a, e, b);
+        prog = 0;
+        if (leader) {
+            a.progress[e] = 0;
+            if (a.mode == 2) { a.reset[e] = 0; a.terminate[e] = 0; }
+        }
+        s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);  // the row this lane just wrote
+        r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
+    } else if (do_reset) {  // the group's branch is uniform
         if (act) reset_body(a, e, b, mid, reset_time, off);
         off = f3{0.f, 0.f, 0.f};
         start = reset_time;

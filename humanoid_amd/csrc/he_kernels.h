@@ -48,6 +48,8 @@ struct ImitArgs {
     uint64_t seed, step;
     he_eval_buffers ev;      // eval recording (modes 0/1) when has_eval
     int has_eval;
+    const float* init_root;  // [N,13] HE_BUF_INIT_ROOT_STATE (the Default / Hybrid state init)
+    const float* rest_pos;   // [24,3] body origins of the zero pose in the root frame (model)
 };
 
 // AMP observation update, launched after an imitation launch
@@ -63,6 +65,11 @@ struct AmpArgs {
     int mode;                 // 0 step update, 1 step update or init by reset flag, 2 init listed envs
     float control_dt;
     he_amp_buffers amp;
+    // the reset draw of each env (modes 1 / 2), to tell a Default init (history = the current row,
+    // _init_amp_obs_default) from a reference one (history from the motion)
+    he_imitation_params ip;
+    const float* phases;      // mode 2: [count]
+    uint64_t seed, step;
     // function-level form (he_amp_observations): explicit inputs, K rows into `out`
     const float *root_pos, *root_rot, *root_vel, *root_ang_vel, *dof_pos, *dof_vel, *key_pos;
     float* out;

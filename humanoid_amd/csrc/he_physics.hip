@@ -57,7 +57,10 @@ struct Lds {
     float q[ND], tgt[ND];
     float u0[NG], uf[NG], rhs[NG], coef[NG], Dinv[NG], sDinv[NG];
     float yh[NG];  // D^-1/2 L^-T (dt rhs): the free motion's share of the one L^-1 sweep
-    float ql[NB][4], qw[NB][4], pw[NB][3];
+    float ql[NB][4], qw[NB][4];
+    float pw[NB][3];  // body origins RELATIVE to the root origin o (world axes): every spatial quantity
+                      // is taken about o, and fp32 keeps ~1e-7 m of them however far o is from the
+                      // world origin (world = o + pw only where a world position is needed)
     float S[NG][6], IS[NG][6];
     float V[NB][6], Acc[NB][6], F[NB][6];
     float Ib[NB][10], Ic[NB][10];  // m, h(3), I(xx yy zz xy xz yz)
@@ -183,10 +186,6 @@ HE_DEV void crf(const float* V, const float* Fm, float* O) {
     O[0] = a.x; O[1] = a.y; O[2] = a.z; O[3] = b.x; O[4] = b.y; O[5] = b.z;
 }
 
-HE_DEV f3 body_point(const Lds& L, int b, f3 local) {
-    f4 q = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
-    return f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} + qapply(q, local);
-}
 
 // rotation-vector exponential / logarithm for the physics kernel: one sincos range reduction and
 // v_rcp_f32 quotients (1 ulp; the fp64 oracle's tolerance covers it). The imitation kernel keeps
@@ -990,7 +989,6 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     const BodyTopo& T = L.T;
     const bool act = lane < NB;
     const int b = act ? lane : 0;
-    const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
     const uint32_t jp = act ? T.jump4[b] : 0xFFFFFFFFu;
     f4 q;
     f3 p;
@@ -999,7 +997,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     const f4 qr = qnormalize(f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]});
     if (b == 0) {
         q = qr;
-        p = o;
+        p = f3{0.f, 0.f, 0.f};  // origins about o
         u[0] = L.u0[0]; u[1] = L.u0[1]; u[2] = L.u0[2];
     } else {
         const int d = 3 * (b - 1);
@@ -1027,8 +1025,8 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     jump(std::integral_constant<int, 1>{});
     jump(std::integral_constant<int, 2>{});
     if constexpr (kKinRounds == 4) jump(std::integral_constant<int, 3>{});
-    if (HE_KIN_ROOTREL && b != 0) {  // root-frame pose of the chain -> world
-        p = o + qapply(qr, p);
+    if (HE_KIN_ROOTREL && b != 0) {  // root-frame pose of the chain -> world axes, origin about o
+        p = qapply(qr, p);
         q = qmul(qr, q);
     }
     // own joint's velocity contribution: root (w0, v0 at o); joint b: (w, (p_b - o) x w), w = R_b u_b
@@ -1037,7 +1035,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         V[0] = u[0]; V[1] = u[1]; V[2] = u[2]; V[3] = L.u0[3]; V[4] = L.u0[4]; V[5] = L.u0[5];
     } else {
         const f3 w = qapply(q, f3{u[0], u[1], u[2]});
-        const f3 l = cross3(p - o, w);
+        const f3 l = cross3(p, w);
         V[0] = w.x; V[1] = w.y; V[2] = w.z; V[3] = l.x; V[4] = l.y; V[5] = l.z;
     }
     float vj[6];  // the joint's own velocity S_b u_b (RNEA velocity-product term below)
@@ -1113,7 +1111,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         const f4 qb = f4{L.qw[bb][0], L.qw[bb][1], L.qw[bb][2], L.qw[bb][3]};
         const f3 e = f3{c == 0 ? 1.f : 0.f, c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f};
         const f3 ax = qapply(qb, e);
-        const f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]} - o, ax);
+        const f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]}, ax);
         const float g[6] = {ax.x, ax.y, ax.z, l.x, l.y, l.z};
         float* S = L.S[i];
 #pragma unroll
@@ -1132,7 +1130,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
             f4 qb = f4{L.qw[bb][0], L.qw[bb][1], L.qw[bb][2], L.qw[bb][3]};
             f3 e = c == 0 ? f3{1.f, 0.f, 0.f} : (c == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
             f3 ax = qapply(qb, e);
-            f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]} - o, ax);
+            f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]}, ax);
             S[0] = ax.x; S[1] = ax.y; S[2] = ax.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
         }
     }
@@ -1300,10 +1298,10 @@ constexpr int COLD = HE_MOTION_COLD;
 // rotation, linear velocity of the origin, angular velocity
 HE_DEV SimBody body_row(const Lds& L, int b) {
     SimBody s;
-    s.pos = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]};
+    const f3 r = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]};  // about o
+    s.pos = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]} + r;
     s.rot = f4{L.qw[b][0], L.qw[b][1], L.qw[b][2], L.qw[b][3]};
     const f3 w = f3{L.V[b][0], L.V[b][1], L.V[b][2]};
-    const f3 r = f3{L.pw[b][0] - L.root_pos[0], L.pw[b][1] - L.root_pos[1], L.pw[b][2] - L.root_pos[2]};
     s.vel = f3{L.V[b][3], L.V[b][4], L.V[b][5]} + cross3(w, r);
     s.ang = w;
     return s;
@@ -1341,7 +1339,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     kinematics<true>(L, m, lane, a.p, !first);
     __builtin_amdgcn_s_setprio(0);
     STAMP(0);
-    const f3 o = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};
     // ---- body spatial inertias about o + RNEA body forces (gravity as base acceleration)
     if (lane < NB) {
         int b = lane;
@@ -1351,7 +1348,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         f3 c0, c1, c2;
         qcols(q, c0, c1, c2);
         f3 cw = qapply(q, f3{m.com[b][0], m.com[b][1], m.com[b][2]});
-        f3 s = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} + cw - o;
+        f3 s = f3{L.pw[b][0], L.pw[b][1], L.pw[b][2]} + cw;  // CoM about o
         const float* in = m.inertia[b];
         float Ib[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
         float R[3][3] = {{c0.x, c1.x, c2.x}, {c0.y, c1.y, c2.y}, {c0.z, c1.z, c2.z}};
@@ -1582,6 +1579,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     const bool corner = lane >= NB && cbody >= 0;
     const int tb_ = lane < NB ? lane : (corner ? cbody : 0);
     const int cc = lane & 7;  // a corner lane's corner index
+    const f3 ow = f3{L.root_pos[0], L.root_pos[1], L.root_pos[2]};  // points are about o; the terrain is world
     const bool isS = gt == HE_GEOM_SPHERE, isC = gt == HE_GEOM_CAPSULE, isB = !isS && !isC;
     float cd[kPts];
     f3 cxs[kPts], cns[kPts];
@@ -1629,7 +1627,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #pragma unroll
         for (int ci = 0; ci < kPts; ++ci) {
             const f3 x = ci == 0 ? X0 : P1;
-            cd[ci] = terrain_dist(ter, x, cns[ci]) - rt;
+            cd[ci] = terrain_dist(ter, ow + x, cns[ci]) - rt;
             cxs[ci] = x - cns[ci] * rt;
             cand[ci] = ci < npts && cd[ci] < off;
         }
@@ -1877,7 +1875,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const uint32_t anc0 = lane < nr ? T.anc_mask[L.cb0[ci]] : 0u;
             const uint32_t anc1 = (lane < nr && L.cb1[ci] >= 0) ? T.anc_mask[L.cb1[ci]] : 0u;
             const f3 dd = f3{dir[0], dir[1], dir[2]};
-            const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]} - o, dd);
+            const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]}, dd);  // contact points about o
             // bodies on some row's support (wave-uniform): the only ones whose dofs can be nonzero
             const uint32_t lb = wave_or(anc0 | anc1);
             // z = J_r^T and brow = J_r uf, four dofs per pinned group (their LDS reads overlap; the

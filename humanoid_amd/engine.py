@@ -210,6 +210,12 @@ class Engine:
         """f32 [N, HE_CACHE_WORDS]: the solver's warm-start cache (signature, keys, impulses)."""
         return self.buffer(_abi.BUF_CONTACT_CACHE)
 
+    @property
+    def initial_root_states(self):
+        """f32 [N,13]: _initial_humanoid_root_states (humanoid_phc.py:522-523), the root state the
+        Default / Hybrid state init resets to; writable."""
+        return self.buffer(_abi.BUF_INIT_ROOT_STATE)
+
     # ------------------------------------------------------------------ state writes
     def _contig(self, t, dtype=None):
         import torch

@@ -99,7 +99,7 @@ class EnvConfig:  # config.py:89-157
     kd_scale: float = 1.0
     log_interval: int = 32
     rew_power_coef: float = 0.0005
-    state_init: str = "Random"   # StateInit (config.py:114): Random, Start (Default / Hybrid raise)
+    state_init: str = "Random"   # StateInit (config.py:114): Default, Start, Random, Hybrid
     hybrid_init_prob: float = 0.5  # config.py:139 (Hybrid only)
     add_obs_noise: bool = False    # config.py:120-121, humanoid_phc.py:956
     obs_noise_std: float = 0.1
@@ -110,7 +110,7 @@ class EnvConfig:  # config.py:89-157
     # engine extensions (not in the reference config)
     seed: int = 0
     max_contacts: int = 20
-    solver_iterations: int = 8
+    solver_iterations: int = 4  # physx.num_position_iterations (isaacgym_env.py:17)
 
     @property
     def device(self) -> str:
@@ -151,13 +151,10 @@ class HumanoidPHC:
             raise ValueError("the engine runs on the GPU only (device_type='cuda')")
         cfg.robot.check()
         # _reset_actors (humanoid_phc.py:679-686): Random and Start sample the reference motion
-        # (_reset_ref_state_init); Default (the initial pose, no reference) and Hybrid (a Bernoulli
-        # mix of both) need a reset path that writes the initial state and the observation without a
-        # motion sample, which the engine does not have: they raise instead of resetting otherwise
-        if cfg.state_init in ("Default", "Hybrid"):
-            raise NotImplementedError(f"state_init={cfg.state_init!r} is not supported by the engine "
-                                      "(Random, the reference default, and Start are)")
-        if cfg.state_init not in ("Random", "Start"):
+        # (_reset_ref_state_init), Default resets to the initial pose (_reset_default), Hybrid mixes
+        # them by a Bernoulli(hybrid_init_prob) draw (_reset_hybrid_state_init); all four run in the
+        # engine's reset (he_reset_envs, and the device reset of he_env_step)
+        if cfg.state_init not in _abi.STATE_INIT:
             raise ValueError(f"Unsupported state initialization strategy: {cfg.state_init}")
         self.cfg = cfg
         self.device = torch.device(cfg.device)
@@ -229,10 +226,6 @@ class HumanoidPHC:
         self._load(sample_idxes=torch.from_numpy(idx))
 
     # -- parameters ----------------------------------------------------------------------
-    @property
-    def _start_at_zero(self):
-        """_sample_ref_state (humanoid_phc.py:848-855): motion time 0 for Start and in test mode."""
-        return self.cfg.state_init == "Start" or self.flag_test
 
     def _obs_noise(self, env_ids=None):
         """humanoid_phc.py:956-959: obs + N(0, obs_noise_std) while training (not in test mode), on the
@@ -257,7 +250,8 @@ class HumanoidPHC:
                                              enable_early_termination=self.cfg.enable_early_termination,
                                              eval_mode=self.flag_im_eval, termination_distance=self._term_dist,
                                              reset_body_ids=self._reset_bodies,
-                                             state_init_start=self._start_at_zero)
+                                             state_init=self.cfg.state_init,
+                                             hybrid_init_prob=self.cfg.hybrid_init_prob, test_mode=self.flag_test)
 
     def set_termination_distances(self, termination_distances):  # :1338-1339
         self._term_dist = termination_distances
@@ -285,10 +279,9 @@ class HumanoidPHC:
         import torch
         if len(env_ids) == 0:
             return
-        if self._start_at_zero:
-            phases = torch.zeros(len(env_ids), device=self.device)
-        else:
-            phases = torch.rand(len(env_ids), device=self.device, generator=self._gen)
+        # one uniform draw per env; the engine resolves it by the state init (Start / test mode: t = 0,
+        # Hybrid: the Bernoulli and the phase, include/humanoid_engine.h)
+        phases = torch.rand(len(env_ids), device=self.device, generator=self._gen)
         self.engine.reset_envs(self._params, self._em, env_ids.to(torch.int32), phases, self.obs_buf,
                                self._reset_u8, self._term_u8)
         self._obs_noise(env_ids)

@@ -117,10 +117,27 @@ typedef struct he_imitation_params {
     int32_t eval_mode;               /* flag_im_eval: mean-distance termination */
     int32_t reset_body_mask;         /* bit b set = body b in _reset_bodies_id */
     float term_dist[HE_NUM_BODIES];  /* _termination_distances */
-    int32_t state_init;              /* reset motion time (humanoid_phc.py:848-852): 0 Random =
-                                        sample_time_interval (config.py:114), 1 Start / test mode = 0 */
+    int32_t state_init;              /* StateInit (envs/state_init.py; config.py:114 default Random):
+                                        0 Default: the initial pose (humanoid_phc.py:688-692),
+                                        1 Start: the reference state at motion time 0,
+                                        2 Random: at sample_time_interval of the phase (:848-852),
+                                        3 Hybrid: Bernoulli(hybrid_init_prob) Random, else Default
+                                        (:733-745) */
+    float hybrid_init_prob;          /* config.py:139 */
+    int32_t test_mode;               /* flag_test: reference-state inits at motion time 0 (:855-856) */
     int32_t reserved;
 } he_imitation_params;
+
+/* StateInit values (envs/state_init.py) */
+#define HE_STATE_INIT_DEFAULT 0
+#define HE_STATE_INIT_START 1
+#define HE_STATE_INIT_RANDOM 2
+#define HE_STATE_INIT_HYBRID 3
+/* How a reset turns its uniform draw u in [0,1) (he_reset_envs' `phases`, or the device reset's
+ * hash) into the state init, identically in the kernels and the oracle: Default -> the initial
+ * pose; Start -> reference at t = 0; Random -> reference at sample_time_interval(u); Hybrid -> the
+ * reference at sample_time_interval(u / p) when u < p = hybrid_init_prob (u / p is uniform given
+ * the draw), else the initial pose; test_mode puts every reference init at t = 0. */
 
 /* Buffer kinds (humanoid_phc.py:497-554, the tensors gymtorch.wrap_tensor exposed). */
 typedef enum he_buf_kind {
@@ -133,7 +150,11 @@ typedef enum he_buf_kind {
     HE_BUF_NUM_CONTACTS = 6,   /* i32 [N]     contact slots used last substep (limits included) */
     HE_BUF_DROPPED_CONTACTS = 7, /* i32 [N]   contacts generated past the capacity, last substep */
     HE_BUF_CONTACT_CACHE = 8,  /* f32 [N,HE_CACHE_WORDS] solver warm-start cache (see above) */
-    HE_BUF_COUNT = 9
+    HE_BUF_INIT_ROOT_STATE = 9, /* f32 [N,13] _initial_humanoid_root_states (humanoid_phc.py:522-523):
+                                  the creation poses with zero velocities, set by he_create_envs;
+                                  writable (the facade copies the root states after prepare_sim);
+                                  the Default / Hybrid state init resets to it */
+    HE_BUF_COUNT = 10
 } he_buf_kind;
 
 #define HE_DTYPE_F32 1   /* GymTensor.h:23 eGymDataTypeFp32 */
@@ -240,11 +261,14 @@ int he_motion_state(he_engine* h, int k, const int64_t* ids, const float* times,
                     float* rg_pos, float* rb_rot, float* body_vel, float* body_ang_vel,
                     float* dof_pos, float* dof_vel, void* stream);
 
-/* _reset_ref_state_init + _reset_env_tensors + _compute_observations(env_ids)
- * (humanoid_phc.py:694-731, 747-780, 937-961): for env ids [k] (int32), motion time
- * t = floor(phase*len/(1/30))*(1/30) (motion_lib.py:526-535) with `phases` f32 [k] uniform [0,1);
- * writes root/dof/rigid-body state, dof targets := dof_pos, zero contact forces, progress = 0,
- * start_times = t, start_offsets = 0, global_offset = 0, and the k obs rows. */
+/* _reset_actors + _reset_env_tensors + _compute_observations(env_ids) (humanoid_phc.py:665-692,
+ * 694-745, 747-780, 937-961) for env ids [k] (int32), with `phases` f32 [k] uniform [0,1) resolved
+ * by p->state_init (above). A reference-state init: motion time t = floor(phase*len/(1/30))*(1/30)
+ * (motion_lib.py:526-535); writes root/dof/rigid-body state, dof targets := dof_pos, zero contact
+ * forces, progress = 0, start_times = t, start_offsets = 0, global_offset = 0. A Default init
+ * (_reset_default): root := HE_BUF_INIT_ROOT_STATE row, dof pos / vel / targets := 0, the
+ * rigid-body rows of that pose (zero velocities), zero contact forces, progress = 0, the motion
+ * bookkeeping left as it was (the reference does not touch it). Then the k obs rows. */
 int he_reset_envs(he_engine* h, const he_imitation_params* p, const he_env_motion* em,
                   const int32_t* env_ids, int k, const float* phases, float* obs, uint8_t* reset,
                   uint8_t* terminate, void* stream);

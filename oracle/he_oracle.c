@@ -392,10 +392,77 @@ void ho_imitation_step(const he_imitation_params* p, const ho_motion* M, int n, 
 }
 
 /* humanoid_phc.py:694-731 + 747-780 + 901-931 + obs for the reset envs */
-static void reset_env(const he_imitation_params* p, const ho_motion* M, int e, float phase, const int64_t* motion_ids,
+/* The state init of a reset from its uniform draw u (include/humanoid_engine.h, the StateInit
+ * block): 1 = a reference-state init at phase *ph (humanoid_phc.py:694-731, 848-856), 0 = the
+ * initial pose (_reset_default, :688-692); Hybrid = Bernoulli(hybrid_init_prob) of the two
+ * (:733-745), its phase u / p uniform given the draw. float32 as the kernels. */
+static int resolve_init(const he_imitation_params* p, float u, float* ph) {
+    int ref = p->state_init != HE_STATE_INIT_DEFAULT;
+    *ph = u;
+    if (p->state_init == HE_STATE_INIT_HYBRID) {
+        ref = u < p->hybrid_init_prob;
+        *ph = ref ? u / p->hybrid_init_prob : 0.0f;
+    }
+    if (p->state_init == HE_STATE_INIT_START || p->test_mode) *ph = 0.0f;
+    return ref;
+}
+
+/* _reset_default + _reset_env_tensors (humanoid_phc.py:688-692, 747-780): the initial root state,
+ * zero dof state and targets, the zero pose's rigid-body rows (every local rotation the identity:
+ * body origin = root + R_root rest[b], the root's rotation and velocities), zero contact forces,
+ * progress 0; the motion bookkeeping is left as it is (the reference does not touch it). */
+static void default_reset(const he_imitation_params* p, const ho_motion* M, int e, const int64_t* motion_ids,
+                          const float* start_times, const float* start_offsets, const float* global_offset,
+                          int16_t* progress, float* root_states, float* dof_state, float* dof_targets, float* rb_state,
+                          float* contact_forces, float* obs, uint8_t* reset, uint8_t* terminate, const float* init_root,
+                          const float* rest_pos) {
+    const float* ir = init_root + (size_t)e * 13;
+    float* rs = root_states + (size_t)e * 13;
+    for (int c = 0; c < 13; ++c) rs[c] = ir[c];
+    for (int d = 0; d < ND; ++d) {
+        dof_state[((size_t)e * ND + d) * 2 + 0] = 0.0f;
+        dof_state[((size_t)e * ND + d) * 2 + 1] = 0.0f;
+        if (dof_targets) dof_targets[(size_t)e * ND + d] = 0.0f;
+    }
+    R q[4] = {ir[3], ir[4], ir[5], ir[6]}, w[3] = {ir[10], ir[11], ir[12]};
+    float* rb = rb_state + (size_t)e * NB * 13;
+    for (int j = 0; j < NB; ++j) {
+        R lo[3] = {rest_pos[3 * j], rest_pos[3 * j + 1], rest_pos[3 * j + 2]}, ro[3], wx[3];
+        q_rot(q, lo, ro);
+        v3_cross(w, ro, wx);
+        for (int c = 0; c < 3; ++c) {
+            rb[j * 13 + c] = (float)(ir[c] + ro[c]);
+            rb[j * 13 + 7 + c] = (float)(ir[7 + c] + wx[c]);
+            rb[j * 13 + 10 + c] = ir[10 + c];
+        }
+        for (int c = 0; c < 4; ++c) rb[j * 13 + 3 + c] = ir[3 + c];
+        if (contact_forces) for (int c = 0; c < 3; ++c) contact_forces[((size_t)e * NB + j) * 3 + c] = 0.0f;
+    }
+    progress[e] = 0;
+    if (reset) reset[e] = 0;
+    if (terminate) terminate[e] = 0;
+    if (obs) {  /* the observation against the env's (unchanged) motion at t(progress 1) */
+        int64_t mid = motion_ids[e];
+        sim_body s;
+        load_rb(rb, &s);
+        float t2 = env_time(1, p->control_dt, start_times[e], start_offsets[e]);
+        mstate m2;
+        motion_eval(M, mid, t2, global_offset + 3 * e, 0, &m2);
+        self_obs(&s, obs + (size_t)e * HE_OBS_DIM);
+        task_obs(&s, &m2, obs + (size_t)e * HE_OBS_DIM + HE_OBS_SELF);
+    }
+}
+
+static void reset_env(const he_imitation_params* p, const ho_motion* M, int e, float u, const int64_t* motion_ids,
                       float* start_times, float* start_offsets, float* global_offset, int16_t* progress,
                       float* root_states, float* dof_state, float* dof_targets, float* rb_state, float* contact_forces,
-                      float* obs, uint8_t* reset, uint8_t* terminate) {
+                      float* obs, uint8_t* reset, uint8_t* terminate, const float* init_root, const float* rest_pos) {
+    float phase;
+    if (!resolve_init(p, u, &phase)) {
+        default_reset(p, M, e, motion_ids, start_times, start_offsets, global_offset, progress, root_states, dof_state,
+                      dof_targets, rb_state, contact_forces, obs, reset, terminate, init_root, rest_pos);
+        return;
+    }
     int64_t mid = motion_ids[e];
     float t = ho_sample_time_interval(phase, M->lengths[mid]);
     mstate m;
@@ -434,11 +501,13 @@ static void reset_env(const he_imitation_params* p, const ho_motion* M, int e, f
 void ho_reset_envs(const he_imitation_params* p, const ho_motion* M, int k, const int32_t* env_ids, const float* phases,
                    const int64_t* motion_ids, float* start_times, float* start_offsets, float* global_offset,
                    int16_t* progress, float* root_states, float* dof_state, float* dof_targets, float* rb_state,
-                   float* contact_forces, float* obs, uint8_t* reset, uint8_t* terminate) {
+                   float* contact_forces, float* obs, uint8_t* reset, uint8_t* terminate, const float* init_root,
+                   const float* rest_pos) {
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < k; ++i)
         reset_env(p, M, env_ids[i], phases[i], motion_ids, start_times, start_offsets, global_offset, progress,
-                  root_states, dof_state, dof_targets, rb_state, contact_forces, obs, reset, terminate);
+                  root_states, dof_state, dof_targets, rb_state, contact_forces, obs, reset, terminate, init_root,
+                  rest_pos);
 }
 
 /* counter-based uniform in [0,1) shared by engine and oracle (splitmix64 finaliser) */

@@ -118,17 +118,33 @@ def imitation_step(params, mt: MotionTables, rb_state, dof_vel, dof_force, progr
     return out
 
 
-def reset_envs(params, mt: MotionTables, env_ids, phases, motion_ids, state):
+def rest_positions(model):
+    """[24,3] body origins of the zero pose in the root frame (the joint offsets summed along each
+    chain): the Default state init's rigid-body rows (he_engine.cpp he_set_model)."""
+    rest = np.zeros((24, 3), np.float32)
+    for b in range(1, 24):
+        rest[b] = rest[model.parents[b]] + np.asarray(model.local_pos[b], np.float32)
+    return rest
+
+
+def reset_envs(params, mt: MotionTables, env_ids, phases, motion_ids, state, rest_pos=None):
     """state: dict of numpy arrays (modified in place): start_times, start_offsets, global_offset, progress,
     root_states [N,13], dof_state [N,69,2], dof_targets [N,69], rb_state [N,24,13], contact_forces [N,24,3],
-    obs [N,934], reset [N] u8, terminate [N] u8."""
+    obs [N,934], reset [N] u8, terminate [N] u8, and for the Default / Hybrid state init init_root [N,13]
+    (with rest_pos [24,3], rest_positions(model)). `phases` are the resets' uniform draws, resolved by
+    params.state_init as in the engine."""
     ids = np.ascontiguousarray(env_ids, np.int32)
     names = ("start_times", "start_offsets", "global_offset", "progress", "root_states", "dof_state", "dof_targets",
              "rb_state", "contact_forces", "obs", "reset", "terminate")
     for n in names:
         assert state[n].flags.c_contiguous
+    init_root = state.get("init_root")
+    if params.state_init in (0, 3) and (init_root is None or rest_pos is None):
+        raise ValueError("the Default / Hybrid state init needs state['init_root'] and rest_pos")
+    ir = None if init_root is None else f32(init_root)
+    rp = None if rest_pos is None else f32(rest_pos)
     lib().ho_reset_envs(C.byref(params), C.byref(mt.struct), C.c_int(len(ids)), _p(ids), _p(f32(phases)),
-                        _p(np.ascontiguousarray(motion_ids, np.int64)), *[_p(state[n]) for n in names])
+                        _p(np.ascontiguousarray(motion_ids, np.int64)), *[_p(state[n]) for n in names], _p(ir), _p(rp))
     return state
 
 

@@ -118,3 +118,14 @@ def assert_expmap_close(got, ref):
     bad = np.abs(np.asarray(got) - np.asarray(ref)) > tol
     assert not bad.any(), (f"{bad.sum()} exp-map coordinates out of tolerance: got {np.asarray(got)[bad][:4]} "
                            f"ref {np.asarray(ref)[bad][:4]} tol {tol[bad][:4]}")
+
+
+def rounding_noise(root, dof, seed):
+    """In place: the fp32 engine's rounding, modelled for the oracle's sensitivity probes
+    (test_gpu_parity._cond_close): joint angles + 1e-6 rad N(0, 1), joint and root velocities
+    x (1 + 1e-6 N(0, 1)) -- a few fp32 ulps of each, drawn afresh in every policy step, since the
+    engine rounds in every step (its velocity solve through a stiff factor most of all)."""
+    rng = np.random.default_rng(seed)
+    dof[..., 0] += (1e-6 * rng.standard_normal(dof[..., 0].shape)).astype(np.float32)
+    dof[..., 1] *= (1.0 + 1e-6 * rng.standard_normal(dof[..., 1].shape)).astype(np.float32)
+    root[:, 7:13] *= (1.0 + 1e-6 * rng.standard_normal(root[:, 7:13].shape)).astype(np.float32)

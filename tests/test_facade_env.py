@@ -237,19 +237,44 @@ def test_puffer_env_amp_obs(model):
 
 # ------------------------------------------------------------- config branches (A11 mirror)
 def test_env_config_branches_raise_before_the_gpu():
-    """state_init Default / Hybrid and the obs / robot options the fused kernels do not implement
-    raise (NotImplementedError), unknown values raise as the reference does (ValueError,
-    humanoid_phc.py:679-686) -- before any GPU work, so this runs on the CPU."""
+    """The obs / robot options the fused kernels do not implement raise (NotImplementedError), an
+    unknown state_init raises as the reference does (ValueError, humanoid_phc.py:679-686) -- before
+    any GPU work, so this runs on the CPU. (All four StateInit values are implemented.)"""
     from humanoid_amd.env import EnvConfig, HumanoidPHC, RobotConfig
-    for si in ("Default", "Hybrid"):
-        with pytest.raises(NotImplementedError, match="state_init"):
-            HumanoidPHC(EnvConfig(num_envs=4, state_init=si))
+    from humanoid_amd import _abi
+    assert set(_abi.STATE_INIT) == {"Default", "Start", "Random", "Hybrid"}
     with pytest.raises(ValueError, match="Unsupported state initialization"):
         HumanoidPHC(EnvConfig(num_envs=4, state_init="Middle"))
     for kw in (dict(has_upright_start=False), dict(has_shape_obs=True), dict(reduce_action=True), dict(has_mesh=True)):
         with pytest.raises(NotImplementedError, match="RobotConfig"):
             HumanoidPHC(EnvConfig(num_envs=4, robot=RobotConfig(**kw)))
     RobotConfig(has_smpl_pd_offset=True).check()  # supported (pd_action_offset_scale)
+
+
+@pytest.mark.gpu
+def test_state_init_default_through_the_env(model):
+    """state_init=Default through HumanoidPHC / PHCPufferEnv: the full reset puts every env at its
+    creation pose with zero dofs (humanoid_phc.py:688-692) and the motion start times stay at their
+    loaded values; under random actions the fused device resets bring failed envs back there."""
+    from humanoid_amd.env import EnvConfig, PHCPufferEnv
+    n = 32
+    pe = PHCPufferEnv(EnvConfig(num_envs=n, motion_file=_clip_dict(model), seed=5, state_init="Default"))
+    pe.reset()
+    e = pe.env
+    init = e.engine.initial_root_states.clone()
+    assert (e.engine.root_states == init).all()
+    assert (e.engine.dof_state == 0).all()
+    rng = np.random.default_rng(2)
+    resets = 0
+    for _ in range(20):
+        pe.step(rng.uniform(-1, 1, (n, 69)).astype(np.float32))
+        r = e.reset_buf.clone()
+        resets += int(r.sum())
+        if r.any():
+            assert (e.engine.root_states[r] == init[r]).all()
+            assert (e.engine.dof_state.view(n, 69, 2)[r] == 0).all()
+    assert resets > 0
+    pe.close()
 
 
 @pytest.mark.gpu

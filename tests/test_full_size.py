@@ -66,7 +66,7 @@ def test_full_size_standstill_invariant(model):
 
 @pytest.mark.parametrize("config", ["standstill", "imitation", "dr"])
 def test_full_size_sample_matches_oracle(model, he_model, config):
-    import cases  # noqa: F401  (tests/ on the path)
+    import cases  # tests/ on the path
     from humanoid_amd import _abi
     ro = _rollout(config, model)
     for _ in range(5):
@@ -86,7 +86,7 @@ def test_full_size_sample_matches_oracle(model, he_model, config):
     probes = []
     for seed in (123, 124, 125):  # the oracle's own sensitivity (see _cond_close)
         r_s, d_s = root.copy(), dof.copy()
-        d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
+        cases.rounding_noise(r_s, d_s, seed)
         O.physics_step(he_model, sp, r_s, d_s, tgt, 2, cache=cache.copy(), **props)
         probes.append((r_s, d_s))
     c_o = cache.copy()
@@ -124,11 +124,7 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     c_o = ro.eng.contact_cache.cpu().numpy()[idx].copy()
     props = _props(ro, idx)
     sp = _abi.default_sim_params(max_contacts=20, terrain=1)
-    probes = []
-    for seed in (123, 124, 125):
-        d_s = dof.copy()
-        d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
-        probes.append([root.copy(), d_s, c_o.copy(), None])
+    probes = [[root.copy(), dof.copy(), c_o.copy(), None] for _ in range(3)]
     zero = torch.zeros_like(ro.actions)
     mism = np.zeros(len(idx), bool)
     st = CondStats()
@@ -138,9 +134,7 @@ def test_full_size_dr_sample_30_steps(model, he_model):
         tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
         out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o, **props)
         for k, pr in enumerate(probes):
-            if step > 0:  # rounding-level noise in every step, as the fp32 engine rounds in every step
-                pr[1][:, :, 0] += (1e-6 * np.random.default_rng(1000 * k + step).standard_normal(
-                    pr[1][:, :, 0].shape)).astype(np.float32)
+            cases.rounding_noise(pr[0], pr[1], 123 + 1000 * k + step)  # fp32-level noise in every step
             pr[3] = O.physics_step(he_model, sp, pr[0], pr[1], tgt, 2, cache=pr[2], **props)
         torch.cuda.synchronize()
         mism |= np.array([a != b for a, b in zip(contact_keys(ro.eng.contact_cache.cpu().numpy()[idx]),

@@ -190,6 +190,138 @@ def test_reset_envs_matches_golden(he_model, golden):
     assert (reset.cpu().numpy()[I] == 0).all()
 
 
+def _state_init_case(he_model, model, golden, n=24):
+    """An engine over the env_step golden motions, the envs advanced 3 policy steps under random
+    actions, and the oracle state dict mirroring the engine's (init_root included)."""
+    from humanoid_amd.model import pd_action_offset_scale
+    g = golden("env_step")
+    eng = make_engine(he_model, n)
+    tables = tables_from_golden(g)
+    eng.load_motions(tables)
+    off, sc = pd_action_offset_scale(model)
+    eng.set_pd_params(off, sc, None)
+    rng = np.random.default_rng(40)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    eng.root_states.copy_(cu(root))
+    # the initial root states as the reference keeps them: the creation pose, zero velocity
+    init = root.copy()
+    init[:, 7:] = 0.0
+    eng.initial_root_states.copy_(cu(init))
+    st = cu(g["start_times"]); so = torch.zeros(n, device="cuda:0"); go = cu(g["global_offset"])
+    prog = torch.zeros(n, dtype=torch.int16, device="cuda:0")
+    em = eng.env_motion(torch.arange(n, device="cuda:0"), st, so, go, prog)
+    for _ in range(3):
+        eng.step_actions(cu(rng.uniform(-0.3, 0.3, (n, 69)).astype(np.float32)), 2)
+    torch.cuda.synchronize()
+    return eng, em, (st, so, go, prog), O.MotionTables.from_tables(tables), init
+
+
+def _oracle_state(eng, bk, n, init):
+    st, so, go, prog = bk
+    return dict(start_times=st.cpu().numpy().copy(), start_offsets=so.cpu().numpy().copy(),
+                global_offset=go.cpu().numpy().copy(), progress=prog.cpu().numpy().copy(),
+                root_states=eng.root_states.cpu().numpy().copy(), dof_state=eng.dof_state.view(n, 69, 2).cpu().numpy().copy(),
+                dof_targets=eng.dof_targets.cpu().numpy().copy(), rb_state=eng.rb_state.view(n, 24, 13).cpu().numpy().copy(),
+                contact_forces=eng.contact_forces.view(n, 24, 3).cpu().numpy().copy(),
+                obs=np.zeros((n, 934), np.float32), reset=np.zeros(n, np.uint8), terminate=np.zeros(n, np.uint8),
+                init_root=init)
+
+
+def _assert_reset_rows(eng, bk, st_o, ids, n, obs):
+    st, so, go, prog = bk
+    rs = eng.root_states.cpu().numpy()[ids]
+    np.testing.assert_allclose(rs[:, :3], st_o["root_states"][ids, :3], atol=2e-6)
+    quat_close(rs[:, 3:7], st_o["root_states"][ids, 3:7], 5e-6)
+    np.testing.assert_allclose(rs[:, 7:], st_o["root_states"][ids, 7:], atol=1e-5)
+    ds = eng.dof_state.view(n, 69, 2).cpu().numpy()[ids]
+    cases.assert_expmap_close(ds[..., 0], st_o["dof_state"][ids, :, 0])
+    np.testing.assert_allclose(ds[..., 1], st_o["dof_state"][ids, :, 1], atol=1e-5)
+    cases.assert_expmap_close(eng.dof_targets.cpu().numpy()[ids], st_o["dof_targets"][ids])
+    rb = eng.rb_state.view(n, 24, 13).cpu().numpy()[ids]
+    np.testing.assert_allclose(rb[..., :3], st_o["rb_state"][ids, :, :3], atol=2e-6)
+    quat_close(rb[..., 3:7], st_o["rb_state"][ids, :, 3:7], 5e-6)
+    np.testing.assert_allclose(rb[..., 7:], st_o["rb_state"][ids, :, 7:], atol=1e-5)
+    np.testing.assert_array_equal(st.cpu().numpy(), st_o["start_times"])
+    np.testing.assert_array_equal(so.cpu().numpy(), st_o["start_offsets"])
+    np.testing.assert_array_equal(go.cpu().numpy(), st_o["global_offset"])
+    np.testing.assert_array_equal(prog.cpu().numpy()[ids], 0)
+    assert (eng.contact_forces.view(n, 24, 3).cpu().numpy()[ids] == 0).all()
+    og, oo = obs.cpu().numpy()[ids], st_o["obs"][ids]
+    np.testing.assert_allclose(og, oo, atol=5e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("state_init", ["Default", "Hybrid"])
+def test_state_init_default_and_hybrid_match_oracle(he_model, model, golden, state_init):
+    """StateInit.Default and .Hybrid (humanoid_phc.py:679-692, 733-745; config.py:114, 139) through
+    he_reset_envs after 3 policy steps: Default writes the initial root state, zero dofs and targets,
+    the zero pose's body rows and leaves the motion bookkeeping; Hybrid splits the envs by the draw
+    u < hybrid_init_prob (reference init at phase u / p, else Default). Against the oracle's reset from
+    the engine's own pre-reset state; both kinds occur in the Hybrid case."""
+    n = 24
+    eng, em, bk, mt, init = _state_init_case(he_model, model, golden, n)
+    p = _abi.imitation_params(state_init=state_init, hybrid_init_prob=0.5)
+    st_o = _oracle_state(eng, bk, n, init)
+    ids = np.arange(0, n, 2).astype(np.int32)
+    u = np.random.default_rng(41).uniform(0, 1, len(ids)).astype(np.float32)
+    obs = torch.zeros(n, 934, device="cuda:0")
+    reset = torch.ones(n, dtype=torch.uint8, device="cuda:0")
+    term = torch.ones(n, dtype=torch.uint8, device="cuda:0")
+    eng.reset_envs(p, em, cu(ids, torch.int32), cu(u), obs, reset, term)
+    O.reset_envs(p, mt, ids, u, np.arange(n), st_o, rest_pos=O.rest_positions(model))
+    torch.cuda.synchronize()
+    _assert_reset_rows(eng, bk, st_o, ids, n, obs)
+    dflt = ids[u >= 0.5] if state_init == "Hybrid" else ids
+    assert len(dflt) > 0
+    np.testing.assert_array_equal(eng.dof_state.view(n, 69, 2).cpu().numpy()[dflt], 0.0)
+    if state_init == "Hybrid":
+        assert 0 < len(dflt) < len(ids), "both kinds of reset must occur"
+
+
+def test_state_init_hybrid_device_reset_matches_oracle(he_model, model, golden):
+    """The device reset of he_imitation_reset_step (the env step's) under StateInit.Hybrid: the draw
+    is the splitmix hash of (seed, step, env), resolved as in he_reset_envs. Envs are made to fail
+    (bodies thrown off their reference), their reset rows checked against the oracle's reset with
+    the same draws; AMP history rows of Default-reset envs equal their current row
+    (_init_amp_obs_default, humanoid_phc.py:801-803)."""
+    n = 24
+    eng, em, bk, mt, init = _state_init_case(he_model, model, golden, n)
+    S = 4
+    amp = torch.zeros(n, S, 196, device="cuda:0")
+    demo = torch.zeros(n, S, 196, device="cuda:0")
+    eng.set_amp(amp, demo)
+    p = _abi.imitation_params(state_init="Hybrid", hybrid_init_prob=0.5)
+    # every env far from its reference: all terminate (progress > 1) and reset
+    bk[3].fill_(5)
+    eng.root_states[:, 2] += 1.0
+    eng.simulate(1)
+    torch.cuda.synchronize()
+    rb = eng.rb_state.view(n, 24, 13).cpu().numpy().copy()
+    st_o = _oracle_state(eng, bk, n, init)
+    im = O.imitation_step(p, mt, rb, st_o["dof_state"][..., 1], eng.dof_force.view(n, 69).cpu().numpy(),
+                          st_o["progress"], np.arange(n), st_o["start_times"], st_o["start_offsets"],
+                          st_o["global_offset"])
+    obs = torch.zeros(n, 934, device="cuda:0"); rew = torch.zeros(n, device="cuda:0")
+    raw = torch.zeros(n, 5, device="cuda:0")
+    reset = torch.zeros(n, dtype=torch.uint8, device="cuda:0"); term = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    seed, step = 99, 3
+    eng.imitation_reset_step(p, em, obs, rew, raw, reset, term, seed=seed, step_index=step)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(reset.cpu().numpy(), im["reset"])
+    ids = np.nonzero(im["reset"])[0].astype(np.int32)
+    assert len(ids) == n
+    st_o["progress"] = im["progress"]
+    u = np.array([O.hash_uniform(seed, step, int(e)) for e in ids], np.float32)
+    O.reset_envs(p, mt, ids, u, np.arange(n), st_o, rest_pos=O.rest_positions(model))
+    _assert_reset_rows(eng, bk, st_o, ids, n, obs)
+    dflt = ids[u >= 0.5]
+    ref = ids[u < 0.5]
+    assert len(dflt) > 0 and len(ref) > 0
+    a = amp.cpu().numpy()
+    for k in range(1, S):  # Default: the history is the current row
+        np.testing.assert_array_equal(a[dflt, k], a[dflt, 0])
+    assert not np.allclose(a[ref, 1], a[ref, 0])  # reference inits: rows from the motion
+
+
 class CondStats:
     """Counts the elements whose tolerance was widened (see _cond_close) over a whole test."""
 
@@ -255,8 +387,8 @@ def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-
                      max_widened=0.05, env_props=None, **sim):
     """Engine vs oracle for `steps` policy steps (`calls` gym.simulate() each) from the same state,
     both warm-starting from their own caches. The oracle's sensitivity probes (_cond_close) carry
-    rounding-level noise into every policy step (1e-6 rad on the joint angles, fresh each step), as
-    the fp32 engine rounds in every step, not only at the start. Envs whose contact SETS (keys: body, partner, candidate) ever differ are excluded
+    rounding-level noise (cases.rounding_noise) into every policy step, as the fp32 engine rounds in
+    every step, not only at the start. Envs whose contact SETS (keys: body, partner, candidate) ever differ are excluded
     (a point within rounding of the 0.02 m offset, or a tie in the deepest-first reduction), at most
     `max_skip` of them; at most `max_widened` of the compared elements may need the sensitivity
     widening (_cond_close)."""
@@ -273,20 +405,14 @@ def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-
     eng.dof_targets.copy_(cu(targets))
     r_o, d_o, c_o = root.copy(), dof.copy(), O.new_cache(n)
     # sensitivity probes: joint angles moved by 1e-6 rad (three independent draws)
-    probes = []
-    for seed in (123, 124, 125):
-        r_s, d_s = root.copy(), dof.copy()
-        d_s[:, :, 0] += (1e-6 * np.random.default_rng(seed).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
-        probes.append([r_s, d_s, None, O.new_cache(n)])
+    probes = [[root.copy(), dof.copy(), None, O.new_cache(n)] for _ in range(3)]
     sp = _abi.default_sim_params(**sim)
     mismatch = np.zeros(n, bool)
     for step in range(steps):
         eng.simulate(calls)
         out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, calls, cache=c_o, **props)
         for k, pr in enumerate(probes):
-            if step > 0:  # step 0's perturbation is the initial one above
-                noise = np.random.default_rng(1000 * k + step).standard_normal(pr[1][:, :, 0].shape)
-                pr[1][:, :, 0] += (1e-6 * noise).astype(np.float32)
+            cases.rounding_noise(pr[0], pr[1], 123 + 1000 * k + step)
             pr[2] = O.physics_step(eng.he_model, sp, pr[0], pr[1], targets, calls, cache=pr[3], **props)
         torch.cuda.synchronize()
         kg = contact_keys(eng.contact_cache.cpu().numpy())
@@ -479,7 +605,7 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
         probes = []
         for k in range(3):  # oracle sensitivity probes (see _cond_close)
             r_s, d_s = r_pre.copy(), d_pre.copy()
-            d_s[:, :, 0] += (1e-6 * np.random.default_rng(100 * step + k).standard_normal(d_s[:, :, 0].shape)).astype(np.float32)
+            cases.rounding_noise(r_s, d_s, 100 * step + k)
             O.physics_step(eng.he_model, sp, r_s, d_s, tgt.astype(np.float32), 2, cache=c_pre.copy())
             probes.append((r_s, d_s))
         c_o = c_pre.copy()
@@ -721,4 +847,4 @@ def test_saturated_random_actions_stay_physical_on_gpu(he_model, model):
     assert vmax.max() < 15.0, vmax.max()
     assert int((vmax > 10).sum()) <= n // 1000, int((vmax > 10).sum())
     assert np.median(ke) < 1.5e3
-    assert q.max() < np.pi - 0.01
+    assert q.max() <= np.pi - 0.01 + 1e-5  # the limit backstop's cap (limit_clamp) at most

@@ -250,6 +250,6 @@ def test_saturated_random_actions_stay_physical(he_model, model):
     q = np.linalg.norm(dof[..., 0].reshape(n, 23, 3), axis=-1)
     assert vmax.max() < 10.0, vmax.max()
     assert np.median(ke) < 1.5e3, np.median(ke)
-    assert q.max() < np.pi - 0.01
+    assert q.max() <= np.pi - 0.01 + 1e-5  # the limit backstop's cap at most
     vexp, _, _ = _random_action_run(he_model, model, 1.0, 32, 60, bias_midpoint=0)
     assert (vexp > 10.0).sum() > 8, vexp  # the explicit scheme's runaway in the same run
