@@ -105,7 +105,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.max_depenetration_velocity = 10.0
     p.angular_damping = 0.01
     p.max_angular_velocity = 100.0
-    p.solver_iterations = 4  # physx.num_position_iterations (isaacgym_env.py:17)
+    p.solver_iterations = 8  # PGS sweeps per physics step (4 leave 100x the one-step deviation)
     p.self_collision = 1
     p.max_contacts = 20
     p.kp_scale = 1.0

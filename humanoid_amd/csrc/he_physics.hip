@@ -106,6 +106,12 @@ struct Lds {
 #ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
 #define HE_PRED_LEVELS 0
 #endif
+#ifndef HE_PRED_LT_GROUPS  // the midpoint bias's L^-T pass in groups of independent pivots (1) or one by one (0)
+#define HE_PRED_LT_GROUPS 1
+#endif
+#ifndef HE_PRED_JUMP  // the midpoint bias's velocities / accelerations by pointer jumping (1) or chain walks (0)
+#define HE_PRED_JUMP 1
+#endif
 #ifndef HE_BIAS_PREDICTOR  // 0: the midpoint bias compiled out (diagnostic A/B of its code's cost when off)
 #define HE_BIAS_PREDICTOR 1
 #endif
@@ -1210,6 +1216,62 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
     STAMP(25);
     const bool bl = lane < NB;
     const int b = bl ? lane : 0;
+#if HE_PRED_JUMP
+    // velocities and bias accelerations at um by pointer jumping over the chain, as the kinematics
+    // does at u0 (the jump table stops below the root; the root's velocity and base acceleration are
+    // added once at the end): no LDS chain walks
+    float Fb[6];
+    {
+        const uint32_t jp = bl ? T.jump4[b] : 0xFFFFFFFFu;
+        float vj[6];  // the joint's own velocity S_b um_b (the root's S are the unit axes)
+        if (b == 0) {
+            for (int x = 0; x < 6; ++x) vj[x] = L.uf[x];
+        } else {
+            const int d0 = T.dof0[b];
+            const float u0_ = L.uf[d0], u1_ = L.uf[d0 + 1], u2_ = L.uf[d0 + 2];
+            for (int x = 0; x < 6; ++x) vj[x] = L.S[d0][x] * u0_ + L.S[d0 + 1][x] * u1_ + L.S[d0 + 2][x] * u2_;
+        }
+        float V[6];
+        for (int x = 0; x < 6; ++x) V[x] = vj[x];
+        auto prefix6 = [&](float (&y)[6]) {
+            auto round = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                const int j = jump_of<K>(jp);
+                const int src = j < 0 ? lane : j;
+                float ya[6];
+#pragma unroll
+                for (int x = 0; x < 6; ++x) ya[x] = __shfl(y[x], src, W);
+                if (j >= 0)
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) y[x] += ya[x];
+            };
+            round(std::integral_constant<int, 0>{});
+            round(std::integral_constant<int, 1>{});
+            round(std::integral_constant<int, 2>{});
+            if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
+        };
+        prefix6(V);
+        const float um6[6] = {L.uf[0], L.uf[1], L.uf[2], L.uf[3], L.uf[4], L.uf[5]};
+        if (HE_KIN_ROOTREL && b != 0)
+            for (int x = 0; x < 6; ++x) V[x] += um6[x];
+        const f3 vxw = cross3(f3{um6[3], um6[4], um6[5]}, f3{um6[0], um6[1], um6[2]});
+        const float A0[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
+        float A[6];
+        if (b == 0) {
+            for (int x = 0; x < 6; ++x) A[x] = A0[x];
+        } else {
+            crm(V, vj, A);  // joint b's velocity-product term V_b x S_b um_b
+        }
+        prefix6(A);
+        if (HE_KIN_ROOTREL && b != 0)
+            for (int x = 0; x < 6; ++x) A[x] += A0[x];
+        float IA[6], IV[6], X[6];
+        si_apply(L.Ib[b], A, IA);
+        si_apply(L.Ib[b], V, IV);
+        crf(V, IV, X);
+        for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
+    }
+#else
     if (bl) {  // joint velocities S_b uf_b (the root's S are the unit axes) -> Acc
         float vj[6];
         if (b == 0) {
@@ -1247,6 +1309,7 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
         crf(V, IV, X);
         for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
     }
+#endif
     sync();
     if (bl)
         for (int x = 0; x < 6; ++x) L.Acc[b][x] = Fb[x];
@@ -1276,7 +1339,11 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
     float c1 = corr(lane);
     float c2 = lane < NH ? corr(64 + lane) : 0.f;
     STAMP(27);
+#if HE_PRED_LT_GROUPS
+    regla::solve_LT_vec_groups<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+#else
     regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+#endif
     L.yh[lane] += c1 * L.sDinv[lane];
     if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
     sync();
@@ -2102,6 +2169,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         for (int i = lane; i < NG; i += W)
             if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
         sync();
+        // plus the joint-limit force (dof_force = the joint's solver force, drive and limit together;
+        // oracle/he_oracle_physics.c): limit slot c (one per joint) adds g lambda / dt over its joint's
+        // dofs, g = its row (kept in the contact-position words)
+        const int nl = __builtin_amdgcn_readfirstlane(L.nlim);
+        if (lane < nl && nc > 0) {
+            const int d0 = 3 * (L.cb0[lane] - 1);
+            const float lf = L.lam[3 * lane] / dt;
+            L.dforce[d0] += L.cx[lane][0] * lf;
+            L.dforce[d0 + 1] += L.cx[lane][1] * lf;
+            L.dforce[d0 + 2] += L.cx[lane][2] * lf;
+        }
+        sync();
     }
     // damping, the angular-velocity clamps and the semi-implicit position update in one pass per
     // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
@@ -2123,24 +2202,33 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // are then re-derived, u_b = R_b^T (w'_b - w'_parent) (oracle: the same pass)
         const f4 qb = bl ? f4{L.qw[lane][0], L.qw[lane][1], L.qw[lane][2], L.qw[lane][3]} : f4{0.f, 0.f, 0.f, 1.f};
         const f3 wr = root ? f3{w[0], w[1], w[2]} : qapply(qb, f3{w[0], w[1], w[2]});
-        if (bl) { L.Acc[lane][0] = wr.x; L.Acc[lane][1] = wr.y; L.Acc[lane][2] = wr.z; }
-        sync();
-        f3 wo = f3{0.f, 0.f, 0.f};
-        if (bl)
-            for (int k = 0; k <= T.depth[lane]; ++k) {
-                const int a = T.chain[lane][k];
-                wo = wo + f3{L.Acc[a][0], L.Acc[a][1], L.Acc[a][2]};
-            }
+        // chain prefix by pointer jumping (the table stops below the root: its rate is added last)
+        f3 wo = bl ? wr : f3{0.f, 0.f, 0.f};
+        {
+            const uint32_t jp = bl ? T.jump4[lane] : 0xFFFFFFFFu;
+            auto round = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                const int j = jump_of<K>(jp);
+                const int src = j < 0 ? lane : j;
+                const f3 wa = f3{__shfl(wo.x, src, W), __shfl(wo.y, src, W), __shfl(wo.z, src, W)};
+                if (j >= 0) wo = wo + wa;
+            };
+            round(std::integral_constant<int, 0>{});
+            round(std::integral_constant<int, 1>{});
+            round(std::integral_constant<int, 2>{});
+            if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
+            const f3 w0 = f3{__shfl(wr.x, 0, W), __shfl(wr.y, 0, W), __shfl(wr.z, 0, W)};
+            if (HE_KIN_ROOTREL && bl && !root) wo = wo + w0;
+        }
         const float wmax = p.max_angular_velocity;
         const float wn2 = dot3(wo, wo);
         const bool over = bl && wn2 > wmax * wmax;
         if (__ballot(over) != 0ull) {  // rare (wave-uniform branch)
             const f3 wc = over ? wo * (wmax * __builtin_amdgcn_rsqf(wn2)) : wo;
-            if (bl) { L.Acc[lane][3] = wc.x; L.Acc[lane][4] = wc.y; L.Acc[lane][5] = wc.z; }
-            sync();
+            const int pb = bl && !root ? T.chain[lane][T.depth[lane] - 1] : 0;
+            const f3 wp = f3{__shfl(wc.x, pb, W), __shfl(wc.y, pb, W), __shfl(wc.z, pb, W)};
             if (bl) {
-                const int pb = root ? 0 : T.chain[lane][T.depth[lane] - 1];
-                const f3 rel = root ? wc : wc - f3{L.Acc[pb][3], L.Acc[pb][4], L.Acc[pb][5]};
+                const f3 rel = root ? wc : wc - wp;
                 const f3 ub = root ? rel : qapply(qconj(qb), rel);
                 w[0] = ub.x; w[1] = ub.y; w[2] = ub.z;
             }

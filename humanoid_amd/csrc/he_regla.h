@@ -393,6 +393,38 @@ __device__ __forceinline__ void solve_LT_vec(const float* Lp, int dj, int dj2, f
     }
 }
 
+// solve_LT_vec in groups of mutually independent pivots (no pivot of a group is an ancestor of
+// another, so every y_K of a group is final when the group starts; ElimGroups below): the group's
+// broadcasts are read first, then its updates, so the dependent chain is paid once per group (30
+// groups of the 75 pivots) instead of once per pivot. Each register's updates keep their order
+// within a group only up to the group's order, so the rounding differs from solve_LT_vec.
+template <int GMAX>
+struct ElimGroups;
+template <int S0, int Q, int N>
+__device__ __forceinline__ void lt_group_read(float (&yk)[N], float yl, float y2) {
+    if constexpr (Q < N) {
+        constexpr int K = kElimOrder[S0 + Q];
+        yk[Q] = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
+        lt_group_read<S0, Q + 1, N>(yk, yl, y2);
+    }
+}
+template <int S0, int Q, int N>
+__device__ __forceinline__ void lt_group_update(const float* Lp, int dj, int dj2, const float (&yk)[N], float& yl,
+                                                float& y2) {
+    if constexpr (Q < N) {
+        constexpr int K = kElimOrder[S0 + Q];
+        if constexpr (kDofNanc[K] - 1 > 0) {
+            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+            if (lanes<lo>()) yl = yl - Lp[kPackStart[K] + dj] * yk[Q];
+            if constexpr (K > 64) {
+                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+                if (lanes<hi>()) y2 = y2 - Lp[kPackStart[K] + dj2] * yk[Q];
+            }
+        }
+        lt_group_update<S0, Q + 1, N>(Lp, dj, dj2, yk, yl, y2);
+    }
+}
+
 // ---------------------------------------------------------------- grouped elimination
 // Consecutive steps of kElimOrder whose dofs are mutually independent (neither is an ancestor of
 // the other: different branches) touch disjoint pivots and rows, so a group of them runs as one
@@ -429,6 +461,19 @@ struct ElimGroups {
 #endif
 constexpr int kElimGroupMax = HE_ELIM_GMAX;
 constexpr ElimGroups<kElimGroupMax> kElimGroups{};
+constexpr ElimGroups<8> kLTGroups{};  // solve_LT_vec_groups: 30 groups
+
+template <int G>
+__device__ __forceinline__ void solve_LT_vec_groups(const float* Lp, int dj, int dj2, float& yl, float& y2) {
+    if constexpr (G < kLTGroups.count) {
+        constexpr int S0 = kLTGroups.start[G], N = kLTGroups.start[G + 1] - kLTGroups.start[G];
+        float yk[N];
+        lt_group_read<S0, 0, N>(yk, yl, y2);
+        lt_group_update<S0, 0, N>(Lp, dj, dj2, yk, yl, y2);
+        __builtin_amdgcn_sched_barrier(0);  // the next group's row loads stay behind (VGPR budget)
+        solve_LT_vec_groups<G + 1>(Lp, dj, dj2, yl, y2);
+    }
+}
 
 #ifndef HE_FAC_VINV  // +0.4% (A/B r01)
 #define HE_FAC_VINV 1

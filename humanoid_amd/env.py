@@ -110,7 +110,7 @@ class EnvConfig:  # config.py:89-157
     # engine extensions (not in the reference config)
     seed: int = 0
     max_contacts: int = 20
-    solver_iterations: int = 4  # physx.num_position_iterations (isaacgym_env.py:17)
+    solver_iterations: int = 8  # PGS sweeps per physics step
 
     @property
     def device(self) -> str:

@@ -308,8 +308,7 @@ class Gym:
         params = _abi.default_sim_params(
             dt=sp.dt, contact_offset=px.contact_offset, max_depenetration_velocity=px.max_depenetration_velocity,
             angular_damping=o.angular_damping, max_angular_velocity=o.max_angular_velocity,
-            friction=plane.static_friction, self_collision=int(bool(sim.self_collision)), substeps=int(sp.substeps),
-            solver_iterations=int(px.num_position_iterations))
+            friction=plane.static_friction, self_collision=int(bool(sim.self_collision)), substeps=int(sp.substeps))
         params.gravity[:] = (sp.gravity.x, sp.gravity.y, sp.gravity.z)
         n = len(sim.envs)
         xy = np.array([p[0][:2] for p in sim.start_poses], np.float32)

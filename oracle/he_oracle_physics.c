@@ -32,6 +32,25 @@ typedef double R;
 #define MAXC 64
 #define MAXROW (3 * MAXC)
 
+/* Sensitivity probes (tests/test_gpu_parity.py _cond_close): rounding-level noise on the Delassus
+ * operator and the contact right-hand side, A_rc (1 + rel xi), b_r (1 + rel xi) with xi uniform in
+ * [-1, 1] hashed from (seed, env, physics step, r, c). A resting body's contacts are statically
+ * indeterminate (A nearly singular), and how the impulses spread over them -- which friction row
+ * reaches its bound first -- moves with A's rounding as much as with the state's: the fp32 engine
+ * rounds A in every step. 0 (the default) = off. Test infrastructure only. */
+static double g_probe_rel = 0.0;
+static uint64_t g_probe_seed = 0;
+static __thread int g_probe_env, g_probe_sub;
+void ho_set_probe_noise(uint64_t seed, double rel) { g_probe_seed = seed; g_probe_rel = rel; }
+static double probe_xi(int r, int c) {
+    uint64_t z = g_probe_seed * 0x9E3779B97F4A7C15ull ^ ((uint64_t)g_probe_env + 0x632BE59BD9B4E019ull) * 0xBF58476D1CE4E5B9ull ^
+                 ((uint64_t)g_probe_sub * 4099u + (uint64_t)r * 131u + (uint64_t)c + 0x2545F4914F6CDD1Dull) * 0x94D049BB133111EBull;
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
 typedef struct topo {
     int dof_parent[NG];
     int dof_body[NG];
@@ -751,6 +770,8 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     memset(out->contact_force, 0, sizeof(out->contact_force));
     R unew[NG];
     memcpy(unew, uf, sizeof(unew));
+    R lim_tau[ND];
+    memset(lim_tau, 0, sizeof(lim_tau));
     if (nc > 0) {
         int nr = 3 * nc;
         R brow[MAXROW];
@@ -788,6 +809,16 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                 A[r][c2] = acc;
                 A[c2][r] = acc;
             }
+        if (g_probe_rel > 0) { /* sensitivity probe (above) */
+            for (int r = 0; r < nr; ++r) {
+                for (int c2 = 0; c2 <= r; ++c2) {
+                    A[r][c2] *= 1.0 + g_probe_rel * probe_xi(r, c2);
+                    A[c2][r] = A[r][c2];
+                }
+                brow[r] *= 1.0 + g_probe_rel * probe_xi(r, MAXROW);
+            }
+            ++g_probe_sub;
+        }
         R lam[MAXROW];
         memset(lam, 0, sizeof(lam));
         if (ws && p->warm_start)
@@ -862,7 +893,10 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         for (int i = 0; i < NG; ++i) unew[i] += y[i];
         for (int ci = 0; ci < nc; ++ci) {
             const contact* c = &cs[ci];
-            if (c->b1 == -2) continue; /* joint limits are not contact forces */
+            if (c->b1 == -2) { /* a joint limit: a joint force (below), not a contact force */
+                for (int x = 0; x < 3; ++x) lim_tau[3 * (c->b0 - 1) + x] += c->g[x] * lam[3 * ci] / dt;
+                continue;
+            }
             for (int x = 0; x < 3; ++x) {
                 R f = (lam[3 * ci] * c->n[x] + lam[3 * ci + 1] * c->t1[x] + lam[3 * ci + 2] * c->t2[x]) / dt;
                 out->contact_force[c->b0][x] += f;
@@ -872,8 +906,13 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     } else if (ws) {
         ws->n = 0;
     }
-    /* drive force actually applied: tau(u+) = tau_exp - (dt kp + kd)(u+ - u) */
+    /* drive force actually applied: tau(u+) = tau_exp - (dt kp + kd)(u+ - u); then the joint-limit
+     * force: dof_force is the joint's solver force, drive and limit constraints together (PhysX
+     * articulations report the joint solver forces, PxArticulationCache::jointSolverForces; Isaac
+     * Gym's dof-force sensor reads them -- unpinned here): the limit row g over the
+     * joint's dofs with its impulse lambda adds g lambda / dt */
     for (int d = 0; d < ND; ++d) out->dof_force[d] -= coef[6 + d] * (unew[6 + d] - u0[6 + d]);
+    for (int d = 0; d < ND; ++d) out->dof_force[d] += lim_tau[d];
     /* angular damping and max angular velocity (asset options, humanoid_phc.py:212-213) */
     R damp = 1.0 / (1.0 + dt * p->angular_damping);
     for (int c = 0; c < 3; ++c) unew[c] *= damp;
@@ -1000,6 +1039,8 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         }
         step_out out;
         memset(&out, 0, sizeof(out));
+        g_probe_env = e;
+        g_probe_sub = 0;
         for (int it = 0; it < substeps; ++it) substep(m, &t, p, &s, mass_scale ? ms : NULL, mu, tk, &out, &ws);
         for (int c = 0; c < 3; ++c) { rs[c] = (float)s.root_pos[c]; rs[7 + c] = (float)s.root_v[c]; rs[10 + c] = (float)s.root_w[c]; }
         for (int c = 0; c < 4; ++c) rs[3 + c] = (float)s.root_q[c];

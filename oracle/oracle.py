@@ -153,6 +153,12 @@ def new_cache(n):
     return np.zeros((n, _abi.CACHE_WORDS), np.float32)
 
 
+def set_probe_noise(seed=0, rel=0.0):
+    """Sensitivity probes only: rounding-level noise rel on the Delassus operator and the contact
+    right-hand side of the following physics_step calls (he_oracle_physics.c); rel 0 turns it off."""
+    lib().ho_set_probe_noise(C.c_uint64(int(seed)), C.c_double(float(rel)))
+
+
 def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, dof_state, targets, substeps=2,
                  mass_scale=None, friction=None, terrain_kind=None, cache=None):
     """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays) and on the warm-start

@@ -129,3 +129,17 @@ def rounding_noise(root, dof, seed):
     dof[..., 0] += (1e-6 * rng.standard_normal(dof[..., 0].shape)).astype(np.float32)
     dof[..., 1] *= (1.0 + 1e-6 * rng.standard_normal(dof[..., 1].shape)).astype(np.float32)
     root[:, 7:13] *= (1.0 + 1e-6 * rng.standard_normal(root[:, 7:13].shape)).astype(np.float32)
+
+
+def probe_physics_step(he_model, sp, root, dof, targets, calls, cache, seed, **props):
+    """One oracle policy step of a sensitivity probe (test_gpu_parity._cond_close), in place on
+    root / dof / cache: the fp32 engine's rounding modelled on the state (rounding_noise) and on the
+    contact solve's Delassus operator and right-hand side (oracle set_probe_noise, relative 1e-6),
+    fresh in every step."""
+    from oracle import oracle as O
+    rounding_noise(root, dof, seed)
+    O.set_probe_noise(seed, 1e-6)
+    try:
+        return O.physics_step(he_model, sp, root, dof, targets, calls, cache=cache, **props)
+    finally:
+        O.set_probe_noise(0, 0.0)

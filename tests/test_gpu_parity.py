@@ -370,6 +370,32 @@ def contact_keys(cache):
     return [tuple(sorted(keys[e, :n[e]].tolist())) for e in range(c.shape[0])]
 
 
+def friction_states(cache, mu):
+    """Per env: the stick / slip state of every contact of the last solve, from a warm-start cache:
+    sorted (key, s1, s2) with s = +1 / -1 when a friction impulse sits on its bound +-mu lambda_n
+    (within 1e-6 of it: the clamp acted, sliding), 0 inside (sticking); contacts with no normal impulse and the joint
+    limits left out. A friction row crossing its bound is a discontinuity of the step like a contact
+    entering the set: where the fp32 engine and the fp64 oracle land on different sides, their
+    trajectories part by the slip, so such envs are excluded like contact-set mismatches."""
+    c = np.ascontiguousarray(cache, np.float32)
+    n = c[:, 7].view(np.int32)
+    keys = c[:, _abi.CACHE_KEYS:_abi.CACHE_KEYS + _abi.MAX_CONTACTS].view(np.int32)
+    lam = c[:, _abi.CACHE_LAMBDA:_abi.CACHE_LAMBDA + 3 * _abi.MAX_CONTACTS].reshape(c.shape[0], -1, 3)
+    mu = np.broadcast_to(np.asarray(mu, np.float32), (c.shape[0],))
+    out = []
+    for e in range(c.shape[0]):
+        st = []
+        for k in range(n[e]):
+            key = int(keys[e, k])
+            ln = float(lam[e, k, 0])
+            if ((key >> 8) & 0xFF) == 0 or ln <= 1e-5:  # b1 + 2 == 0: a joint limit
+                continue
+            bound = float(mu[e]) * ln * (1.0 - 1e-6)
+            st.append((key,) + tuple(int(np.sign(lam[e, k, x])) if abs(lam[e, k, x]) >= bound else 0 for x in (1, 2)))
+        out.append(tuple(sorted(st)))
+    return out
+
+
 def _obs_tol(oo):
     """Per-element obs tolerance: 5e-5 + 1e-5 rel, and for the velocity blocks (self lin/ang vel
     214:358, task vel/ang-vel differences 574:718) 2e-6 of the 3-vector's norm: a body spinning at
@@ -384,14 +410,17 @@ def _obs_tol(oo):
 
 
 def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-4, vel_tol=1e-2, max_skip=0.02,
-                     max_widened=0.05, env_props=None, **sim):
+                     max_widened=0.05, env_props=None, max_slip=0.0, **sim):
     """Engine vs oracle for `steps` policy steps (`calls` gym.simulate() each) from the same state,
     both warm-starting from their own caches. The oracle's sensitivity probes (_cond_close) carry
-    rounding-level noise (cases.rounding_noise) into every policy step, as the fp32 engine rounds in
-    every step, not only at the start. Envs whose contact SETS (keys: body, partner, candidate) ever differ are excluded
-    (a point within rounding of the 0.02 m offset, or a tie in the deepest-first reduction), at most
-    `max_skip` of them; at most `max_widened` of the compared elements may need the sensitivity
-    widening (_cond_close)."""
+    rounding-level noise (cases.probe_physics_step: state and Delassus operator) into every policy
+    step, as the fp32 engine rounds in
+    every step, not only at the start. Envs whose contact SETS (keys: body, partner, candidate) ever
+    differ are excluded (a point within rounding of the 0.02 m offset, or a tie in the deepest-first
+    reduction), at most `max_skip` of them; with max_slip > 0 so are envs whose stick / slip states
+    ever differ (friction_states), at most `max_slip` together with those (otherwise the count is
+    reported); at most `max_widened` of the compared elements may need the sensitivity widening
+    (_cond_close), taken over 3 probes (8 past 5 steps)."""
     n = root.shape[0]
     eng = make_engine(he_model, n, **sim)
     props = {}
@@ -405,24 +434,33 @@ def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-
     eng.dof_targets.copy_(cu(targets))
     r_o, d_o, c_o = root.copy(), dof.copy(), O.new_cache(n)
     # sensitivity probes: joint angles moved by 1e-6 rad (three independent draws)
-    probes = [[root.copy(), dof.copy(), None, O.new_cache(n)] for _ in range(3)]
+    # more probes over longer horizons: a friction row that crosses its bound in some of them shows
+    # the element's discontinuity, which three draws can miss
+    probes = [[root.copy(), dof.copy(), None, O.new_cache(n)] for _ in range(3 if steps <= 5 else 8)]
     sp = _abi.default_sim_params(**sim)
     mismatch = np.zeros(n, bool)
+    slip = np.zeros(n, bool)
     for step in range(steps):
         eng.simulate(calls)
         out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, calls, cache=c_o, **props)
         for k, pr in enumerate(probes):
-            cases.rounding_noise(pr[0], pr[1], 123 + 1000 * k + step)
-            pr[2] = O.physics_step(eng.he_model, sp, pr[0], pr[1], targets, calls, cache=pr[3], **props)
+            pr[2] = cases.probe_physics_step(eng.he_model, sp, pr[0], pr[1], targets, calls, pr[3], 123 + 1000 * k + step,
+                                             **props)
         torch.cuda.synchronize()
-        kg = contact_keys(eng.contact_cache.cpu().numpy())
+        cg = eng.contact_cache.cpu().numpy()
+        kg = contact_keys(cg)
         ko = contact_keys(c_o)
         mismatch |= np.array([a != b for a, b in zip(kg, ko)])
+        mu = props["friction"] if "friction" in props else sp.friction
+        slip |= np.array([a != b for a, b in zip(friction_states(cg, mu), friction_states(c_o, mu))])
         mismatch |= eng.num_contacts.cpu().numpy() != out["num_contacts"]
         mismatch |= eng.dropped_contacts.cpu().numpy() != out["dropped"]
-    ok = ~mismatch
-    print(f"contact-set mismatch: {mismatch.sum()}/{n} envs")
+    excl = mismatch | (slip if max_slip > 0 else False)
+    ok = ~excl
+    print(f"contact-set mismatch: {mismatch.sum()}/{n} envs, stick/slip mismatch: {(slip & ~mismatch).sum()}/{n}"
+          f"{'' if max_slip > 0 else ' (reported, not excluded)'}")
     assert mismatch.mean() <= max_skip, f"contact-set mismatch in {mismatch.sum()}/{n} envs"
+    assert excl.mean() <= max(max_skip, max_slip), f"{excl.sum()}/{n} envs excluded"
     rg = eng.root_states.cpu().numpy()
     dg = eng.dof_state.view(n, 69, 2).cpu().numpy()
     rbg = eng.rb_state.view(n, 24, 13).cpu().numpy()
@@ -542,6 +580,13 @@ def test_knee_limit_matches_oracle(he_model, model):
     q = eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0]
     ang = np.linalg.norm(q.reshape(n, 23, 3), axis=-1)
     assert ang.max() < np.pi and ang[:, [1, 5]].min() > np.pi - 0.05  # knees (joints 2, 6) on the limit
+    # dof_force carries the limit force with the drive's: along the knee's axis the two
+    # cancel to the inertial remainder, as in the oracle (compared above at 0.5 N m)
+    f = eng.dof_force.view(n, 69).cpu().numpy().reshape(n, 23, 3)
+    qa = q.reshape(n, 23, 3)
+    for j in (1, 5):
+        along = (f[:, j] * qa[:, j]).sum(1) / np.linalg.norm(qa[:, j], axis=1)
+        assert (np.abs(along) < 50.0).all(), along
 
 
 def test_contact_overflow_counted_and_reduced(he_model):
@@ -605,8 +650,7 @@ def test_env_step_fused_matches_oracle(he_model, model, golden):
         probes = []
         for k in range(3):  # oracle sensitivity probes (see _cond_close)
             r_s, d_s = r_pre.copy(), d_pre.copy()
-            cases.rounding_noise(r_s, d_s, 100 * step + k)
-            O.physics_step(eng.he_model, sp, r_s, d_s, tgt.astype(np.float32), 2, cache=c_pre.copy())
+            cases.probe_physics_step(eng.he_model, sp, r_s, d_s, tgt.astype(np.float32), 2, c_pre.copy(), 100 * step + k)
             probes.append((r_s, d_s))
         c_o = c_pre.copy()
         out = O.physics_step(eng.he_model, sp, r_pre, d_pre, tgt.astype(np.float32), 2, cache=c_o)

@@ -208,3 +208,35 @@ def test_moderate_random_actions_stay_physical(he_model, model):
     q = np.linalg.norm(dof[..., 0].reshape(n, 23, 3), axis=-1)
     assert vmax < 7.0, vmax
     assert q.max() < np.pi - 0.01
+
+
+def test_limit_force_is_part_of_dof_force(he_model, model):
+    """dof_force is the joint's solver force, drive and limit together (PhysX's articulation
+    joint solver forces): knees driven at +5 rad targets (humanoid_phc.py:441-446) rest on their
+    angle limit, where the saturated drive (500 N m along the joint's axis) is held by the limit, so
+    the reported force along the axis is the small inertial remainder (~5 N m), not the drive's
+    500. A joint off its limit reports its drive force alone (the power reward, humanoid_phc.py:
+    1297-1305, reads these)."""
+    n = 4
+    rng = np.random.default_rng(7)
+    root, dof = cases.standing_state(model, n, rng, xy_jitter=0.5)
+    root[:, 2] += 1.5
+    targets = np.zeros((n, 69), np.float32)
+    targets[:, [4, 16]] = 5.0
+    sp = _abi.default_sim_params(self_collision=0)
+    cache = O.new_cache(n)
+    for _ in range(20):
+        out = O.physics_step(he_model, sp, root, dof, targets, 2, cache=cache)
+    for j in (1, 5):  # L_Knee, R_Knee joints
+        q = dof[:, 3 * j:3 * j + 3, 0].astype(np.float64)
+        t = np.linalg.norm(q, axis=1)
+        assert (t > np.pi - 0.03).all()  # on the limit
+        f = out["dof_force"][:, 3 * j:3 * j + 3].astype(np.float64)
+        assert (np.abs((f * q).sum(1) / t) < 50.0).all(), (f * q).sum(1) / t
+    # the first step of the same bodies, far from the limit: the drive force alone (the implicit
+    # drive's 1504 N m command, effort-scaled, relieved by the step's motion: ~135 N m)
+    r2, d2 = cases.standing_state(model, n, np.random.default_rng(7), xy_jitter=0.5)
+    r2[:, 2] += 1.5
+    o2 = O.physics_step(he_model, sp, r2, d2, targets, 2, cache=O.new_cache(n))
+    f = o2["dof_force"][:, [4, 16]]
+    assert (np.abs(f) > 100.0).all(), f

@@ -22,11 +22,12 @@ from humanoid_amd.model import load_default_model, pd_action_offset_scale  # noq
 from oracle import oracle as O  # noqa: E402
 
 SETTINGS = {"cold_8": (8, False), "warm_2": (2, True), "warm_4": (4, True), "warm_6": (6, True),
-            "warm_8": (8, True), "warm_16": (16, True)}
+            "warm_8": (8, True), "warm_16": (16, True), "warm_8_tol1e-5": (8, True, 1e-5),
+            "warm_8_tol1e-4": (8, True, 1e-4), "warm_16_tol1e-5": (16, True, 1e-5)}
 
 
-def one_step(hm, r, d, c, targets, iters, warm):
-    sp = _abi.default_sim_params(solver_iterations=iters, warm_start=1 if warm else 0)
+def one_step(hm, r, d, c, targets, iters, warm, tol=0.0):
+    sp = _abi.default_sim_params(solver_iterations=iters, warm_start=1 if warm else 0, solver_tolerance=tol)
     r, d = r.copy(), d.copy()
     cache = c.copy() if warm else None
     out = O.physics_step(hm, sp, r, d, targets, 2, cache=cache)
@@ -39,12 +40,12 @@ def scenario(hm, root, dof, target_fn, steps):
     res = {k: [] for k in SETTINGS}
     dv = {k: [] for k in SETTINGS}
     dq = {k: [] for k in SETTINGS}
-    sp8 = _abi.default_sim_params()
+    sp8 = _abi.default_sim_params()  # the trajectory: the engine default
     for t in range(steps):
         tg = target_fn(t)
         rr, dr, _ = one_step(hm, r, d, c, tg, 64, True)
-        for k, (it, warm) in SETTINGS.items():
-            rs, ds, rsd = one_step(hm, r, d, c, tg, it, warm)
+        for k, st in SETTINGS.items():
+            rs, ds, rsd = one_step(hm, r, d, c, tg, *st)
             res[k].append(rsd)
             dv[k].append(np.abs(ds[..., 1] - dr[..., 1]).max(1))
             dq[k].append(np.abs(ds[..., 0] - dr[..., 0]).max(1))
