@@ -3,7 +3,7 @@ spread under the sensitivity probes' modelled rounding (tests/cases.probe_physic
 scenario the distribution of |gpu - oracle| / |probe - oracle| over the joint velocities and angles.
 Calibrates the probes (diagnostic).
 
-  python tools/diag_onestep.py
+  python tests/diag/diag_onestep.py
 """
 import json
 import os
@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

@@ -2,14 +2,14 @@
 envs from the same state, engine vs oracle: per env the contact keys, the impulses of every row
 (warm-start cache words) and the max joint-velocity difference.
 
-  python tools/diag_self.py
+  python tests/diag/diag_self.py
 """
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

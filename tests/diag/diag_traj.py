@@ -2,7 +2,7 @@
 for every policy step, per env, max |gpu - oracle| of the joint angles, the oracle's own spread
 under fp32-level noise (3 probes, tests/cases.rounding_noise), and the step's contact count.
 
-  python tools/diag_traj.py [case]   (case: traj30 | cold)
+  python tests/diag/diag_traj.py [case]   (case: traj30 | cold)
 """
 import json
 import os
@@ -10,7 +10,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

@@ -5,7 +5,7 @@ Standing envs under random PD actions U(-amp, amp) of the PD scale, new every po
 the median internal kinetic energy at the end and the largest link world angular velocity.
 Airborne envs (no contact) under U(+-0.5): median internal kinetic energy after 3 s.
 
-  python tools/energy_probe.py [--n 256] [--steps 60]
+  python tests/diag/energy_probe.py [--n 256] [--steps 60]
 """
 import argparse
 import json
@@ -15,7 +15,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

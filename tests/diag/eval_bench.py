@@ -5,7 +5,7 @@ Reference flow (host): the per-step D2H copies of body_pos / body_pos_gt (humano
 and, per batch, the restated compute_metrics_lite over 4096 motions of 149 frames (the smpl_sim
 call at phc_train.py:188; here oracle/eval_metrics.py, numpy).
 
-Usage: python tools/eval_bench.py [--out profiles/r01/eval_bench.json]"""
+Usage: python tests/diag/eval_bench.py [--out profiles/r01/eval_bench.json]"""
 import argparse
 import json
 import os
@@ -15,7 +15,7 @@ import time
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from humanoid_amd.eval import EvalRecorder  # noqa: E402

@@ -9,7 +9,7 @@ Host path (the reference's data flow, restated by oracle.HostExperience): per st
 the host gathers (obs stays on the device in the reference, gathered there by torch indexing) and
 the C restatement of the Cython GAE, plus the advantage H2D copy (core.py:249).
 
-Usage: python tools/handoff_bench.py [--out profiles/r01/handoff_bench.json] [--mask]"""
+Usage: python tests/diag/handoff_bench.py [--out profiles/r01/handoff_bench.json] [--mask]"""
 import argparse
 import json
 import os
@@ -19,7 +19,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from humanoid_amd.experience import Experience  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 

@@ -5,7 +5,7 @@ from that same state: the residual after the sweeps and the one-step deviation o
 velocities / positions. Scenarios: standing bodies under random actions (U(-0.5, 0.5) of the PD
 scale, new each step) and lying bodies thrown out of the plane (cases.lying_state, tumbling).
 
-  python tools/pgs_iterations.py > profiles/r02/pgs_iterations.json
+  python tests/diag/pgs_iterations.py > profiles/r02/pgs_iterations.json
 """
 import json
 import os
@@ -13,8 +13,8 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "..", "tests"))
 
 import cases  # noqa: E402
 from humanoid_amd import _abi  # noqa: E402

@@ -3,7 +3,7 @@ fallen / tumbling bodies stepped with the engine's capacity (max_contacts 20, de
 reduction) and with the oracle's own 64-contact capacity, and the difference reported:
 penetration (lowest contact-candidate gap), CoM trajectory, contacts dropped.
 
-  python tools/truncation_effect.py [--envs 128] [--steps 60] > profiles/r02/truncation_effect.json
+  python tests/diag/truncation_effect.py [--envs 128] [--steps 60] > profiles/r02/truncation_effect.json
 """
 import argparse
 import json
@@ -12,8 +12,8 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "..", "tests"))
 
 import cases  # noqa: E402
 from humanoid_amd import _abi  # noqa: E402
