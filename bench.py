@@ -49,9 +49,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=20)
     ap.add_argument("--scheme", choices=["default", "r02"], default="default",
-                    help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 4 sweeps, "
-                         "link world angular-velocity clamp; r02 = round 2's energy-unstable scheme (2 x 1/60 s, "
-                         "explicit bias, 8 sweeps), for the cost comparison only (DESIGN §5)")
+                    help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 sweeps, "
+                         "link world angular-velocity clamp; r02 = round 2's energy-unstable step (2 x 1/60 s, "
+                         "explicit bias, 8 sweeps) with round 3's clamps, for the cost comparison only (DESIGN §5)")
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
@@ -256,7 +256,7 @@ def sim_substeps(args):
 def scheme_params(args):
     """he_sim_params overrides of the --scheme."""
     if getattr(args, "scheme", "default") == "r02":
-        return dict(substeps=1, bias_midpoint=0, solver_iterations=8, max_angular_velocity=1e9)
+        return dict(substeps=1, bias_midpoint=0, solver_iterations=8)
     return {}
 
 

@@ -2,8 +2,8 @@
 random actions U(-amp, amp) of the PD scale, per amplitude the envs whose root ever exceeds
 10 / 15 / 50 m/s, the worst root and centre-of-mass speeds, the worst joint angle and the median
 internal kinetic energy (about the centre of mass) at the end. Engine (GPU) run, under the default
-physics scheme and, for comparison, round 2's (one 1/60 s physics step per simulate, explicit bias,
-no world angular-velocity clamp).
+physics scheme and, for comparison, round 2's step (one 1/60 s physics step per simulate, explicit
+bias) under round 3's angular-velocity clamps.
 
   python tools/action_regimes.py > profiles/r03/action_regimes.json
 """
@@ -41,7 +41,7 @@ def kinetic(model, rb):
     return ke, vcom, 0.5 * m.sum() * (vcom * vcom).sum(-1)
 
 
-SCHEMES = {"default": {}, "r02": dict(substeps=1, bias_midpoint=0, max_angular_velocity=1e9)}
+SCHEMES = {"default": {}, "r02": dict(substeps=1, bias_midpoint=0)}  # round 2's step with round 3's clamps
 
 
 def main():
@@ -72,13 +72,15 @@ def main():
         ke, _, kc = kinetic(model, eng.rb_state.view(n, -1, 13))
         q = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3).norm(dim=-1)
         v = vmax.cpu().numpy()
+        v[~np.isfinite(v)] = np.inf  # a blown-up env counts as over every bound
         c = cmax.cpu().numpy()
+        c[~np.isfinite(c)] = np.inf
         key = str(amp) if scheme == "default" else f"{scheme}:{amp}"
         res[key] = {"envs_over_10mps": int((v > 10).sum()), "envs_over_15mps": int((v > 15).sum()),
                     "envs_over_50mps": int((v > 50).sum()),
                     "root_speed_max": float(v.max()), "root_speed_p99": float(np.percentile(v, 99)),
                     "com_speed_max": float(c.max()), "envs_com_over_5mps": int((c > 5).sum()),
-                    "internal_ke_median_J": float((ke - kc).median()),
+                    "internal_ke_median_J": float((ke - kc).nan_to_num(nan=float("inf")).median()),
                     "joint_angle_max": float(q.max())}
         print(key, res[key], file=sys.stderr, flush=True)
         del eng
