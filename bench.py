@@ -47,7 +47,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
-    ap.add_argument("--max-contacts", type=int, default=20)
+    ap.add_argument("--max-contacts", type=int, default=40)
     ap.add_argument("--scheme", choices=["default", "r02"], default="default",
                     help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 sweeps, "
                          "link world angular-velocity clamp; r02 = round 2's energy-unstable step (2 x 1/60 s, "

@@ -10,14 +10,35 @@ import numpy as np
 from .model import HumanoidModel
 
 NB, ND, NG = 24, 69, 75
-MAX_PAIRS, MAX_CONTACTS = 256, 21
+MAX_PAIRS = 256
 OBS_SELF, OBS_TASK, OBS_DIM = 358, 576, 934
 
 (BUF_ROOT_STATE, BUF_DOF_STATE, BUF_RB_STATE, BUF_CONTACT_FORCE, BUF_DOF_FORCE, BUF_DOF_TARGET, BUF_NUM_CONTACTS,
  BUF_DROPPED_CONTACTS, BUF_CONTACT_CACHE, BUF_INIT_ROOT_STATE) = range(10)
 # StateInit (envs/state_init.py) -> he_imitation_params.state_init
 STATE_INIT = {"Default": 0, "Start": 1, "Random": 2, "Hybrid": 3}
-CACHE_WORDS, CACHE_KEYS, CACHE_LAMBDA = 96, 8, 32  # he_sim_params warm-start cache layout
+CACHE_WORDS, CACHE_KEYS, CACHE_LAMBDA = 104, 8, 40  # he_sim_params warm-start cache layout (row keys, impulses)
+MAX_CONTACTS, MAX_ROWS = 40, 63
+KEY_PATCH = 15  # row key sub-index of a body's terrain-patch friction rows
+
+
+def cache_rows(cache):
+    """Rows of warm-start caches [N, CACHE_WORDS] (include/humanoid_engine.h): row counts [N],
+    16-bit row keys [N, MAX_ROWS] (int64, -1 past the count) and impulses [N, MAX_ROWS]."""
+    c = np.ascontiguousarray(cache, np.float32)
+    n = c[:, 7].view(np.int32).copy()
+    kw = c[:, CACHE_KEYS:CACHE_KEYS + (MAX_ROWS + 1) // 2].view(np.uint32)
+    keys = np.stack([kw & 0xFFFF, kw >> 16], -1).reshape(c.shape[0], -1)[:, :MAX_ROWS].astype(np.int64)
+    lam = c[:, CACHE_LAMBDA:CACHE_LAMBDA + MAX_ROWS].copy()
+    keys[np.arange(MAX_ROWS)[None, :] >= n[:, None]] = -1
+    return n, keys, lam
+
+
+def key_fields(key):
+    """(body0, body1, sub, kind) of a 16-bit row key: body1 -1 terrain, -2 joint limit; kind 0
+    normal, 1 / 2 tangential, 3 torsional."""
+    key = int(key)
+    return key & 31, ((key >> 5) & 31) - 2, (key >> 10) & 15, key >> 14
 DTYPE_F32, DTYPE_I32 = 1, 2
 
 
@@ -107,7 +128,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.max_angular_velocity = 100.0
     p.solver_iterations = 8  # PGS sweeps per physics step (4 leave 100x the one-step deviation)
     p.self_collision = 1
-    p.max_contacts = 20
+    p.max_contacts = 40
     p.kp_scale = 1.0
     p.kd_scale = 1.0
     p.terrain = 0

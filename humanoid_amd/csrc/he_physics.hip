@@ -33,11 +33,11 @@ namespace {
 constexpr int NB = HE_NUM_BODIES;
 constexpr int ND = HE_NUM_DOF;
 constexpr int NG = HE_NUM_GEN;
-constexpr int MAXC = HE_MAX_CONTACTS;
-constexpr int MAXR = 3 * MAXC;  // <= 63: one contact row per lane
+constexpr int MAXC = HE_MAX_CONTACTS;  // contact slots (points, joint limits)
+constexpr int MAXR = HE_MAX_ROWS;      // solver rows, one per lane (patch friction, oracle build_rows)
 constexpr int W = 64;
-static_assert(MAXR <= W - 1, "contact rows must fit one per lane");
-static_assert(MAXC <= NB, "per-contact impulses reuse a per-body scratch array");
+static_assert(MAXR <= W - 1, "solver rows must fit one per lane");
+static_assert(MAXC < W, "one slot per lane in the row-layout pass");
 static_assert(smpl::kNG == NG && smpl::kNB == NB, "generated topology mismatch");
 
 struct BodyTopo {
@@ -55,34 +55,36 @@ struct BodyTopo {
 
 struct Lds {
     float q[ND], tgt[ND];
-    float u0[NG], uf[NG], rhs[NG], coef[NG], Dinv[NG], sDinv[NG];
+    float u0[NG], uf[NG], rhs[NG], coef[NG], sDinv[NG];
     float yh[NG];  // D^-1/2 L^-T (dt rhs): the free motion's share of the one L^-1 sweep
     float ql[NB][4], qw[NB][4];
     float pw[NB][3];  // body origins RELATIVE to the root origin o (world axes): every spatial quantity
                       // is taken about o, and fp32 keeps ~1e-7 m of them however far o is from the
                       // world origin (world = o + pw only where a world position is needed)
     float S[NG][6], IS[NG][6];
-    float V[NB][6], Acc[NB][6], F[NB][6];
+    float V[NB][6], F[NB][6];
+    alignas(16) float Acc[NB][6];  // contact phase: the bodies' bounding spheres (bsph) instead
     float Ib[NB][10], Ic[NB][10];  // m, h(3), I(xx yy zz xy xz yz)
     alignas(16) float Lp[smpl::kNpack + 4];  // packed unit-lower factor L (row K: ancestors in chain
                                              // order); Lp[kNpack] is the elimination's store sink
-    float cx[MAXC][3], cn[MAXC][3], ct1[MAXC][3], ct2[MAXC][3], cgap[MAXC], cmu[MAXC];
-    int cb0[MAXC], cb1[MAXC];
+    float cx[MAXC][3], cn[MAXC][3], cgap[MAXC];  // slot: point about o (a joint limit: its row), normal, gap
+    int cbb[MAXC];                                // slot: body0 | (body1 + 2) << 8
     float lam[W];  // impulses of the last solve (lane = row): the warm-start cache and the forces
     float cf[NB][3];
     float dforce[ND];
     float root_pos[3], root_q[4];
     float qloc[NB][4];  // each joint's local rotation exp(q_b), from the kinematics (reused by integrate)
     int nc, nterr;                 // contact slots, of which limits + terrain (slots [0, nterr))
-    int nlim;                      // joint-limit slots [0, nlim)
+    int nlim;                      // joint-limit slots [0, nlim) (one row each: rows [0, nlim))
     uint32_t limmask;              // bodies whose joint-angle limit row is emitted this substep
     int ncand;                     // contacts generated (dropped = ncand - nc), last substep
     alignas(8) int imbook[14];     // fused imitation: the env's bookkeeping + motion metadata (ImitBook)
-    int ckey[MAXC];                // warm-start key of each slot (he_sim_params cache layout)
-    int wckey[MAXC];               // the previous solve's keys (its impulses: lam)
-    int nwc;                       // slots cached in wckey / lam
+    int ckey[MAXC];                // 16-bit key of each slot's normal row (include/humanoid_engine.h)
+    int wckey[W];                  // the previous solve's row keys (its impulses: lam)
+    int nwc;                       // rows cached in wckey / lam
     int8_t tbase[NB], tcnt[NB];    // body b's terrain contacts: slots tbase[b] .. + tcnt[b]
-    float4 bsph[NB];               // per-body bounding sphere of the collision segment (cull)
+    int8_t srow0[MAXC];            // first solver row of each slot
+    int8_t rslot[W], rkind[W];     // solver row -> its slot, its kind (0 normal / limit, 1 2 tangential, 3 torsional)
     BodyTopo T;
 };
 
@@ -94,14 +96,8 @@ struct Lds {
 #ifndef HE_PRIO_FACTOR
 #define HE_PRIO_FACTOR 3
 #endif
-#ifndef HE_BIAS_FROM_V  // +0.5%, but its different rounding pushes one chaotic sampled env past the
-#define HE_BIAS_FROM_V 0  // full-size parity tolerance (r01): off
-#endif
 #ifndef HE_DELASSUS48
 #define HE_DELASSUS48 1
-#endif
-#ifndef HE_ONE_SWEEP
-#define HE_ONE_SWEEP 1
 #endif
 #ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
 #define HE_PRED_LEVELS 0
@@ -224,11 +220,10 @@ HE_DEV bool angle_row(f3 th, f3 u, const he_sim_params& p, float& gap, f3& dir) 
     return t >= 1e-6f && gap < p.limit_margin + p.dt * fmaxf(closing, 0.f);
 }
 
-// The substep's limit rows (gap, row over the joint's dofs) per joint b - 1, from the kinematics to
-// the contact phase, kept in the friction-basis arrays: those are dead from the previous substep's
-// forces until this substep's friction-basis pass, which runs after the limit slots are stored.
-HE_DEV float* limit_rows(Lds& L) { return &L.ct1[0][0]; }
-static_assert(4 * (NB - 1) <= 6 * MAXC, "the limit rows fit the ct1 / ct2 arrays");
+// the bodies' bounding spheres of the self-collision cull, in the RNEA acceleration scratch (dead
+// from the midpoint bias until the next substep's kinematics)
+HE_DEV float4* bsph(Lds& L) { return reinterpret_cast<float4*>(&L.Acc[0][0]); }
+static_assert(sizeof(float4) * NB <= sizeof(float) * 6 * NB, "bounding spheres fit the Acc scratch");
 // Backstop when the limit rows lose (oracle/he_oracle_physics.c limit_clamp): a limit against a
 // deep self contact has no solution, and a joint near 100 rad/s can cross the margin in one
 // substep. nq = exp(q_old) (x) exp(dt w) before the log (exp(q_old) has w >= 0: the kinematics'
@@ -257,20 +252,16 @@ HE_DEV bool limit_clamp(f4 nq, f3& nv, float (&w)[3]) {
     return true;
 }
 
-// The next substep's limit rows from joint b's exp map th and velocity u (lane = body b; every
-// lane calls, the root and lanes >= NB with on = false): which rows are emitted, their gap and
-// direction, read by the drive terms (a joint on its limit cannot give way) and by the contact
-// phase (the limit slots). Evaluated where q and u are set -- the state load, then each
-// integration but the last -- so no substep re-reads them for it.
+// Which joints emit their limit row in the next substep, from joint b's exp map th and velocity u
+// (lane = body b; every lane calls, the root and lanes >= NB with on = false), read by the drive
+// terms (a joint on its limit cannot give way). Evaluated where q and u are set -- the state load,
+// then each integration but the last; the contact phase re-evaluates the rows themselves from the
+// same L.q / L.u0 (bit-identical inputs, the same decision).
 HE_DEV void limit_detect(Lds& L, int lane, bool joint, f3 th, f3 u, const he_sim_params& sp) {
     float lg = 0.f;
     f3 ld = f3{0.f, 0.f, 0.f};
     const bool on = joint && angle_row(th, u, sp, lg, ld);
     const uint64_t bm = __ballot(on);
-    if (on) {
-        float* lr = limit_rows(L) + 4 * (lane - 1);
-        lr[0] = lg; lr[1] = -ld.x; lr[2] = -ld.y; lr[3] = -ld.z;  // the row is -q^
-    }
     if (lane == 0) L.limmask = (uint32_t)bm;
 }
 
@@ -357,14 +348,15 @@ template <int S>
 HE_DEV float swizzle_xor(float v) {
     return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (S << 10)));
 }
-HE_DEV void store_contact(Lds& L, int slot, int b0, int b1, f3 x, f3 n, float gap, float mu) {
-    L.cb0[slot] = b0;
-    L.cb1[slot] = b1;
+HE_DEV void store_contact(Lds& L, int slot, int b0, int b1, f3 x, f3 n, float gap, int key) {
+    L.cbb[slot] = b0 | ((b1 + 2) << 8);
     L.cx[slot][0] = x.x; L.cx[slot][1] = x.y; L.cx[slot][2] = x.z;
-    L.cn[slot][0] = n.x; L.cn[slot][1] = n.y; L.cn[slot][2] = n.z;  // friction basis: one pass, lane = contact
+    L.cn[slot][0] = n.x; L.cn[slot][1] = n.y; L.cn[slot][2] = n.z;
     L.cgap[slot] = gap;
-    L.cmu[slot] = mu;
+    L.ckey[slot] = key;
 }
+// 16-bit row keys (include/humanoid_engine.h cache layout)
+HE_DEV int row_key(int b0, int b1, int sub, int kind) { return b0 | ((b1 + 2) << 5) | (sub << 10) | (kind << 14); }
 
 // ordered multiply / multiply-add (volatile asm keeps program order against the surrounding LDS
 // reads, so the unrolled sweeps do not hoist every load ahead of the arithmetic)
@@ -569,38 +561,30 @@ HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uin
     }
 }
 
-// one Gauss-Seidel sweep over the contacts: normal row clamped at 0, friction rows to the pyramid
-// |lambda_t| <= mu lambda_n, in delta form. Lane r holds cd_r = -w_r / A[r][r] (the unconstrained
-// impulse change of row r), lambda_r as of the sweep's start and the negated scaled Delassus
-// column acolp[R] = -A[R][r] / A[r][r]. Row R's change is the clamp of cd_R against the bounds
-// shifted by lambda_R (max(cd, -lambda) for a normal row), so the dependent chain per row is
-// clamp -> v_readlane -> fma: the change d goes to every lane's cd += acolp[R] * d and into lane
-// R of dvec; lambda += dvec once per sweep. The friction bounds mu (lambda_n + d_n) -+ lambda
-// are two fmas on the normal row's d from bases formed at the sweep's start (off the chain).
-template <int CI>
-HE_DEV void pgs_sweep(float& cd, float& dvec, const float& lamv, const float (&acolp)[MAXR], float muL, int nc) {
-    if constexpr (CI < MAXC) {
-        if (CI >= nc) return;
-        constexpr int R0 = 3 * CI;
-        // bounds of this contact's friction rows: mu lambda_n(start) -+ lambda_row, per lane
-        const float lnold = regla::rdlane(lamv, R0);
-        const float hb = fmaf(muL, lnold, -lamv), lbs = fmaf(-muL, lnold, -lamv);
-        // normal row
-        // (each change's v_writelane into dvec is issued after the fma that the next row waits on)
-        float cn;  // max(cd, -lambda): one v_max (no NaN-quieting canonicalize pair)
-        asm("v_max_f32 %0, %1, %2" : "=v"(cn) : "v"(cd), "v"(-lamv));
-        const float dn = regla::rdlane(cn, R0);
-        cd = fmaf(acolp[R0], dn, cd);
-        const float hi = fmaf(muL, dn, hb), lo = fmaf(-muL, dn, lbs);
-        dvec = regla::wrlane<R0>(dn, dvec);
-        // friction rows
-        const float d1 = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R0 + 1);
-        cd = fmaf(acolp[R0 + 1], d1, cd);
-        dvec = regla::wrlane<R0 + 1>(d1, dvec);
-        const float d2 = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R0 + 2);
-        cd = fmaf(acolp[R0 + 2], d2, cd);
-        dvec = regla::wrlane<R0 + 2>(d2, dvec);
-        pgs_sweep<CI + 1>(cd, dvec, lamv, acolp, muL, nc);
+// one Gauss-Seidel sweep over the solver rows (patch friction, oracle build_rows), in delta form.
+// Lane r holds cd_r = -w_r / A[r][r] (the unconstrained impulse change of row r), its bounds on the
+// change [lo_r, hi_r] and the negated scaled Delassus column acolp[R] = -A[R][r] / A[r][r]: a normal
+// row [-lambda_r, +inf), a friction row the bound B_r = muw_r x (its patch's normal impulses) shifted
+// by its own impulse, [-B_r - lambda_r, B_r - lambda_r] (lambda as of the sweep's start). Row R's
+// change is its clamp, so the dependent chain per row is med3 -> v_readlane -> fma: the change d goes
+// to every lane's cd += acolp[R] d and into lane R of dvec; lambda += dvec once per sweep. When R is
+// a normal row of lane r's patch (bit R of the lane's patch mask), lane r's bounds widen by muw_r d
+// right away -- the patch's normal rows come before its friction rows, so a friction row sees this
+// sweep's normal impulses (Gauss-Seidel, as the oracle's bound from the current impulses).
+template <int R>
+HE_DEV void pgs_sweep(float& cd, float& dvec, float& lo, float& hi, const float (&acolp)[MAXR], uint32_t mlo,
+                      uint32_t mhi, float muw, int nr) {
+    if constexpr (R < MAXR) {
+        if (R >= nr) return;
+        const float d = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R);
+        cd = fmaf(acolp[R], d, cd);
+        dvec = regla::wrlane<R>(d, dvec);
+        // muw where bit R of the patch mask is set, else 0: a sign-extended bit field as an AND mask
+        const int sel = __builtin_amdgcn_sbfe((int)(R < 32 ? mlo : mhi), R & 31, 1);
+        const float kk = __int_as_float(sel & __float_as_int(muw));
+        hi = fmaf(kk, d, hi);
+        lo = fmaf(-kk, d, lo);
+        pgs_sweep<R + 1>(cd, dvec, lo, hi, acolp, mlo, mhi, muw, nr);
     }
 }
 
@@ -1542,26 +1526,16 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         factor_lds_groups<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
 #endif
         __builtin_amdgcn_s_setprio(0);
-        L.Dinv[lane] = 1.0f / Dl;
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
-        if (lane < NH) { L.Dinv[64 + lane] = 1.0f / D2; L.sDinv[64 + lane] = 1.0f / sqrtf(D2); }
-#if HE_ONE_SWEEP
+        if (lane < NH) L.sDinv[64 + lane] = 1.0f / sqrtf(D2);
         // the free velocity is not formed here: the contact bias takes z.u0 + zh.yh, and one L^-1
         // sweep after the solver gives uf = u0 + L^-1 D^-1/2 (yh + Zh^T lambda)
         L.yh[lane] = yl * (1.0f / sqrtf(Dl));
         if (lane < NH) L.yh[64 + lane] = y2 * (1.0f / sqrtf(D2));
-#else
-        yl *= 1.0f / Dl;
-        y2 = lane < NH ? y2 * (1.0f / D2) : 0.f;
-#endif
     }
     sync();
     STAMP(5);
-#if HE_ONE_SWEEP
     if (HE_BIAS_PREDICTOR && p.bias_midpoint) bias_midpoint(L, T, lane, p, stamps, t_prev);
-#else
-#error "the midpoint bias is implemented on the one-sweep path (HE_ONE_SWEEP=1)"
-#endif
     // the contact phase's model reads (geometry of the lane's body, self-collision pair indices)
     // depend on nothing computed here: issued now, they land behind the free-velocity sweep
     constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
@@ -1586,20 +1560,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             if (pi >= npairs) prs[rd].x = -1;
         }
     }
-    // ---- free velocity uf = u0 + L^-1 D^-1 L^-T (dt*rhs): the L^-1 sweep
-#if !HE_ONE_SWEEP
-    {
-        float r1[regla::kRowRegs], r2[regla::kRowRegs];
-        load_rows(L, T, lane, r1, r2);
-        STAMP(22);
-        __builtin_amdgcn_s_setprio(HE_PRIO_SOLVE);
-        solve_L(r1, r2, lane, yl, y2);
-        __builtin_amdgcn_s_setprio(0);
-        STAMP(23);
-        L.uf[lane] = L.u0[lane] + yl;
-        if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
-    }
-#endif
     sync();
     STAMP(6);
     // ---- contact slots: joint limits, terrain (bodies in order, box corners deepest-first), self
@@ -1616,17 +1576,21 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     static_assert(kCand <= NG * 6, "candidate gaps fit the IS scratch");
     // the previous solve's impulses (lane = row) before the self-pair list reuses L.lam as scratch
     const float lam_prev = L.lam[lane];
-    // -- joint-angle limit slots (lane = joint b - 1)
+    // -- joint-angle limit slots (lane = joint b - 1): the rows limit_detect flagged, re-evaluated
+    // from the same state words
     int nlim = 0, nlim_all = 0;
     if (p.joint_limits) {
         const uint32_t lm = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.limmask);
         const bool act = lane < NB - 1 && ((lm >> (lane + 1)) & 1u);
         const int pre = wave_prefix(act, lane, nlim_all);
         if (act && pre < maxc) {
-            // the row over the joint's dofs travels in the contact position (unused by a limit)
-            const float* lr = limit_rows(L) + 4 * lane;
-            store_contact(L, pre, lane + 1, -2, f3{lr[1], lr[2], lr[3]}, f3{0.f, 0.f, 1.f}, lr[0], 0.f);
-            L.ckey[pre] = (lane + 1) | (7 << 16);
+            const int j = lane < NB - 1 ? lane : 0;
+            float lg;
+            f3 ld;
+            angle_row(f3{L.q[3 * j], L.q[3 * j + 1], L.q[3 * j + 2]}, f3{L.u0[6 + 3 * j], L.u0[7 + 3 * j], L.u0[8 + 3 * j]},
+                      p, lg, ld);
+            // the row over the joint's dofs (-q^) travels in the contact position (unused by a limit)
+            store_contact(L, pre, lane + 1, -2, ld * -1.f, f3{0.f, 0.f, 1.f}, lg, row_key(lane + 1, -2, 7, 0));
         }
         nlim = nlim_all < maxc ? nlim_all : maxc;
     }
@@ -1681,7 +1645,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float* sg = L.Ib[lane];
             sg[0] = P0.x; sg[1] = P0.y; sg[2] = P0.z; sg[3] = P1.x; sg[4] = P1.y; sg[5] = P1.z; sg[6] = rs;
             const f3 mid = (P0 + P1) * 0.5f;
-            L.bsph[lane] = make_float4(mid.x, mid.y, mid.z, 0.5f * norm3(P1 - P0) + rs);
+            bsph(L)[lane] = make_float4(mid.x, mid.y, mid.z, 0.5f * norm3(P1 - P0) + rs);
         }
         // a corner lane's point: ((Pc +- ex) +- ey) +- ez, signs by the bits of c
         f3 X0 = P0;
@@ -1737,6 +1701,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     };
     // the contact key's sub-index: the point's index on its body (a box's corner index)
     auto sub_of = [&](int ci) { return corner ? cc : ci; };
+    // candidate gaps and bodies for the reduction (IS scratch: gaps [0, kCand), bodies (-1: a self
+    // pair) [kCand, 2 kCand), the rank order [2 kCand, 3 kCand))
+    int* gb = reinterpret_cast<int*>(gl + kCand);
+    int* gord = reinterpret_cast<int*>(gl + 2 * kCand);
+    static_assert(3 * kCand <= NG * 6, "reduction scratch fits IS");
+    int rows_terr = 0;  // solver rows of every terrain candidate kept (patch friction)
     {
         terr_all = terrain_candidates();
         STAMP(16);
@@ -1745,13 +1715,15 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         for (int ci = 0; ci < kPts; ++ci) {
             if (cand[ci] && rank[ci] < 4) {
                 const int k = base + rank[ci];
-                if (k < kCand) gl[k] = cd[ci];
-                if (nlim + k < maxc) {
-                    store_contact(L, nlim + k, tb_, -1, cxs[ci], cns[ci], cd[ci], mu);
-                    L.ckey[nlim + k] = tb_ | (1 << 8) | (sub_of(ci) << 16);
-                }
+                if (k < kCand) { gl[k] = cd[ci]; gb[k] = tb_; }
+                if (nlim + k < maxc)
+                    store_contact(L, nlim + k, tb_, -1, cxs[ci], cns[ci], cd[ci], row_key(tb_, -1, sub_of(ci), 0));
             }
         }
+        // rows of the body's patch: k points, k normal rows + 2 tangential (+ 1 torsional from k = 2)
+        const int pr = myn == 0 ? 0 : myn + (myn >= 2 ? 3 : 2);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) rows_terr += __popcll(__ballot((pr >> k) & 1)) << k;
         nc = nlim + terr_all < maxc ? nlim + terr_all : maxc;
         if (lane < NB) {  // the body's slot range, for the per-body force sums
             const int s0 = nlim + base;
@@ -1774,7 +1746,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 const int i = prs[rd].x, j = prs[rd].y;
                 bool need = false;
                 if (i >= 0) {
-                    const float4 bi = L.bsph[i], bj = L.bsph[j];
+                    const float4 bi = bsph(L)[i], bj = bsph(L)[j];
                     const f3 d = f3{bi.x - bj.x, bi.y - bj.y, bi.z - bj.z};
                     const float lim = bi.w + bj.w + off + 1e-3f;
                     need = dot3(d, d) < lim * lim;
@@ -1825,25 +1797,23 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     };
     if (self_col) {
         self_all = self_pairs([&](bool hit, int i, int j, f3 px, f3 pn, float pgap, int k) {
-            if (hit && k < kCand) gl[k] = pgap;
-            if (hit && nlim + k < maxc) {
-                store_contact(L, nlim + k, i, j, px, pn, pgap, mu);
-                L.ckey[nlim + k] = i | ((j + 2) << 8);
-            }
+            if (hit && k < kCand) { gl[k] = pgap; gb[k] = -1; }
+            if (hit && nlim + k < maxc) store_contact(L, nlim + k, i, j, px, pn, pgap, row_key(i, j, 0, 0));
         });
         nc = nlim + terr_all + self_all < maxc ? nlim + terr_all + self_all : maxc;
     }
     const int ncand_all = nlim_all + terr_all + self_all;
-    if (nlim + terr_all + self_all > maxc && nlim < maxc) {
-        // ---- overflow (rare, wave-uniform): keep the `keep` deepest contacts, in slot order
+    if ((nlim + terr_all + self_all > maxc || nlim + rows_terr + 3 * self_all > MAXR) && nlim < maxc) {
+        // ---- overflow (rare, wave-uniform): past the slots or the solver rows. The contacts are
+        // taken deepest first (smallest gap, ties in slot order), each kept while its rows still fit
+        // (a self pair or a body's first terrain point 3, its second 2, 1 after: oracle gen_contacts),
+        // and the kept ones are regenerated in slot order
         sync();
         const int keep = maxc - nlim;
         const int T = terr_all + self_all < kCand ? terr_all + self_all : kCand;
-        uint64_t km[2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < 2; ++h) {  // each candidate's depth rank -> the rank order
             const int k = h * W + lane;
-            bool kept = false;
             if (k < T) {
                 const float gk = gl[k];
                 int r = 0;
@@ -1851,9 +1821,28 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float g2 = gl[jj];
                     r += (g2 < gk || (g2 == gk && jj < k)) ? 1 : 0;
                 }
-                kept = r < keep;
+                gord[r] = k;
             }
-            km[h] = __ballot(kept);
+        }
+        sync();
+        // the greedy pass in rank order (wave-uniform): candidate and body from registers by
+        // v_readlane, the kept points per body in lane = body
+        const int ko0 = lane < T ? gord[lane] : 0, ko1 = W + lane < T ? gord[W + lane < kCand ? W + lane : 0] : 0;
+        const int kb0 = gb[ko0], kb1 = gb[ko1];
+        uint64_t km[2] = {0ull, 0ull};
+        int rows = nlim, kept_n = 0, pcnt = 0;
+        for (int q = 0; q < T; ++q) {
+            const int k = q < W ? __builtin_amdgcn_readlane(ko0, q & (W - 1)) : __builtin_amdgcn_readlane(ko1, q & (W - 1));
+            const int b = q < W ? __builtin_amdgcn_readlane(kb0, q & (W - 1)) : __builtin_amdgcn_readlane(kb1, q & (W - 1));
+            const int pc = b >= 0 ? __builtin_amdgcn_readlane(pcnt, b) : 0;
+            const int cost = b < 0 ? 3 : (pc == 0 ? 3 : (pc == 1 ? 2 : 1));
+            if (kept_n < keep && rows + cost <= MAXR) {
+                rows += cost;
+                ++kept_n;
+                pcnt += lane == b ? 1 : 0;
+                if (k < W) km[0] |= 1ull << (k & (W - 1));
+                else km[1] |= 1ull << (k & (W - 1));
+            }
         }
         auto before = [&](int k) {  // kept candidates below index k
             const uint64_t lo = k >= W ? km[0] : (k <= 0 ? 0ull : km[0] & ((~0ull) >> (W - k)));
@@ -1866,11 +1855,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         for (int ci = 0; ci < kPts; ++ci) {
             if (cand[ci] && rank[ci] < 4) {
                 const int k = base + rank[ci];
-                if (is_kept(k)) {
-                    const int slot = nlim + before(k);
-                    store_contact(L, slot, tb_, -1, cxs[ci], cns[ci], cd[ci], mu);
-                    L.ckey[slot] = tb_ | (1 << 8) | (sub_of(ci) << 16);
-                }
+                if (is_kept(k))
+                    store_contact(L, nlim + before(k), tb_, -1, cxs[ci], cns[ci], cd[ci], row_key(tb_, -1, sub_of(ci), 0));
             }
         }
         if (lane < NB) {
@@ -1881,11 +1867,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         if (lane == 0) L.nterr = nlim + before(terr_all);
         if (self_col) {
             self_pairs([&](bool hit, int i, int j, f3 px, f3 pn, float pgap, int k) {
-                if (hit && is_kept(k)) {
-                    const int slot = nlim + before(k);
-                    store_contact(L, slot, i, j, px, pn, pgap, mu);
-                    L.ckey[slot] = i | ((j + 2) << 8);
-                }
+                if (hit && is_kept(k)) store_contact(L, nlim + before(k), i, j, px, pn, pgap, row_key(i, j, 0, 0));
             });
         }
         nc = nlim + before(T);
@@ -1894,113 +1876,160 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     if (lane == 0) { L.nc = nc; L.nlim = nlim; L.ncand = ncand_all; }
     if (lane < NB) { L.cf[lane][0] = 0.f; L.cf[lane][1] = 0.f; L.cf[lane][2] = 0.f; }
     sync();
-    if (lane < nc) {  // tangent basis of every contact at once (lane = contact)
-        f3 t1, t2;
-        friction_basis(f3{L.cn[lane][0], L.cn[lane][1], L.cn[lane][2]}, t1, t2);
-        L.ct1[lane][0] = t1.x; L.ct1[lane][1] = t1.y; L.ct1[lane][2] = t1.z;
-        L.ct2[lane][0] = t2.x; L.ct2[lane][1] = t2.y; L.ct2[lane][2] = t2.z;
+    // ---- solver rows (patch friction, oracle build_rows), lane = slot: a joint limit 1 row, a point
+    // its normal row, the last point of a body's terrain patch then the patch's 2 tangential rows
+    // (+ 1 torsional from 2 points on), a self pair its normal and 2 tangential rows; the row table
+    // (row -> slot, kind) by the slots' exclusive prefix
+    int nr = 0;
+    {
+        const bool on = lane < nc;
+        const int bb = on ? L.cbb[lane < MAXC ? lane : 0] : 0;
+        const int b0 = bb & 0xFF, b1 = (bb >> 8) - 2;
+        int cost = 0;
+        if (on) {
+            if (b1 == -2) cost = 1;
+            else if (b1 >= 0) cost = 3;
+            else {
+                const int tn = L.tcnt[b0];
+                cost = lane == L.tbase[b0] + tn - 1 ? 1 + (tn >= 2 ? 3 : 2) : 1;
+            }
+        }
+        int start = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint64_t bm = __ballot((cost >> k) & 1);
+            start += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << k;
+            nr += __popcll(bm) << k;
+        }
+        if (on) {
+            L.srow0[lane < MAXC ? lane : 0] = (int8_t)start;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cost) { L.rslot[start + k] = (int8_t)lane; L.rkind[start + k] = (int8_t)k; }
+        }
     }
     sync();
     STAMP(7);
-    // ---- warm start: the previous solve's impulse of each row's contact key (lane c matches its
-    // slot's key against the old keys by readlane, row lanes fetch the index and the impulse)
+    // ---- each row's Jacobian data (lane = row): slot, kind, bodies; a friction row's patch (a
+    // body's terrain points [tbase, tbase + tcnt), or the self pair alone): normal = the normalised
+    // sum of the points' normals, the tangent basis of it, the points' centroid, the torsion radius
+    // (mean tangential distance of the points from the centroid); its normal rows n0 .. n0 + cnt - 1
+    // as a lane mask, its bound weight muw (mu, or mu r for the torsional row), its 16-bit key
+    const bool act = lane < nr;
+    const int rs_ = act ? L.rslot[lane] : 0;
+    const int kind = act ? L.rkind[lane] : 0;
+    const int rbb = L.cbb[rs_];
+    const int rb0 = rbb & 0xFF, rb1 = (rbb >> 8) - 2;
+    f3 dd, rho;
+    float muw = 0.f;
+    uint32_t mlo = 0u, mhi = 0u;
+    int rkey;
+    {
+        const f3 xs = f3{L.cx[rs_][0], L.cx[rs_][1], L.cx[rs_][2]};
+        const f3 ns = f3{L.cn[rs_][0], L.cn[rs_][1], L.cn[rs_][2]};
+        const bool terr = rb1 == -1;
+        const int p0 = terr ? L.tbase[rb0] : rs_;
+        const int pc = terr ? L.tcnt[rb0] : 1;
+        f3 px[4];
+        f3 np = f3{0.f, 0.f, 0.f}, xp = f3{0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int sj = j < pc ? p0 + j : p0;
+            px[j] = f3{L.cx[sj][0], L.cx[sj][1], L.cx[sj][2]};
+            if (j < pc) {
+                np = np + f3{L.cn[sj][0], L.cn[sj][1], L.cn[sj][2]};
+                xp = xp + px[j];
+            }
+        }
+        np = np * (1.0f / norm3(np));
+        xp = xp * (1.0f / (float)pc);
+        float rp = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f3 d = px[j] - xp;
+            const f3 tg = d - np * dot3(d, np);
+            if (j < pc) rp += norm3(tg);
+        }
+        rp *= 1.0f / (float)pc;
+        f3 t1, t2;
+        friction_basis(np, t1, t2);
+        dd = kind == 0 ? ns : (kind == 1 ? t1 : (kind == 2 ? t2 : f3{0.f, 0.f, 0.f}));
+        rho = kind == 3 ? np : cross3(kind == 0 ? xs : xp, dd);  // contact points about o
+        if (act && kind > 0) {
+            muw = kind == 3 ? mu * rp : mu;
+            const int n0 = lane - (kind - 1) - pc;
+            const uint64_t pm = ((1ull << pc) - 1ull) << n0;
+            mlo = (uint32_t)pm;
+            mhi = (uint32_t)(pm >> 32);
+        }
+        const int k0 = L.ckey[rs_];
+        rkey = kind == 0 ? k0 : ((terr ? row_key(rb0, -1, HE_KEY_PATCH, 0) : k0) | (kind << 14));
+        // the row's linear direction for the reported forces (IS scratch, read after the solve; a
+        // joint limit's and a torsional row's: none)
+        if (act) {
+            float* fr = gl + 2 * kCand;
+            const bool none = rb1 == -2;
+            fr[3 * lane] = none ? 0.f : dd.x;
+            fr[3 * lane + 1] = none ? 0.f : dd.y;
+            fr[3 * lane + 2] = none ? 0.f : dd.z;
+        }
+    }
+    static_assert(2 * kCand + 3 * W <= NG * 6, "per-row force directions fit IS");
+    // ---- warm start: the previous solve's impulse of each row's key (lane r matches its key against
+    // the old keys by readlane and fetches the impulse)
     float lam0 = 0.f;
     {
         const int nw = __builtin_amdgcn_readfirstlane(L.nwc);
-        if (nw > 0 && nc > 0) {
-            const int wk = lane < nw ? L.wckey[lane < MAXC ? lane : 0] : -1;
-            const int ck = lane < nc ? L.ckey[lane < MAXC ? lane : 0] : -2;
-            const int nr = 3 * nc;
-            if (nw == nc && __ballot(lane < nc && wk != ck) == 0ull) {
-                lam0 = lane < nr ? lam_prev : 0.f;  // the same contacts in the same slots (at rest)
+        if (nw > 0 && nr > 0) {
+            const int wk = lane < nw ? L.wckey[lane] : -1;
+            const int ck = act ? rkey : -2;
+            if (nw == nr && __ballot(act && wk != ck) == 0ull) {
+                lam0 = act ? lam_prev : 0.f;  // the same rows in the same order (at rest)
             } else {
                 int src = -1;
                 for (int j = 0; j < nw; ++j) {
                     const int kj = __builtin_amdgcn_readlane(wk, j);
                     src = (src < 0 && kj == ck) ? j : src;
                 }
-                const int r = lane < nr ? lane : 0;
-                const int ci = r / 3, kind = r - 3 * ci;
-                const int srow = __shfl(src, ci, W);
-                const float v = __shfl(lam_prev, srow >= 0 ? 3 * srow + kind : 0, W);
-                lam0 = (lane < nr && srow >= 0) ? v : 0.f;
+                const float v = __shfl(lam_prev, src >= 0 ? src : 0, W);
+                lam0 = (act && src >= 0) ? v : 0.f;
             }
         }
+        // the old keys are matched: this solve's row keys replace them (the next solve's warm start)
+        L.wckey[lane] = act ? rkey : -1;
     }
-    if (nc > 0) {
+    if (nr > 0) {
         // ---- contact rows, one per lane: z = J_r^T, brow = J_r uf + bias, then z <- D^-1/2 L^-T z
         // (dofs outside every row's support stay zero and are skipped wave-uniformly), so that the
         // Delassus operator A = Zh Zh^T is a plain Gram matrix of the lanes' registers
-        const int nr = 3 * nc;
         float brow = 0.f, diag = 0.f, lamv = 0.f;
         float acol[MAXR];  // lane c: A[r][c]
         regla::ZVec z;     // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
         {
-            const int r = lane < nr ? lane : 0;
-            const int ci = r / 3, kind = r - 3 * ci;
-            const float* dir = kind == 0 ? L.cn[ci] : (kind == 1 ? L.ct1[ci] : L.ct2[ci]);
-            const uint32_t anc0 = lane < nr ? T.anc_mask[L.cb0[ci]] : 0u;
-            const uint32_t anc1 = (lane < nr && L.cb1[ci] >= 0) ? T.anc_mask[L.cb1[ci]] : 0u;
-            const f3 dd = f3{dir[0], dir[1], dir[2]};
-            const f3 rho = cross3(f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]}, dd);  // contact points about o
+            const uint32_t anc0 = act ? T.anc_mask[rb0] : 0u;
+            const uint32_t anc1 = (act && rb1 >= 0) ? T.anc_mask[rb1] : 0u;
             // bodies on some row's support (wave-uniform): the only ones whose dofs can be nonzero
             const uint32_t lb = wave_or(anc0 | anc1);
-            // z = J_r^T and brow = J_r uf, four dofs per pinned group (their LDS reads overlap; the
-            // results are fixed in place so the loads cannot all be hoisted ahead of the math)
+            // z = J_r^T and brow = J_r u0 on the matrix cores
             float bacc[4] = {0.f, 0.f, 0.f, 0.f};
-#if HE_JT_MFMA
             zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane, nr <= 32);
-            // joint-limit slots: the normal row is the stored row over the joint's three dofs (its
-            // support is the joint's ancestor chain, anc0), the two friction rows are zero
-            const bool limrow = lane < nr && L.cb1[ci] == -2;
+            // joint-limit rows: the stored row over the joint's three dofs (its support is the joint's
+            // ancestor chain, anc0)
+            const bool limrow = act && rb1 == -2;
             if (__ballot(limrow)) {  // wave-uniform
-                const int bl = limrow ? L.cb0[ci] : 0;
-                const float g3[3] = {kind == 0 ? L.cx[ci][0] : 0.f, kind == 0 ? L.cx[ci][1] : 0.f,
-                                     kind == 0 ? L.cx[ci][2] : 0.f};
+                const int bl = limrow ? rb0 : 0;
+                const float g3[3] = {L.cx[rs_][0], L.cx[rs_][1], L.cx[rs_][2]};
 #pragma unroll
                 for (int i = 0; i < NG; ++i) {
                     const float v = i < 6 ? 0.f : (bl == (i < 6 ? 0 : (i - 6) / 3 + 1) ? g3[i < 6 ? 0 : (i - 6) % 3] : 0.f);
                     ZV(z, i) = limrow ? v : ZV(z, i);
                 }
             }
-#if HE_ONE_SWEEP && HE_BIAS_FROM_V
-            {
-                // J_r u0 = (rho, dd) . (V_b0 - V_b1): the contact bodies' spatial velocities about o
-                // from the kinematics (V_b = sum over the chain of S_i u0_i), not a 75-dof dot product
-                const int b0i = lane < nr ? L.cb0[ci] : 0, b1i = lane < nr ? L.cb1[ci] : -1;
-                const float* V0 = L.V[b0i];
-                const float* V1 = L.V[b1i >= 0 ? b1i : 0];
-                const float s1 = b1i >= 0 ? 1.f : 0.f;
-                const float u6[6] = {rho.x, rho.y, rho.z, dd.x, dd.y, dd.z};
 #pragma unroll
-                for (int x = 0; x < 6; ++x) bacc[x & 3] = fmaf(u6[x], V0[x] - s1 * V1[x], bacc[x & 3]);
-                if (lane >= nr) bacc[0] = bacc[1] = bacc[2] = bacc[3] = 0.f;
-            }
-#else
-#pragma unroll
-            for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), HE_ONE_SWEEP ? L.u0[i] : L.uf[i], bacc[i & 3]);  // J_r u
-#endif
-#else
-#error "joint-limit rows and the warm start are implemented on the MFMA J^T path (HE_JT_MFMA=1)"
-            {
-                // root: S = unit axes, so z = sgn0 * (rho, dd)
-                const float s0 = (float)(anc0 & 1u) - (float)(anc1 & 1u);
-                ZV(z, 0) = s0 * rho.x; ZV(z, 1) = s0 * rho.y; ZV(z, 2) = s0 * rho.z;
-                ZV(z, 3) = s0 * dd.x; ZV(z, 4) = s0 * dd.y; ZV(z, 5) = s0 * dd.z;
-            }
-            for (int i = 0; i < 6; ++i) bacc[i & 3] = fmaf(ZV(z, i), L.uf[i], bacc[i & 3]);
-            const f3 cx = f3{L.cx[ci][0], L.cx[ci][1], L.cx[ci][2]};
-            {
-                float cur[15];
-                if ((lb >> 1) & 1u) zrow_load(L, 1, cur);
-                else
-                    for (int x = 0; x < 15; ++x) regla::undef_reg(cur[x]);
-                zrow_bodies<1>(z, bacc, lb, anc0, anc1, cx, dd, L, cur);
-            }
-#endif
+            for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), L.u0[i], bacc[i & 3]);  // J_r u0
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
-            if (lane < nr && kind == 0) {
-                const float g = L.cgap[ci];
+            if (act && kind == 0) {
+                const float g = L.cgap[rs_];
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             STAMP(20);
@@ -2015,7 +2044,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #pragma unroll
             for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(ZV(z, i), ZV(z, i), dacc[i & 3]);
             diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
-#if HE_ONE_SWEEP
             {  // J_r (uf - u0) = zh_r . yh, yh_i broadcast from lane i (v_readlane: no LDS loads to
                // hoist into registers at the phase's register peak)
                 const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
@@ -2025,7 +2053,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     yacc[i & 3] = fmaf(ZV(z, i), regla::rdlane(i < 64 ? yhl : yh2, i & 63), yacc[i & 3]);
                 brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
             }
-#endif
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
 #pragma unroll
@@ -2040,9 +2067,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             else delassus_mfma(z, acol, live);
         }
         STAMP(9);
-        // ---- projected Gauss-Seidel, pyramidal friction; lane r keeps residual w and impulse lam
+        // ---- projected Gauss-Seidel over the rows (pgs_sweep): lane r keeps its unconstrained change,
+        // its impulse and its bounds
         {
-            const float invd = 1.0f / (lane < nr ? diag + 1e-12f : 1.f);
+            const float invd = 1.0f / (act ? diag + 1e-12f : 1.f);
             // residual at the warm start: w = brow + A lambda0 (acol: lane c holds A[r][c] = A[c][r])
             float w0 = brow;
             if (__ballot(lam0 != 0.f)) {  // wave-uniform; rows >= nr hold no impulse
@@ -2058,28 +2086,52 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 else aw(std::integral_constant<int, MAXR>{});
             }
             lamv = lam0;
-            float cd = lane < nr ? -w0 * invd : 0.f;
+            float cd = act ? -w0 * invd : 0.f;
             const float ninvd = -invd;
 #pragma unroll
             for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
-            const float muL = lane < nr ? L.cmu[lane / 3] : 0.f;
-            const int ncu = __builtin_amdgcn_readfirstlane(nc);
+            // a friction row's bound at the warm start: muw x its patch's normal impulses (<= 4 rows)
+            const bool isn = kind == 0;
+            float bnd = 0.f;
+            if (__ballot(lam0 != 0.f)) {
+                const int n0 = act && !isn ? (int)__builtin_ctzll(((uint64_t)mhi << 32) | mlo) : 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = __shfl(lam0, (n0 + j) & (W - 1), W);
+                    const int bit = n0 + j;
+                    const bool in = bit < 32 ? ((mlo >> (bit & 31)) & 1u) : ((mhi >> (bit & 31)) & 1u);
+                    bnd += in ? v : 0.f;
+                }
+                bnd *= muw;
+            }
+            const float kInf = __builtin_inff();
+            float lo = isn ? -lamv : -bnd - lamv;
+            float hi = isn ? kInf : bnd - lamv;
+            const int nru = __builtin_amdgcn_readfirstlane(nr);
             __builtin_amdgcn_s_setprio(HE_PRIO_PGS);
             const float tol = p.solver_tolerance;
             for (int it = 0; it < p.solver_iterations; ++it) {
                 float dvec = 0.f;
-                pgs_sweep<0>(cd, dvec, lamv, acol, muL, ncu);
+                // the row count through an opaque copy per sweep: the 63 early-exit compares stay
+                // scalar compares in the sweep instead of being hoisted out of the loop as 63
+                // lane-mask pairs (SGPR spills)
+                int nrs = nru;
+                asm volatile("" : "+s"(nrs));
+                pgs_sweep<0>(cd, dvec, lo, hi, acol, mlo, mhi, muw, nrs);
+                // the bound at the sweep's end: B = hi + lambda(start); then the bounds about the new impulse
+                const float bn = hi + lamv;
                 lamv += dvec;
+                lo = isn ? -lamv : -bn - lamv;
+                hi = isn ? kInf : bn - lamv;
                 // converged (optional, solver_tolerance > 0): no row's velocity moved by more than
                 // the tolerance in this sweep, |d lambda_r| A_rr (oracle: the same test)
-                if (tol > 0.f && __ballot(lane < nr && fabsf(dvec) * diag > tol) == 0ull) break;
+                if (tol > 0.f && __ballot(act && fabsf(dvec) * diag > tol) == 0ull) break;
             }
             __builtin_amdgcn_s_setprio(0);
         }
-        // the solve's impulses and keys: the next solve's warm start and the reported forces
-        L.lam[lane] = lane < nr ? lamv : 0.f;
-        if (lane < nc) L.wckey[lane] = L.ckey[lane];
-        if (lane == 0) L.nwc = p.warm_start ? nc : 0;  // warm_start 0: every substep's solve is cold
+        // the solve's impulses and row keys: the next solve's warm start and the reported forces
+        L.lam[lane] = act ? lamv : 0.f;
+        if (lane == 0) L.nwc = p.warm_start ? nr : 0;  // warm_start 0: every substep's solve is cold
         sync();
         STAMP(10);
         // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
@@ -2093,65 +2145,57 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? ZV(z, 64 + i < NG ? 64 + i : 0) * lamv : 0.f;
             float yl = reduce_scatter<64>(v64);
             float y2 = __shfl(reduce_scatter<16>(v16), 4 * (lane & 15), W);
-#if HE_ONE_SWEEP
             yl = (yl + L.yh[lane]) * L.sDinv[lane];
             y2 = lane < NH ? (y2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
-#else
-            yl *= L.sDinv[lane];
-            y2 = lane < NH ? y2 * L.sDinv[64 + lane] : 0.f;
-#endif
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
             load_rows(L, T, lane, r1, r2);
             solve_L(r1, r2, lane, yl, y2);
             __builtin_amdgcn_s_setprio(0);
-#if HE_ONE_SWEEP
             L.uf[lane] = L.u0[lane] + yl;
             if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
-#else
-            L.uf[lane] += yl;
-            if (lane < NH) L.uf[64 + lane] += y2;
-#endif
         }
         // ---- reported contact forces (net linear contact impulse per body / dt): the output is the
         // last substep's, so the earlier substeps skip them (their cf rows stay zero, as set above)
-        float (*fc)[6] = L.Acc;  // per-contact scratch (Acc is dead in the contact phase)
         if (last) {
-        if (lane < nc) {
-            const int c = lane;
-            const float ln = L.lam[3 * c], la = L.lam[3 * c + 1], lb = L.lam[3 * c + 2];
-            fc[c][0] = ln * L.cn[c][0] + la * L.ct1[c][0] + lb * L.ct2[c][0];
-            fc[c][1] = ln * L.cn[c][1] + la * L.ct1[c][1] + lb * L.ct2[c][1];
-            fc[c][2] = ln * L.cn[c][2] + la * L.ct1[c][2] + lb * L.ct2[c][2];
-        }
-        sync();
-        if (lane < NB) {
-            // the body's own terrain contacts (a contiguous slot range, in slot order), then the
-            // self-pair contacts with their sign; the same summation order as over all slots
-            float F3[3] = {0.f, 0.f, 0.f};
-            const int tb = L.tbase[lane], tn = L.tcnt[lane];
+            float* fr = gl + 2 * kCand;  // per-row linear impulses: the stored directions x lambda
+            if (act) {
+                fr[3 * lane] *= lamv;
+                fr[3 * lane + 1] *= lamv;
+                fr[3 * lane + 2] *= lamv;
+            }
+            sync();
+            if (lane < NB) {
+                // the body's own terrain rows (its patch: a contiguous row range, in row order), then
+                // the self-pair rows with their sign; the same summation order as over all rows
+                float F3[3] = {0.f, 0.f, 0.f};
+                const int tn = L.tcnt[lane];
+                const int r0 = tn > 0 ? L.srow0[L.tbase[lane]] : 0;
+                const int rn = tn == 0 ? 0 : tn + (tn >= 2 ? 3 : 2);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (k < tn) {
-                    const int c = tb + k;
-                    for (int x = 0; x < 3; ++x) F3[x] += fc[c][x];
+                for (int k = 0; k < 7; ++k) {
+                    if (k < rn) {
+                        const int r = r0 + k;
+                        for (int x = 0; x < 3; ++x) F3[x] += fr[3 * r + x];
+                    }
                 }
+                const int nterr = __builtin_amdgcn_readfirstlane(L.nterr);
+                for (int c = nterr; c < nc; ++c) {  // wave-uniform bounds
+                    const int cb = L.cbb[c];
+                    const float sg = ((cb & 0xFF) == lane ? 1.f : 0.f) - ((cb >> 8) - 2 == lane ? 1.f : 0.f);
+                    const int r = L.srow0[c];
+                    for (int k = 0; k < 3; ++k)
+                        for (int x = 0; x < 3; ++x) F3[x] += sg * fr[3 * (r + k) + x];
+                }
+                L.cf[lane][0] = F3[0] / dt; L.cf[lane][1] = F3[1] / dt; L.cf[lane][2] = F3[2] / dt;
             }
-            const int nterr = __builtin_amdgcn_readfirstlane(L.nterr);
-            for (int c = nterr; c < nc; ++c) {  // wave-uniform bounds
-                const float sg = (L.cb0[c] == lane ? 1.f : 0.f) - (L.cb1[c] == lane ? 1.f : 0.f);
-                for (int x = 0; x < 3; ++x) F3[x] += sg * fc[c][x];
-            }
-            L.cf[lane][0] = F3[0] / dt; L.cf[lane][1] = F3[1] / dt; L.cf[lane][2] = F3[2] / dt;
-        }
-        sync();
+            sync();
         }  // last
     }
-    if (nc == 0) {  // nothing to warm-start the next solve from
+    if (nr == 0) {  // nothing to warm-start the next solve from
         L.lam[lane] = 0.f;
         if (lane == 0) L.nwc = 0;
     }
-#if HE_ONE_SWEEP
-    if (nc == 0) {  // no contact: uf = u0 + L^-1 D^-1/2 yh
+    if (nr == 0) {  // no contact: uf = u0 + L^-1 D^-1/2 yh
         float yl = L.yh[lane] * L.sDinv[lane];
         float y2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
@@ -2161,7 +2205,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
         sync();
     }
-#endif
     STAMP(11);
     // ---- drive force actually applied, damping, clamps, write velocities
     const float damp = 1.0f / (1.0f + dt * p.angular_damping);
@@ -2170,15 +2213,15 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
         sync();
         // plus the joint-limit force (dof_force = the joint's solver force, drive and limit together;
-        // oracle/he_oracle_physics.c): limit slot c (one per joint) adds g lambda / dt over its joint's
-        // dofs, g = its row (kept in the contact-position words)
+        // oracle/he_oracle_physics.c): limit slot c (one per joint, row c) adds g lambda / dt over its
+        // joint's dofs, g = its row (kept in the contact-position words)
         const int nl = __builtin_amdgcn_readfirstlane(L.nlim);
-        if (lane < nl && nc > 0) {
-            const int d0 = 3 * (L.cb0[lane] - 1);
-            const float lf = L.lam[3 * lane] / dt;
-            L.dforce[d0] += L.cx[lane][0] * lf;
-            L.dforce[d0 + 1] += L.cx[lane][1] * lf;
-            L.dforce[d0 + 2] += L.cx[lane][2] * lf;
+        if (lane < nl && nr > 0) {
+            const int d0 = 3 * ((L.cbb[lane < MAXC ? lane : 0] & 0xFF) - 1);
+            const float lf = L.lam[lane] / dt;
+            L.dforce[d0] += L.cx[lane < MAXC ? lane : 0][0] * lf;
+            L.dforce[d0 + 1] += L.cx[lane < MAXC ? lane : 0][1] * lf;
+            L.dforce[d0 + 2] += L.cx[lane < MAXC ? lane : 0][2] * lf;
         }
         sync();
     }
@@ -2266,7 +2309,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     STAMP(12);
 }
 
-__global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
+// (64, 2): two waves per SIMD, i.e. at most 256 VGPRs + AGPRs; the allocator fits the kernel in them
+// without scratch (unconstrained it parks one kernel-lifetime value in an AGPR at 257 and falls
+// to one wave per SIMD)
+__global__ void __launch_bounds__(64, 2) physics_kernel(PhysArgs a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
     const int e = blockIdx.x;
@@ -2316,15 +2362,22 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         const bool diff = lane < 7 && __float_as_uint(w1) != __float_as_uint(sig);
         const bool valid = cw && a.p.warm_start && __ballot(diff) == 0ull;
         const int nw = valid ? __builtin_amdgcn_readlane(__float_as_int(w1), 7) : 0;
-        const int nwc = nw < 0 ? 0 : (nw > MAXC ? MAXC : nw);
-        if (lane >= HE_CACHE_KEYS && lane < HE_CACHE_KEYS + MAXC) L.wckey[lane - HE_CACHE_KEYS] = __float_as_int(w1);
-        // impulses: words 32..63 from the first read, 64..94 from the second
+        const int nwc = nw < 0 ? 0 : (nw > MAXR ? MAXR : nw);
+        // row keys: 16 bits each, rows 2j / 2j + 1 in word HE_CACHE_KEYS + j
+        constexpr int KW = (MAXR + 1) / 2;
+        if (lane >= HE_CACHE_KEYS && lane < HE_CACHE_KEYS + KW) {
+            const int j = lane - HE_CACHE_KEYS;
+            const uint32_t kw = __float_as_uint(w1);
+            L.wckey[2 * j] = (int)(kw & 0xFFFFu);
+            L.wckey[2 * j + 1] = (int)(kw >> 16);
+        }
+        // impulses: rows 0 .. W - HE_CACHE_LAMBDA - 1 from the first read, the rest from the second
         if (lane >= HE_CACHE_LAMBDA) L.lam[lane - HE_CACHE_LAMBDA] = valid ? w1 : 0.f;
-        if (lane < W - HE_CACHE_LAMBDA) L.lam[W - HE_CACHE_LAMBDA + lane] = valid ? w2 : 0.f;
+        if (lane < HE_CACHE_LAMBDA) L.lam[W - HE_CACHE_LAMBDA + lane] = valid && W + lane < HE_CACHE_WORDS ? w2 : 0.f;
         if (lane == 0) L.nwc = nwc;
     }
-    static_assert(HE_CACHE_LAMBDA + 3 * MAXC <= HE_CACHE_WORDS && HE_CACHE_KEYS + MAXC <= HE_CACHE_LAMBDA &&
-                  HE_CACHE_WORDS <= 2 * W, "cache layout");
+    static_assert(HE_CACHE_KEYS + (MAXR + 1) / 2 <= HE_CACHE_LAMBDA && HE_CACHE_LAMBDA + MAXR <= HE_CACHE_WORDS &&
+                  HE_CACHE_WORDS <= 2 * W && HE_CACHE_LAMBDA < W, "cache layout");
     if (a.fused && lane == 0) {  // fused imitation: bookkeeping + motion metadata (trips 1, 2) now
         const ImitArgs& im = a.im;
         const int64_t mid = clamp_mid(im.m, im.motion_ids[e]);
@@ -2389,20 +2442,25 @@ __global__ void __launch_bounds__(64) physics_kernel(PhysArgs a) {
         imitation_finish<false>(a.im, e, e, lane, lane == 0, imitation_frames_blend(iraw), sb, pw);
     }
     STAMP(24);
-    if (a.cache) {  // signature (the root pose just written), slot count, keys, impulses
+    if (a.cache) {  // signature (the root pose just written), row count, row keys, impulses
         float* cw = a.cache + (size_t)e * HE_CACHE_WORDS;
         const int nwc = a.p.warm_start ? L.nwc : 0;
+        constexpr int KW = (MAXR + 1) / 2;
         float v = 0.f;
         if (lane < 3) v = L.root_pos[lane];
         else if (lane < 7) v = L.root_q[lane < 7 ? lane - 3 : 0];
         else if (lane == 7) v = __int_as_float(nwc);
-        else if (lane < HE_CACHE_KEYS + MAXC) v = lane - HE_CACHE_KEYS < nwc ? __int_as_float(L.wckey[lane - HE_CACHE_KEYS]) : 0.f;
-        else if (lane >= HE_CACHE_LAMBDA) v = lane - HE_CACHE_LAMBDA < 3 * nwc ? L.lam[lane - HE_CACHE_LAMBDA] : 0.f;
+        else if (lane < HE_CACHE_KEYS + KW) {
+            const int j = lane - HE_CACHE_KEYS;
+            const uint32_t k0 = 2 * j < nwc ? (uint32_t)L.wckey[2 * j] & 0xFFFFu : 0u;
+            const uint32_t k1 = 2 * j + 1 < nwc ? (uint32_t)L.wckey[2 * j + 1] & 0xFFFFu : 0u;
+            v = __uint_as_float(k0 | (k1 << 16));
+        } else if (lane >= HE_CACHE_LAMBDA) v = lane - HE_CACHE_LAMBDA < nwc ? L.lam[lane - HE_CACHE_LAMBDA] : 0.f;
         if (!a.p.warm_start) v = 0.f;
         cw[lane] = v;
         if (lane < HE_CACHE_WORDS - W) {
             const int r = W - HE_CACHE_LAMBDA + lane;
-            cw[W + lane] = a.p.warm_start && r < 3 * nwc ? L.lam[r] : 0.f;
+            cw[W + lane] = a.p.warm_start && r < nwc ? L.lam[r] : 0.f;
         }
     }
 }

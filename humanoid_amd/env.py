@@ -109,7 +109,7 @@ class EnvConfig:  # config.py:89-157
     reward: RewardConfig = field(default_factory=RewardConfig)
     # engine extensions (not in the reference config)
     seed: int = 0
-    max_contacts: int = 20
+    max_contacts: int = 40
     solver_iterations: int = 8  # PGS sweeps per physics step
 
     @property

@@ -28,7 +28,11 @@ extern "C" {
 #define HE_NUM_GEN 75          /* 6 root + 69 joint generalized velocities */
 #define HE_MAX_PAIRS 256
 #define HE_STAMP_SLOTS 32 /* diagnostic per-phase cycle slots per env (he_set_debug_stamps) */
-#define HE_MAX_CONTACTS 21       /* 3 rows each: all contact rows of an env fit one 64-lane wave */
+#define HE_MAX_CONTACTS 40       /* contact slots (points, joint limits) per env */
+#define HE_MAX_ROWS 63           /* solver rows per env, one per lane of a 64-lane wave: a joint limit
+                                    1, a point 1 normal row, its friction on its patch (patch friction:
+                                    2 tangential rows per body-terrain patch and, from 2 points on, 1
+                                    torsional row; a self pair 2 tangential rows of its own) */
 #define HE_OBS_SELF 358
 #define HE_OBS_TASK 576
 #define HE_OBS_DIM 934         /* humanoid_phc.py:458-467 */
@@ -70,7 +74,8 @@ typedef struct he_sim_params {
     float max_angular_velocity;      /* 100 */
     int32_t solver_iterations;       /* PGS sweeps per substep */
     int32_t self_collision;          /* 1 = has_self_collision (config.py:57) */
-    int32_t max_contacts;            /* <= HE_MAX_CONTACTS */
+    int32_t max_contacts;            /* contact slots, <= HE_MAX_CONTACTS (rows are capped at
+                                        HE_MAX_ROWS whatever this is) */
     float kp_scale, kd_scale;        /* config.py:106-107 */
     int32_t terrain;                 /* 0 plane everywhere, 1 per-env terrain kind (config 5) */
     float terrain_slope;             /* radians, terrain kind 1 */
@@ -95,16 +100,19 @@ typedef struct he_sim_params {
 
 /* Per-env solver warm-start cache (f32 words; HE_BUF_CONTACT_CACHE), written at the end of every
  * step and read at the start of the next when the env's root pose still equals the signature
- * (any external state write -- a reset -- invalidates it):
- *   [0,7)  signature: root position, root quaternion as written by the step
- *   7      number of cached contact slots (int32 bits)
- *   [8,8+HE_MAX_CONTACTS)  contact keys (int32 bits): body0 | (body1 + 2) << 8 | sub << 16 with
- *          body1 = -1 terrain (sub = candidate: capsule end / box corner), -2 joint limit
- *          (sub = 1 + 2 axis + side), else the self-collision partner (sub = 0)
- *   [32,32+3*HE_MAX_CONTACTS)  impulses of the slots' rows (normal, friction, friction) */
-#define HE_CACHE_WORDS 96
+ * (any external state write -- a reset -- invalidates it). It holds the last solve's rows:
+ *   [0,7)   signature: root position, root quaternion as written by the step
+ *   7       number of cached rows (int32 bits)
+ *   [8,40)  row keys, 16 bits each, row 2j in the low half of word 8 + j, row 2j+1 in the high half:
+ *           body0 | (body1 + 2) << 5 | sub << 10 | kind << 14 with body1 = -1 terrain (sub = the
+ *           point: capsule end / box corner; HE_KEY_PATCH for the friction rows of the body's
+ *           terrain patch), -2 joint limit (sub = 1 + 2 axis + side, 7 the rotation angle), else
+ *           the self-collision partner (sub = 0); kind 0 normal, 1 and 2 tangential, 3 torsional
+ *   [40,40+HE_MAX_ROWS)  the rows' impulses */
+#define HE_CACHE_WORDS 104
 #define HE_CACHE_KEYS 8
-#define HE_CACHE_LAMBDA 32
+#define HE_CACHE_LAMBDA 40
+#define HE_KEY_PATCH 15
 
 /* Imitation (reward / reset / obs) parameters: config.py:37-50, 97-112; humanoid_phc.py:1230-1335. */
 typedef struct he_imitation_params {

@@ -27,8 +27,9 @@ typedef double R;
 #define NB HE_NUM_BODIES
 #define ND HE_NUM_DOF
 #define NG HE_NUM_GEN
-/* The oracle's own contact capacity: max_contacts above the engine's HE_MAX_CONTACTS makes the
- * engine's truncation visible (tests/test_contacts.py); the warm-start cache needs <= 21. */
+/* The oracle's own capacity: max_contacts above the engine's HE_MAX_CONTACTS lifts the slot and
+ * row caps (HE_MAX_ROWS) so that the engine's truncation becomes visible
+ * (tests/diag/truncation_effect.py); the warm-start cache holds HE_MAX_ROWS rows. */
 #define MAXC 64
 #define MAXROW (3 * MAXC)
 
@@ -240,12 +241,29 @@ static void body_inertia(const he_model* m, const kin* k, int b, R mass_scale, s
  * one row layout and one Gauss-Seidel order with the engine. */
 typedef struct contact {
     int b0, b1;       /* b1 = -1 for terrain, -2 for a joint limit (b0 = the joint's body) */
-    int key;          /* warm-start key: b0 | (b1 + 2) << 8 | sub << 16 */
-    R x[3], n[3], t1[3], t2[3];
+    int key;          /* warm-start key of its normal row: b0 | (b1 + 2) << 5 | sub << 10 */
+    R x[3], n[3];
     R gap;
     R mu;
     R g[3];           /* joint limit: the row over the joint's three dofs */
 } contact;
+
+/* A solver row (patch friction; include/humanoid_engine.h HE_MAX_ROWS). Rows in Gauss-Seidel order:
+ * for every slot its normal row (a joint limit: its one row); after the last point of a body's
+ * terrain patch (the body's terrain slots, contiguous) the patch's friction rows: 2 tangential
+ * rows at the points' centroid and, from 2 points on, 1 torsional row about the patch normal; a
+ * self pair is a patch of its own point (2 tangential rows). PhysX runs patch friction (Isaac
+ * Gym's default), with friction per body-ground patch rather than per point. */
+typedef struct srow {
+    int slot, kind;   /* kind 0 normal / limit, 1 and 2 tangential, 3 torsional */
+    int n0, cnt;      /* friction rows: the patch's normal rows n0 .. n0 + cnt - 1 */
+    int b0, b1;
+    R dir[3], rho[3]; /* J = (rho, dir) about o: rho = (x - o) x dir; torsion rho = n_patch, dir = 0 */
+    R muw;            /* friction bound |lambda| <= muw * (sum of the patch's normal impulses):
+                         mu (tangential), mu r_patch (torsion: r_patch = the points' mean distance
+                         from the centroid in the tangent plane) */
+    int key;          /* 16-bit row key (include/humanoid_engine.h, the cache layout) */
+} srow;
 
 static R terrain_height(const he_sim_params* p, int kind, const R* x, R* n) {
     /* returns signed distance of x to the terrain surface along its normal n */
@@ -340,13 +358,12 @@ static int add_contact(contact* cs, int nc, int maxc, int* total, int b0, int b1
     if (nc >= maxc) return nc;
     contact* c = &cs[nc];
     c->b0 = b0; c->b1 = b1;
-    c->key = b0 | ((b1 + 2) << 8) | (sub << 16);
+    c->key = b0 | ((b1 + 2) << 5) | (sub << 10);
     memcpy(c->x, x, sizeof(R) * 3);
     memcpy(c->n, n, sizeof(R) * 3);
     c->gap = gap;
     c->mu = mu;
     c->g[0] = c->g[1] = c->g[2] = 0;
-    friction_basis(n, c->t1, c->t2);
     return nc + 1;
 }
 
@@ -446,32 +463,119 @@ static int gen_limits(const he_model* m, const he_sim_params* p, const env_state
     return nc;
 }
 
+/* Solver rows of a slot set (limits 1; a body's terrain patch of k points k normal rows + 2
+ * tangential + 1 torsional from k = 2; a self pair 3) */
+static int rows_of(const contact* cs, int nc) {
+    int nr = 0, pos = 0; /* pos: the point's index in its body's terrain patch */
+    for (int i = 0; i < nc; ++i) {
+        if (cs[i].b1 != -1) { nr += cs[i].b1 == -2 ? 1 : 3; continue; }
+        pos = (i > 0 && cs[i - 1].b1 == -1 && cs[i - 1].b0 == cs[i].b0) ? pos + 1 : 0;
+        nr += pos == 0 ? 3 : (pos == 1 ? 2 : 1);
+    }
+    return nr;
+}
+
 /* Contact slots: joint limits, terrain (bodies in order, box corners deepest-first), self pairs.
- * All are generated (up to the oracle's own MAXC); when they exceed max_contacts, the limits are
- * kept and the contacts reduced to the deepest (smallest gap, ties in slot order), in slot order:
- * the shallow speculative contacts go first, never a body's only penetrating one.
- * Returns the slots used (<= max_contacts); *total counts every contact generated. */
+ * All are generated (up to the oracle's own MAXC). When they exceed max_contacts slots or
+ * HE_MAX_ROWS rows, the limits are kept and the contacts are taken deepest first (smallest gap,
+ * ties in slot order), each one kept while its rows still fit (3 for a self pair or a body's first
+ * terrain point, 2 for its second -- the normal and the patch's torsional row -- 1 after), and the
+ * kept ones stay in slot order: the shallow speculative contacts go first, never a body's only
+ * penetrating one. Returns the slots used; *total counts every contact generated. */
 static int gen_all(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
                    R mu, contact* cs, int* total, int* nlim_out);
+/* diagnostic (tests/diag): the smallest gap among the dropped contacts of an env's last substep */
+static __thread R g_drop_gap;
+static float* g_drop_out;
+void ho_set_drop_gap_out(float* out) { g_drop_out = out; }
 static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
                         R mu, contact* cs, int* total) {
     int nlim = 0;
+    g_drop_gap = INFINITY;
     int nc = gen_all(m, p, k, s, terrain_kind, mu, cs, total, &nlim);
-    int maxc = p->max_contacts < MAXC ? p->max_contacts : MAXC;
-    if (nc <= maxc) return nc;
-    int keep = maxc - nlim; /* contact slots left after the limits */
-    if (keep < 0) { keep = 0; nlim = maxc; }
-    int kept[MAXC];
+    const int big = p->max_contacts > HE_MAX_CONTACTS; /* the oracle's own, larger capacity */
+    const int maxc = p->max_contacts < MAXC ? p->max_contacts : MAXC;
+    const int maxr = big ? MAXROW : HE_MAX_ROWS;
+    if (nc <= maxc && rows_of(cs, nc) <= maxr) return nc;
+    const int klim = nlim < maxc ? nlim : maxc; /* limits first, one row each */
+    int order[MAXC], no = 0;
     for (int i = nlim; i < nc; ++i) {
-        int rank = 0; /* contacts deeper than i (ties: earlier slots first) */
-        for (int j = nlim; j < nc; ++j)
-            if (cs[j].gap < cs[i].gap || (cs[j].gap == cs[i].gap && j < i)) ++rank;
-        kept[i] = rank < keep;
+        int j = no++; /* insertion by (gap, slot) */
+        while (j > 0 && (cs[order[j - 1]].gap > cs[i].gap)) { order[j] = order[j - 1]; --j; }
+        order[j] = i;
     }
-    int out = nlim;
-    for (int i = nlim; i < nc; ++i)
+    int kept[MAXC] = {0}, pc[NB] = {0};
+    int rows = klim, slots = klim;
+    for (int q = 0; q < no; ++q) {
+        const int i = order[q];
+        const int terr = cs[i].b1 == -1;
+        const int cost = !terr ? 3 : (pc[cs[i].b0] == 0 ? 3 : (pc[cs[i].b0] == 1 ? 2 : 1));
+        if (slots < maxc && rows + cost <= maxr) {
+            kept[i] = 1;
+            rows += cost;
+            ++slots;
+            if (terr) ++pc[cs[i].b0];
+        }
+    }
+    int out = klim;
+    for (int i = nlim; i < nc; ++i) {
         if (kept[i]) cs[out++] = cs[i];
+        else if (cs[i].gap < g_drop_gap) g_drop_gap = cs[i].gap;
+    }
     return out;
+}
+
+/* The solver rows of the kept slots (srow above), about the root origin o. */
+static int build_rows(const contact* cs, int nc, const R* o, srow* rows) {
+    int nr = 0;
+    for (int i = 0; i < nc; ++i) {
+        const contact* c = &cs[i];
+        srow* r = &rows[nr];
+        memset(r, 0, sizeof(*r));
+        r->slot = i; r->kind = 0; r->n0 = nr; r->cnt = 1; r->b0 = c->b0; r->b1 = c->b1; r->key = c->key;
+        if (c->b1 == -2) { ++nr; continue; } /* joint limit: its row is g over the joint's dofs */
+        R xo[3] = {c->x[0] - o[0], c->x[1] - o[1], c->x[2] - o[2]};
+        memcpy(r->dir, c->n, sizeof(r->dir));
+        cross3(xo, c->n, r->rho);
+        ++nr;
+        const int terr = c->b1 == -1;
+        if (terr && i + 1 < nc && cs[i + 1].b1 == -1 && cs[i + 1].b0 == c->b0) continue; /* not the patch's last point */
+        int first = i;
+        if (terr) while (first > 0 && cs[first - 1].b1 == -1 && cs[first - 1].b0 == c->b0) --first;
+        const int cnt = i - first + 1;
+        R np[3] = {0, 0, 0}, xp[3] = {0, 0, 0};
+        for (int j = first; j <= i; ++j)
+            for (int x = 0; x < 3; ++x) { np[x] += cs[j].n[x]; xp[x] += cs[j].x[x]; }
+        const R nn = sqrt(dot3(np, np));
+        for (int x = 0; x < 3; ++x) { np[x] /= nn; xp[x] /= cnt; }
+        R t1[3], t2[3];
+        friction_basis(np, t1, t2);
+        R rp = 0;
+        for (int j = first; j <= i; ++j) {
+            R d[3] = {cs[j].x[0] - xp[0], cs[j].x[1] - xp[1], cs[j].x[2] - xp[2]};
+            const R dn = dot3(d, np);
+            R tg[3] = {d[0] - dn * np[0], d[1] - dn * np[1], d[2] - dn * np[2]};
+            rp += sqrt(dot3(tg, tg));
+        }
+        rp /= cnt;
+        R xpo[3] = {xp[0] - o[0], xp[1] - o[1], xp[2] - o[2]};
+        const int nf = cnt >= 2 ? 3 : 2;
+        for (int kd = 1; kd <= nf; ++kd) {
+            srow* f = &rows[nr++];
+            memset(f, 0, sizeof(*f));
+            f->slot = i; f->kind = kd; f->n0 = nr - 1 - (kd - 1) - cnt; f->cnt = cnt; f->b0 = c->b0; f->b1 = c->b1;
+            if (kd < 3) {
+                memcpy(f->dir, kd == 1 ? t1 : t2, sizeof(f->dir));
+                cross3(xpo, f->dir, f->rho);
+                f->muw = c->mu;
+            } else {
+                memcpy(f->rho, np, sizeof(f->rho));
+                f->muw = c->mu * rp;
+            }
+            f->key = (terr ? (c->b0 | (1 << 5) | (HE_KEY_PATCH << 10)) : c->key) | (kd << 14);
+        }
+    }
+    return nr;
 }
 static int gen_all(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
                    R mu, contact* cs, int* total, int* nlim_out) {
@@ -582,13 +686,13 @@ typedef struct step_out {
     int sweeps;           /* Gauss-Seidel sweeps of the last substep's solve */
 } step_out;
 
-/* Warm-start cache: the previous solve's impulses by contact key (PhysX warm-starts its solver
- * from the previous frame's impulses). Rows of a contact whose key is found start at the cached
- * impulse instead of 0. */
+/* Warm-start cache: the previous solve's impulses by row key (PhysX warm-starts its solver from
+ * the previous frame's impulses). A row whose key is found starts at the cached impulse instead
+ * of 0. */
 typedef struct warm_cache {
-    int n;
-    int key[MAXC];
-    R lam[MAXC][3];
+    int n;            /* rows */
+    int key[MAXROW];  /* 16-bit row keys */
+    R lam[MAXROW];
 } warm_cache;
 
 /* one substep; updates s in place */
@@ -773,32 +877,30 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     R lim_tau[ND];
     memset(lim_tau, 0, sizeof(lim_tau));
     if (nc > 0) {
-        int nr = 3 * nc;
+        static __thread srow rows[MAXROW];
+        const int nr = build_rows(cs, nc, k.o, rows);
         R brow[MAXROW];
         for (int r = 0; r < nr; ++r) {
-            const contact* c = &cs[r / 3];
+            const srow* w = &rows[r];
+            const contact* c = &cs[w->slot];
             R* z = Z[r];
-            if (c->b1 == -2) { /* joint limit: the row over the joint's dofs, two zero rows */
+            if (w->b1 == -2) { /* joint limit: the row over the joint's dofs */
                 for (int i = 0; i < NG; ++i) z[i] = 0;
-                if (r % 3 == 0)
-                    for (int x = 0; x < 3; ++x) z[t->body_dof0[c->b0] + x] = c->g[x];
+                for (int x = 0; x < 3; ++x) z[t->body_dof0[w->b0] + x] = c->g[x];
             } else {
-                const R* dir = (r % 3 == 0) ? c->n : (r % 3 == 1 ? c->t1 : c->t2);
-                R rho[3], xo[3] = {c->x[0] - k.o[0], c->x[1] - k.o[1], c->x[2] - k.o[2]};
-                cross3(xo, dir, rho);
                 for (int i = 0; i < NG; ++i) {
                     int bi = t->dof_body[i];
                     R sgn = 0;
-                    if (t->is_anc[bi][c->b0]) sgn += 1;
-                    if (c->b1 >= 0 && t->is_anc[bi][c->b1]) sgn -= 1;
+                    if (t->is_anc[bi][w->b0]) sgn += 1;
+                    if (w->b1 >= 0 && t->is_anc[bi][w->b1]) sgn -= 1;
                     const R* S = k.S[i];
-                    z[i] = sgn == 0 ? 0 : sgn * (S[0] * rho[0] + S[1] * rho[1] + S[2] * rho[2] + S[3] * dir[0] + S[4] * dir[1] + S[5] * dir[2]);
+                    z[i] = sgn == 0 ? 0 : sgn * (S[0] * w->rho[0] + S[1] * w->rho[1] + S[2] * w->rho[2] + S[3] * w->dir[0] + S[4] * w->dir[1] + S[5] * w->dir[2]);
                 }
             }
             R ju = 0;
             for (int i = 0; i < NG; ++i) ju += z[i] * uf[i];
             R bb = 0;
-            if (r % 3 == 0) bb = c->gap >= 0 ? c->gap / dt : fmax(p->baumgarte * c->gap / dt, -p->max_depenetration_velocity);
+            if (w->kind == 0) bb = c->gap >= 0 ? c->gap / dt : fmax(p->baumgarte * c->gap / dt, -p->max_depenetration_velocity);
             brow[r] = ju + bb;
             ltdl_solve_LT(H, t->dof_parent, z);
         }
@@ -822,30 +924,28 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         R lam[MAXROW];
         memset(lam, 0, sizeof(lam));
         if (ws && p->warm_start)
-            for (int ci = 0; ci < nc; ++ci)
+            for (int r = 0; r < nr; ++r)
                 for (int j = 0; j < ws->n; ++j)
-                    if (ws->key[j] == cs[ci].key) {
-                        for (int x = 0; x < 3; ++x) lam[3 * ci + x] = ws->lam[j][x];
+                    if (ws->key[j] == rows[r].key) {
+                        lam[r] = ws->lam[j];
                         break;
                     }
+        /* friction bound of row r from the current normal impulses of its patch */
+#define PATCH_BOUND(r) ({ R b_ = 0; for (int k_ = 0; k_ < rows[r].cnt; ++k_) b_ += lam[rows[r].n0 + k_]; rows[r].muw * b_; })
         int sweeps = 0;
         for (int it = 0; it < p->solver_iterations; ++it) {
             R lam_prev[MAXROW];
             memcpy(lam_prev, lam, sizeof(R) * nr);
             ++sweeps;
-            for (int ci = 0; ci < nc; ++ci) {
-                int r0 = 3 * ci;
-                R w = brow[r0];
-                for (int j = 0; j < nr; ++j) w += A[r0][j] * lam[j];
-                R ln = lam[r0] - w / (A[r0][r0] + 1e-12);
-                lam[r0] = ln > 0 ? ln : 0;
-                R bound = cs[ci].mu * lam[r0];
-                for (int tdir = 1; tdir <= 2; ++tdir) {
-                    int r = r0 + tdir;
-                    R wt = brow[r];
-                    for (int j = 0; j < nr; ++j) wt += A[r][j] * lam[j];
-                    R lt = lam[r] - wt / (A[r][r] + 1e-12);
-                    lam[r] = lt > bound ? bound : (lt < -bound ? -bound : lt);
+            for (int r = 0; r < nr; ++r) {
+                R w = brow[r];
+                for (int j = 0; j < nr; ++j) w += A[r][j] * lam[j];
+                const R l = lam[r] - w / (A[r][r] + 1e-12);
+                if (rows[r].kind == 0) {
+                    lam[r] = l > 0 ? l : 0;
+                } else {
+                    const R bound = PATCH_BOUND(r);
+                    lam[r] = l > bound ? bound : (l < -bound ? -bound : l);
                 }
             }
             /* converged: no row's velocity moved by more than solver_tolerance in this sweep
@@ -861,27 +961,24 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         }
         out->sweeps = sweeps;
         /* complementarity residual of the returned impulses: normal rows min(w, lambda) -> 0,
-         * friction rows w = 0 inside the cone (or lambda on the bound) */
-        for (int ci = 0; ci < nc; ++ci) {
-            int r0 = 3 * ci;
-            for (int x = 0; x < 3; ++x) {
-                int r = r0 + x;
-                R w = brow[r];
-                for (int j = 0; j < nr; ++j) w += A[r][j] * lam[j];
-                R res;
-                if (x == 0) res = fmin(w, lam[r] * A[r][r]);
-                else {
-                    R bound = cs[ci].mu * lam[r0];
-                    res = (lam[r] >= bound - 1e-12 && w < 0) || (lam[r] <= -bound + 1e-12 && w > 0) ? 0 : w;
-                }
-                if (fabs(res) > out->residual) out->residual = fabs(res);
+         * friction rows w = 0 inside the bound (or lambda on the bound) */
+        for (int r = 0; r < nr; ++r) {
+            R w = brow[r];
+            for (int j = 0; j < nr; ++j) w += A[r][j] * lam[j];
+            R res;
+            if (rows[r].kind == 0) res = fmin(w, lam[r] * A[r][r]);
+            else {
+                const R bound = PATCH_BOUND(r);
+                res = (lam[r] >= bound - 1e-12 && w < 0) || (lam[r] <= -bound + 1e-12 && w > 0) ? 0 : w;
             }
+            if (fabs(res) > out->residual) out->residual = fabs(res);
         }
+#undef PATCH_BOUND
         if (ws) {
-            ws->n = nc;
-            for (int ci = 0; ci < nc; ++ci) {
-                ws->key[ci] = cs[ci].key;
-                for (int x = 0; x < 3; ++x) ws->lam[ci][x] = lam[3 * ci + x];
+            ws->n = nr;
+            for (int r = 0; r < nr; ++r) {
+                ws->key[r] = rows[r].key;
+                ws->lam[r] = lam[r];
             }
         }
         R y[NG];
@@ -891,16 +988,16 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
         ltdl_solve_L(H, t->dof_parent, y);
         for (int i = 0; i < NG; ++i) unew[i] += y[i];
-        for (int ci = 0; ci < nc; ++ci) {
-            const contact* c = &cs[ci];
-            if (c->b1 == -2) { /* a joint limit: a joint force (below), not a contact force */
-                for (int x = 0; x < 3; ++x) lim_tau[3 * (c->b0 - 1) + x] += c->g[x] * lam[3 * ci] / dt;
+        for (int r = 0; r < nr; ++r) {
+            const srow* w = &rows[r];
+            if (w->b1 == -2) { /* a joint limit: a joint force (below), not a contact force */
+                for (int x = 0; x < 3; ++x) lim_tau[3 * (w->b0 - 1) + x] += cs[w->slot].g[x] * lam[r] / dt;
                 continue;
             }
-            for (int x = 0; x < 3; ++x) {
-                R f = (lam[3 * ci] * c->n[x] + lam[3 * ci + 1] * c->t1[x] + lam[3 * ci + 2] * c->t2[x]) / dt;
-                out->contact_force[c->b0][x] += f;
-                if (c->b1 >= 0) out->contact_force[c->b1][x] -= f;
+            for (int x = 0; x < 3; ++x) { /* linear force of the row (a torsional row has none) */
+                R f = lam[r] * w->dir[x] / dt;
+                out->contact_force[w->b0][x] += f;
+                if (w->b1 >= 0) out->contact_force[w->b1][x] -= f;
             }
         }
     } else if (ws) {
@@ -1029,12 +1126,12 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         if (cw && p->warm_start && memcmp(cw, rs, 7 * sizeof(float)) == 0) {
             int32_t nn;
             memcpy(&nn, cw + 7, 4);
-            ws.n = nn < 0 ? 0 : (nn > HE_MAX_CONTACTS ? HE_MAX_CONTACTS : nn);
+            ws.n = nn < 0 ? 0 : (nn > HE_MAX_ROWS ? HE_MAX_ROWS : nn);
             for (int j = 0; j < ws.n; ++j) {
-                int32_t key;
-                memcpy(&key, cw + HE_CACHE_KEYS + j, 4);
-                ws.key[j] = key;
-                for (int x = 0; x < 3; ++x) ws.lam[j][x] = cw[HE_CACHE_LAMBDA + 3 * j + x];
+                uint32_t kw;
+                memcpy(&kw, cw + HE_CACHE_KEYS + j / 2, 4);
+                ws.key[j] = (int)((kw >> (16 * (j & 1))) & 0xFFFFu);
+                ws.lam[j] = cw[HE_CACHE_LAMBDA + j];
             }
         }
         step_out out;
@@ -1056,16 +1153,19 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         if (dropped) dropped[e] = out.dropped;
         if (residual) residual[e] = (float)out.residual;
         if (sweeps) sweeps[e] = out.sweeps;
+        if (g_drop_out) g_drop_out[e] = (float)g_drop_gap;
         if (cw) {
             memset(cw, 0, HE_CACHE_WORDS * sizeof(float));
             if (p->warm_start) {
                 memcpy(cw, rs, 7 * sizeof(float));
-                int32_t nn = ws.n > HE_MAX_CONTACTS ? HE_MAX_CONTACTS : ws.n;
+                int32_t nn = ws.n > HE_MAX_ROWS ? HE_MAX_ROWS : ws.n; /* the oracle's larger capacity: truncated */
                 memcpy(cw + 7, &nn, 4);
                 for (int j = 0; j < nn; ++j) {
-                    int32_t key = ws.key[j];
-                    memcpy(cw + HE_CACHE_KEYS + j, &key, 4);
-                    for (int x = 0; x < 3; ++x) cw[HE_CACHE_LAMBDA + 3 * j + x] = (float)ws.lam[j][x];
+                    uint32_t kw;
+                    memcpy(&kw, cw + HE_CACHE_KEYS + j / 2, 4);
+                    kw |= ((uint32_t)ws.key[j] & 0xFFFFu) << (16 * (j & 1));
+                    memcpy(cw + HE_CACHE_KEYS + j / 2, &kw, 4);
+                    cw[HE_CACHE_LAMBDA + j] = (float)ws.lam[j];
                 }
             }
         }

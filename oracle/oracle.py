@@ -159,6 +159,12 @@ def set_probe_noise(seed=0, rel=0.0):
     lib().ho_set_probe_noise(C.c_uint64(int(seed)), C.c_double(float(rel)))
 
 
+def set_drop_gap_out(arr=None):
+    """Diagnostics only: float32 [N] that the following physics_step calls fill with the smallest gap
+    among each env's dropped contacts of the last substep (inf: none dropped); None turns it off."""
+    lib().ho_set_drop_gap_out(None if arr is None else arr.ctypes.data_as(C.POINTER(C.c_float)))
+
+
 def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, dof_state, targets, substeps=2,
                  mass_scale=None, friction=None, terrain_kind=None, cache=None):
     """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays) and on the warm-start

@@ -22,7 +22,7 @@ def _rollout(config, model):
     import bench
     if not torch.cuda.is_available():
         pytest.skip("needs the GPU")
-    args = argparse.Namespace(config=config, num_envs=4096, clips=128, seed=0, max_contacts=20)
+    args = argparse.Namespace(config=config, num_envs=4096, clips=128, seed=0, max_contacts=40)
     return bench.Rollout(args, model, 0, 0)
 
 
@@ -81,7 +81,7 @@ def test_full_size_sample_matches_oracle(model, he_model, config):
     torch.cuda.synchronize()
     tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
     from test_gpu_parity import CondStats, _cond_close, contact_keys
-    sp = _abi.default_sim_params(max_contacts=20, terrain=1 if config == "dr" else 0)
+    sp = _abi.default_sim_params(max_contacts=40, terrain=1 if config == "dr" else 0)
     props = _props(ro, idx)
     probes = []
     for seed in (123, 124, 125):  # the oracle's own sensitivity (see _cond_close)
@@ -123,7 +123,7 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     dof = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy()
     c_o = ro.eng.contact_cache.cpu().numpy()[idx].copy()
     props = _props(ro, idx)
-    sp = _abi.default_sim_params(max_contacts=20, terrain=1)
+    sp = _abi.default_sim_params(max_contacts=40, terrain=1)
     probes = [[root.copy(), dof.copy(), c_o.copy(), None] for _ in range(8)]  # 30 steps: 8 probes
     zero = torch.zeros_like(ro.actions)
     mism = np.zeros(len(idx), bool)

@@ -15,6 +15,8 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 torch = pytest.importorskip("torch")
 
+from humanoid_amd import _abi  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -22,7 +24,7 @@ def _rollout(config, model, seed=0):
     import bench
     if not torch.cuda.is_available():
         pytest.fail("GPU test run without a visible GPU")
-    args = argparse.Namespace(config=config, num_envs=4096, clips=128, seed=seed, max_contacts=20)
+    args = argparse.Namespace(config=config, num_envs=4096, clips=128, seed=seed, max_contacts=40)
     return bench.Rollout(args, model, 0, 0)
 
 
@@ -32,7 +34,9 @@ def _check(ro, rew_max):
         assert torch.isfinite(t).all()
     q = ro.eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3)
     assert q.norm(dim=-1).max().item() < np.pi
-    assert (ro.eng.num_contacts <= 20).all() and (ro.eng.num_contacts >= 0).all()
+    assert (ro.eng.num_contacts <= _abi.MAX_CONTACTS).all() and (ro.eng.num_contacts >= 0).all()
+    rows = ro.eng.contact_cache[:, 7].contiguous().view(torch.int32)  # solver rows of the last solve
+    assert ((rows >= 0) & (rows <= _abi.MAX_ROWS)).all()
     assert (ro.eng.dropped_contacts >= 0).all()
     assert ro.rew.max().item() <= rew_max
     return q

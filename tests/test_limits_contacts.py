@@ -133,7 +133,7 @@ def test_cache_signature_invalidates_on_external_write(he_model, model):
     r, d = root.copy(), dof.copy()
     for _ in range(3):
         O.physics_step(he_model, sp, r, d, targets, 2, cache=cache)
-    assert cache[:, 7].view(np.int32).tolist() == [16, 16]
+    assert cache[:, 7].view(np.int32).tolist() == [28, 28]  # 4 boxes x (4 normal + 2 tangential + 1 torsional rows)
     np.testing.assert_array_equal(cache[:, :3], r[:, :3])
     # env 1 is "reset" to its start state: the warm and cold steps of it agree exactly
     r2, d2 = r.copy(), d.copy()
@@ -191,7 +191,7 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
 
 def test_moderate_random_actions_stay_physical(he_model, model):
     """Random actions U(-0.5, 0.5) of the PD scale on standing bodies for 2 s keep every root below
-    5 m/s (measured 5.7 max over 512 envs, tools/energy_probe.py; CoM below 4.4) and no joint past the
+    5 m/s (measured 5.7 max over 512 envs, tests/diag/energy_probe.py; CoM below 4.4) and no joint past the
     limit. The saturated U(-1, 1) case is test_physics_invariants.py::test_saturated_random_actions_stay_physical."""
     from humanoid_amd.model import pd_action_offset_scale
     n = 64

@@ -244,7 +244,7 @@ def test_saturated_random_actions_stay_physical(he_model, model):
     """VERDICT r02 item 1's bar on the CPU: standing bodies under U(+-1) random actions (saturated PD
     targets, new every policy step) for 2 s: no root ever exceeds 10 m/s, the median internal kinetic
     energy stays at the dt-refined level (~0.9 kJ; the explicit bias: ~22 kJ with most roots over
-    10 m/s, tools/energy_probe.py) and no joint passes its angle cap."""
+    10 m/s, tests/diag/energy_probe.py) and no joint passes its angle cap."""
     n = 128
     vmax, ke, dof = _random_action_run(he_model, model, 1.0, n, 60)
     q = np.linalg.norm(dof[..., 0].reshape(n, 23, 3), axis=-1)

@@ -9,7 +9,7 @@ import argparse, sys, numpy as np, torch
 sys.path.insert(0, '.')
 import bench
 from humanoid_amd.model import load_default_model
-args = argparse.Namespace(config='imitation', num_envs=4096, clips=128, seed=0, max_contacts=20)
+args = argparse.Namespace(config='imitation', num_envs=4096, clips=128, seed=0, max_contacts=40)
 ro = bench.Rollout(args, load_default_model(), 0, 0)
 for _ in range(20):
     ro.tracking_actions(); ro.step()

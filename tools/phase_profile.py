@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--num-envs", type=int, default=4096)
-    ap.add_argument("--max-contacts", type=int, default=20)
+    ap.add_argument("--max-contacts", type=int, default=40)
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--scheme", choices=["default", "r02"], default="default")
     args = ap.parse_args()

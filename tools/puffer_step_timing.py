@@ -5,9 +5,9 @@ import bench
 from humanoid_amd.model import load_default_model
 from humanoid_amd.env import EnvConfig, PHCPufferEnv
 model = load_default_model()
-args = argparse.Namespace(config="standstill", num_envs=4096, clips=128, seed=0, max_contacts=20, puffer_steps=200)
+args = argparse.Namespace(config="standstill", num_envs=4096, clips=128, seed=0, max_contacts=40, puffer_steps=200)
 clips = bench.make_clips(args, model)
-cfg = EnvConfig(num_envs=4096, motion_file={f"clip{i}": c for i, c in enumerate(clips)}, seed=0, max_contacts=20)
+cfg = EnvConfig(num_envs=4096, motion_file={f"clip{i}": c for i, c in enumerate(clips)}, seed=0, max_contacts=40)
 pe = PHCPufferEnv(cfg); pe.reset()
 _, actions, _ = bench.build_workload(args, model, 0)
 ad = torch.as_tensor(actions, device="cuda:0")
