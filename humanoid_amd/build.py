@@ -1,6 +1,7 @@
 """Build ``humanoid_amd/libhumanoid_engine.so`` for gfx950 with hipcc (in-tree, travels with the
 repo to the GPU box). Usage: ``python -m humanoid_amd.build [--force]``."""
 import os
+import re
 import subprocess
 import sys
 
@@ -43,15 +44,42 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
+# kernels whose occupancy (waves per SIMD, the compiler's resource report) the build enforces: the
+# physics kernel is one wave per env and latency-bound, and at one wave per SIMD it runs ~40 % slower
+MIN_OCCUPANCY = {"he_physics.hip": ("physics_kernel", 2)}
+
+
+def _check_occupancy(src, stderr):
+    want = MIN_OCCUPANCY.get(os.path.basename(src))
+    if not want:
+        return
+    name, waves = want
+    lines = stderr.splitlines()
+    for i, ln in enumerate(lines):
+        if "Function Name:" in ln and name in ln:
+            for ln2 in lines[i + 1:i + 16]:
+                m = re.search(r"Occupancy \[waves/SIMD\]: (\d+)", ln2)
+                if m:
+                    if int(m.group(1)) < waves:
+                        raise RuntimeError(f"{name}: occupancy {m.group(1)} waves/SIMD < {waves} "
+                                           f"(register pressure; see the resource report)")
+                    return
+    raise RuntimeError(f"{name}: no occupancy in the compiler's resource report")
+
+
 def _compile(hipcc, cmd, src, o, force, hdr_time, verbose):
     stamp = o + ".cmd"  # a flag change rebuilds too
     same_cmd = os.path.exists(stamp) and open(stamp).read() == " ".join(cmd)
     if force or not same_cmd or _mtime(o) < max(_mtime(src), hdr_time):
         if verbose:
             print(" ".join(cmd))
+        if os.path.basename(src) in MIN_OCCUPANCY:
+            cmd = cmd + ["-Rpass-analysis=kernel-resource-usage"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr}")
+        _check_occupancy(src, r.stderr)
+        cmd = cmd[:-1] if cmd[-1] == "-Rpass-analysis=kernel-resource-usage" else cmd
         with open(stamp, "w") as f:
             f.write(" ".join(cmd))
         return True

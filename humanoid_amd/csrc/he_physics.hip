@@ -1908,28 +1908,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 if (k < cost) { L.rslot[start + k] = (int8_t)lane; L.rkind[start + k] = (int8_t)k; }
         }
     }
-    sync();
-    STAMP(7);
-    // ---- each row's Jacobian data (lane = row): slot, kind, bodies; a friction row's patch (a
-    // body's terrain points [tbase, tbase + tcnt), or the self pair alone): normal = the normalised
-    // sum of the points' normals, the tangent basis of it, the points' centroid, the torsion radius
-    // (mean tangential distance of the points from the centroid); its normal rows n0 .. n0 + cnt - 1
-    // as a lane mask, its bound weight muw (mu, or mu r for the torsional row), its 16-bit key
-    const bool act = lane < nr;
-    const int rs_ = act ? L.rslot[lane] : 0;
-    const int kind = act ? L.rkind[lane] : 0;
-    const int rbb = L.cbb[rs_];
-    const int rb0 = rbb & 0xFF, rb1 = (rbb >> 8) - 2;
-    f3 dd, rho;
-    float muw = 0.f;
-    uint32_t mlo = 0u, mhi = 0u;
-    int rkey;
-    {
-        const f3 xs = f3{L.cx[rs_][0], L.cx[rs_][1], L.cx[rs_][2]};
-        const f3 ns = f3{L.cn[rs_][0], L.cn[rs_][1], L.cn[rs_][2]};
-        const bool terr = rb1 == -1;
-        const int p0 = terr ? L.tbase[rb0] : rs_;
-        const int pc = terr ? L.tcnt[rb0] : 1;
+    // ---- each body's terrain patch (lane = body, tcnt > 0): normal = the normalised sum of its
+    // points' normals, the points' centroid (about o) and the torsion radius (mean tangential
+    // distance of the points from the centroid), into the RNEA force scratch F (dead from the
+    // midpoint bias to the next substep's force pass) and the Acc words after the bounding spheres
+    float* prad = &L.Acc[0][0] + 4 * NB;
+    static_assert(5 * NB <= 6 * NB, "patch radii fit Acc after the bounding spheres");
+    if (lane < NB && L.tcnt[lane] > 0) {
+        const int p0 = L.tbase[lane], pc = L.tcnt[lane];
         f3 px[4];
         f3 np = f3{0.f, 0.f, 0.f}, xp = f3{0.f, 0.f, 0.f};
 #pragma unroll
@@ -1950,31 +1936,26 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const f3 tg = d - np * dot3(d, np);
             if (j < pc) rp += norm3(tg);
         }
-        rp *= 1.0f / (float)pc;
-        f3 t1, t2;
-        friction_basis(np, t1, t2);
-        dd = kind == 0 ? ns : (kind == 1 ? t1 : (kind == 2 ? t2 : f3{0.f, 0.f, 0.f}));
-        rho = kind == 3 ? np : cross3(kind == 0 ? xs : xp, dd);  // contact points about o
-        if (act && kind > 0) {
-            muw = kind == 3 ? mu * rp : mu;
-            const int n0 = lane - (kind - 1) - pc;
-            const uint64_t pm = ((1ull << pc) - 1ull) << n0;
-            mlo = (uint32_t)pm;
-            mhi = (uint32_t)(pm >> 32);
-        }
-        const int k0 = L.ckey[rs_];
-        rkey = kind == 0 ? k0 : ((terr ? row_key(rb0, -1, HE_KEY_PATCH, 0) : k0) | (kind << 14));
-        // the row's linear direction for the reported forces (IS scratch, read after the solve; a
-        // joint limit's and a torsional row's: none)
-        if (act) {
-            float* fr = gl + 2 * kCand;
-            const bool none = rb1 == -2;
-            fr[3 * lane] = none ? 0.f : dd.x;
-            fr[3 * lane + 1] = none ? 0.f : dd.y;
-            fr[3 * lane + 2] = none ? 0.f : dd.z;
-        }
+        float* pf = L.F[lane];
+        pf[0] = np.x; pf[1] = np.y; pf[2] = np.z; pf[3] = xp.x; pf[4] = xp.y; pf[5] = xp.z;
+        prad[lane] = rp * (1.0f / (float)pc);
     }
-    static_assert(2 * kCand + 3 * W <= NG * 6, "per-row force directions fit IS");
+    sync();
+    STAMP(7);
+    // ---- each row's Jacobian data (lane = row): slot, kind, bodies; a friction row's patch (a
+    // body's terrain points [tbase, tbase + tcnt), or the self pair alone): normal = the normalised
+    // sum of the points' normals, the tangent basis of it, the points' centroid, the torsion radius
+    // (mean tangential distance of the points from the centroid); its normal rows n0 .. n0 + cnt - 1
+    // as a lane mask, its bound weight muw (mu, or mu r for the torsional row), its 16-bit key
+    const bool act = lane < nr;
+    const int rs_ = act ? L.rslot[lane] : 0;
+    const int kind = act ? L.rkind[lane] : 0;
+    const int rbb = L.cbb[rs_];
+    const int rb0 = rbb & 0xFF, rb1 = (rbb >> 8) - 2;
+    // the row's 16-bit key: a normal row its slot's, a friction row its patch's (terrain: the body's
+    // patch, HE_KEY_PATCH) with the kind
+    const int rkey = kind == 0 ? L.ckey[rs_]
+                               : ((rb1 == -1 ? row_key(rb0, -1, HE_KEY_PATCH, 0) : L.ckey[rs_]) | (kind << 14));
     // ---- warm start: the previous solve's impulse of each row's key (lane r matches its key against
     // the old keys by readlane and fetches the impulse)
     float lam0 = 0.f;
@@ -1998,6 +1979,34 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // the old keys are matched: this solve's row keys replace them (the next solve's warm start)
         L.wckey[lane] = act ? rkey : -1;
     }
+    f3 dd, rho;
+    {
+        const f3 xs = f3{L.cx[rs_][0], L.cx[rs_][1], L.cx[rs_][2]};
+        const f3 ns = f3{L.cn[rs_][0], L.cn[rs_][1], L.cn[rs_][2]};
+        // a friction row's patch: the body's terrain patch (above), or a self pair's own point
+        const bool terr = rb1 == -1;
+        const float* pf = L.F[rb0];
+        const f3 np = terr ? f3{pf[0], pf[1], pf[2]} : ns;
+        const f3 xp = terr ? f3{pf[3], pf[4], pf[5]} : xs;
+        const float rp = terr ? prad[rb0] : 0.f;
+        f3 t1, t2;
+        friction_basis(np, t1, t2);
+        dd = kind == 0 ? ns : (kind == 1 ? t1 : (kind == 2 ? t2 : f3{0.f, 0.f, 0.f}));
+        rho = kind == 3 ? np : cross3(kind == 0 ? xs : xp, dd);  // contact points about o
+        // the friction bound weight, parked in the impulse words (dead from the self-pair list to
+        // the solve's store) until the PGS: a short live range through the rows' register peak
+        L.lam[lane] = act && kind > 0 ? (kind == 3 ? mu * rp : mu) : 0.f;
+        // the row's linear direction for the reported forces (IS scratch, read after the solve; a
+        // joint limit's and a torsional row's: none)
+        if (act) {
+            float* fr = gl + 2 * kCand;
+            const bool none = rb1 == -2;
+            fr[3 * lane] = none ? 0.f : dd.x;
+            fr[3 * lane + 1] = none ? 0.f : dd.y;
+            fr[3 * lane + 2] = none ? 0.f : dd.z;
+        }
+    }
+    static_assert(2 * kCand + 3 * W <= NG * 6, "per-row force directions fit IS");
     if (nr > 0) {
         // ---- contact rows, one per lane: z = J_r^T, brow = J_r uf + bias, then z <- D^-1/2 L^-T z
         // (dofs outside every row's support stay zero and are skipped wave-uniformly), so that the
@@ -2090,8 +2099,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const float ninvd = -invd;
 #pragma unroll
             for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
-            // a friction row's bound at the warm start: muw x its patch's normal impulses (<= 4 rows)
+            // the row's friction bound weight and its patch's normal rows n0 .. n0 + pc - 1 as a
+            // 64-bit lane mask (friction rows only)
             const bool isn = kind == 0;
+            const float muw = L.lam[lane];
+            uint32_t mlo = 0u, mhi = 0u;
+            if (act && !isn) {
+                const int pc = rb1 == -1 ? L.tcnt[rb0] : 1;
+                const uint64_t pm = ((1ull << pc) - 1ull) << (lane - (kind - 1) - pc);
+                mlo = (uint32_t)pm;
+                mhi = (uint32_t)(pm >> 32);
+            }
+            // a friction row's bound at the warm start: muw x its patch's normal impulses (<= 4 rows)
             float bnd = 0.f;
             if (__ballot(lam0 != 0.f)) {
                 const int n0 = act && !isn ? (int)__builtin_ctzll(((uint64_t)mhi << 32) | mlo) : 0;
@@ -2309,10 +2328,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     STAMP(12);
 }
 
-// (64, 2): two waves per SIMD, i.e. at most 256 VGPRs + AGPRs; the allocator fits the kernel in them
-// without scratch (unconstrained it parks one kernel-lifetime value in an AGPR at 257 and falls
-// to one wave per SIMD)
-__global__ void __launch_bounds__(64, 2) physics_kernel(PhysArgs a) {
+// two waves per SIMD need at most 256 VGPRs + AGPRs. The kernel fits (251) without a bound, and
+// the bound itself costs 1.7 % (r03 A/B: the scheduler works to a tighter register target), so it
+// is off; humanoid_amd/build.py checks the compiler's occupancy report instead and fails the build
+// below 2 waves per SIMD. HE_MIN_WAVES 2 forces the fit (spilling before dropping to one wave).
+#ifndef HE_MIN_WAVES
+#define HE_MIN_WAVES 1
+#endif
+__global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
     const int e = blockIdx.x;
