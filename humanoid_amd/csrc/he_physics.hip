@@ -1182,6 +1182,20 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 #else
 #define HE_PRED_FN HE_DEV
 #endif
+// yh += D^-1/2 L^-T dc (lane = dof, then dofs 64..74 on lanes 0..10): the midpoint correction's
+// forward substitution replayed from the stored factor
+HE_DEV void mid_lt(Lds& L, const BodyTopo& T, int lane, float c1, float c2) {
+    using regla::NH;
+#if HE_PRED_LT_GROUPS
+    regla::solve_LT_vec_groups<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+#else
+    regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+#endif
+    L.yh[lane] += c1 * L.sDinv[lane];
+    if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
+    sync();
+}
+
 HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, unsigned long long* stamps,
                                unsigned long long& t_prev) {
     (void)stamps; (void)t_prev;
@@ -1323,14 +1337,7 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
     float c1 = corr(lane);
     float c2 = lane < NH ? corr(64 + lane) : 0.f;
     STAMP(27);
-#if HE_PRED_LT_GROUPS
-    regla::solve_LT_vec_groups<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
-#else
-    regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
-#endif
-    L.yh[lane] += c1 * L.sDinv[lane];
-    if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
-    sync();
+    mid_lt(L, T, lane, c1, c2);
     STAMP(28);
 }
 

@@ -43,6 +43,10 @@ static double g_probe_rel = 0.0;
 static uint64_t g_probe_seed = 0;
 static __thread int g_probe_env, g_probe_sub;
 void ho_set_probe_noise(uint64_t seed, double rel) { g_probe_seed = seed; g_probe_rel = rel; }
+/* diagnostic (tests/diag): friction bounds from the normal impulses at the sweep's start (1)
+ * instead of the current ones (0, the engine's) */
+static int g_lagged_bounds = 0;
+void ho_set_lagged_bounds(int on) { g_lagged_bounds = on; }
 static double probe_xi(int r, int c) {
     uint64_t z = g_probe_seed * 0x9E3779B97F4A7C15ull ^ ((uint64_t)g_probe_env + 0x632BE59BD9B4E019ull) * 0xBF58476D1CE4E5B9ull ^
                  ((uint64_t)g_probe_sub * 4099u + (uint64_t)r * 131u + (uint64_t)c + 0x2545F4914F6CDD1Dull) * 0x94D049BB133111EBull;
@@ -931,7 +935,8 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                         break;
                     }
         /* friction bound of row r from the current normal impulses of its patch */
-#define PATCH_BOUND(r) ({ R b_ = 0; for (int k_ = 0; k_ < rows[r].cnt; ++k_) b_ += lam[rows[r].n0 + k_]; rows[r].muw * b_; })
+#define PATCH_BOUND_OF(L_, r) ({ R b_ = 0; for (int k_ = 0; k_ < rows[r].cnt; ++k_) b_ += L_[rows[r].n0 + k_]; rows[r].muw * b_; })
+#define PATCH_BOUND(r) PATCH_BOUND_OF(lam, r)
         int sweeps = 0;
         for (int it = 0; it < p->solver_iterations; ++it) {
             R lam_prev[MAXROW];
@@ -944,7 +949,7 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                 if (rows[r].kind == 0) {
                     lam[r] = l > 0 ? l : 0;
                 } else {
-                    const R bound = PATCH_BOUND(r);
+                    const R bound = g_lagged_bounds ? PATCH_BOUND_OF(lam_prev, r) : PATCH_BOUND(r);
                     lam[r] = l > bound ? bound : (l < -bound ? -bound : l);
                 }
             }
