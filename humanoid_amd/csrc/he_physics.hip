@@ -102,8 +102,8 @@ struct Lds {
 #ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
 #define HE_PRED_LEVELS 0
 #endif
-#ifndef HE_PRED_LT_GROUPS  // the midpoint bias's L^-T pass in groups of independent pivots (1) or one by one (0)
-#define HE_PRED_LT_GROUPS 1
+#ifndef HE_PRED_LT_GROUPS  // the midpoint bias's L^-T pass: in groups of independent pivots with the row loads
+#define HE_PRED_LT_GROUPS 2  // one group ahead (2), in groups (1), one pivot at a time (0): 2 is +4.3 % (r03 A/B)
 #endif
 #ifndef HE_PRED_JUMP  // the midpoint bias's velocities / accelerations by pointer jumping (1) or chain walks (0)
 #define HE_PRED_JUMP 1
@@ -1186,7 +1186,9 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // forward substitution replayed from the stored factor
 HE_DEV void mid_lt(Lds& L, const BodyTopo& T, int lane, float c1, float c2) {
     using regla::NH;
-#if HE_PRED_LT_GROUPS
+#if HE_PRED_LT_GROUPS == 2
+    regla::solve_LT_vec_pipelined(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+#elif HE_PRED_LT_GROUPS
     regla::solve_LT_vec_groups<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
 #else
     regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
@@ -2335,12 +2337,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     STAMP(12);
 }
 
-// two waves per SIMD need at most 256 VGPRs + AGPRs. The kernel fits (251) without a bound, and
-// the bound itself costs 1.7 % (r03 A/B: the scheduler works to a tighter register target), so it
-// is off; humanoid_amd/build.py checks the compiler's occupancy report instead and fails the build
-// below 2 waves per SIMD. HE_MIN_WAVES 2 forces the fit (spilling before dropping to one wave).
+// two waves per SIMD need at most 256 VGPRs + AGPRs. Unbounded, the allocator lands at 257 (one
+// kernel-lifetime value parked in an AGPR) and the kernel falls to one wave per SIMD; the bound
+// makes it fit without scratch. humanoid_amd/build.py checks the compiler's occupancy report and
+// fails the build below 2 waves per SIMD either way. (Round 3 A/B, profiles/r03/ab_lt_pipe.txt:
+// the pipelined midpoint L^-T with the bound +3.0 % against the grouped one without it, which
+// fits in 251 unbounded.)
 #ifndef HE_MIN_WAVES
-#define HE_MIN_WAVES 1
+#define HE_MIN_WAVES 2
 #endif
 __global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
     extern __shared__ float smem[];

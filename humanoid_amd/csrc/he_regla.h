@@ -463,6 +463,77 @@ constexpr int kElimGroupMax = HE_ELIM_GMAX;
 constexpr ElimGroups<kElimGroupMax> kElimGroups{};
 constexpr ElimGroups<8> kLTGroups{};  // solve_LT_vec_groups: 30 groups
 
+// solve_LT_vec_groups with the packed-row loads one group ahead: group G+1's L entries are read
+// (every lane, its own ancestor offset, clamped into the factor) while group G's pivots are
+// broadcast and applied, so a group pays its readlanes and FMAs but not an LDS round trip. The
+// update stays exec-masked to the pivot's ancestor lanes; same operations in the same order as
+// solve_LT_vec_groups (bit-identical).
+#ifndef HE_LT_PIPE_GROUP
+#define HE_LT_PIPE_GROUP 4
+#endif
+constexpr ElimGroups<HE_LT_PIPE_GROUP> kLTPipeGroups{};
+template <int G>
+struct LTGroup {
+    static constexpr int S0 = G < kLTPipeGroups.count ? kLTPipeGroups.start[G] : 0;
+    static constexpr int N = G < kLTPipeGroups.count ? kLTPipeGroups.start[G + 1] - S0 : 1;
+};
+template <int S0, int Q, int N>
+__device__ __forceinline__ void lt_group_load(const float* Lp, int dj, int dj2, float (&l1)[N], float (&l2)[N]) {
+    if constexpr (Q < N) {
+        constexpr int K = kElimOrder[S0 + Q];
+        constexpr int top = kPackStart[K] + (kDofNanc[K] > 1 ? kDofNanc[K] - 2 : 0);  // the row's last entry
+        if constexpr (kDofNanc[K] - 1 > 0) {
+            const int o1 = kPackStart[K] + dj;
+            l1[Q] = Lp[o1 < top ? o1 : top];
+            if constexpr (K > 64) {
+                const int o2 = kPackStart[K] + dj2;
+                l2[Q] = Lp[o2 < top ? o2 : top];
+            }
+        }
+        lt_group_load<S0, Q + 1, N>(Lp, dj, dj2, l1, l2);
+    }
+}
+template <int S0, int Q, int N>
+__device__ __forceinline__ void lt_group_apply(const float (&l1)[N], const float (&l2)[N], const float (&yk)[N],
+                                               float& yl, float& y2) {
+    if constexpr (Q < N) {
+        constexpr int K = kElimOrder[S0 + Q];
+        if constexpr (kDofNanc[K] - 1 > 0) {
+            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
+            if (lanes<lo>()) yl = yl - l1[Q] * yk[Q];
+            if constexpr (K > 64) {
+                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
+                if (lanes<hi>()) y2 = y2 - l2[Q] * yk[Q];
+            }
+        }
+        lt_group_apply<S0, Q + 1, N>(l1, l2, yk, yl, y2);
+    }
+}
+template <int G>
+__device__ __forceinline__ void solve_LT_vec_pipe(const float* Lp, int dj, int dj2, float& yl, float& y2,
+                                                  const float (&l1)[LTGroup<G>::N], const float (&l2)[LTGroup<G>::N]) {
+    if constexpr (G < kLTPipeGroups.count) {
+        using C = LTGroup<G>;
+        using Nx = LTGroup<G + 1>;
+        float n1[Nx::N], n2[Nx::N];
+        if constexpr (G + 1 < kLTPipeGroups.count) {
+            int off = 0;
+            asm volatile("" : "+v"(off));  // the loads stay here, one group ahead
+            lt_group_load<Nx::S0, 0, Nx::N>(Lp + off, dj, dj2, n1, n2);
+        }
+        float yk[C::N];
+        lt_group_read<C::S0, 0, C::N>(yk, yl, y2);
+        lt_group_apply<C::S0, 0, C::N>(l1, l2, yk, yl, y2);
+        __builtin_amdgcn_sched_barrier(0);
+        solve_LT_vec_pipe<G + 1>(Lp, dj, dj2, yl, y2, n1, n2);
+    }
+}
+__device__ __forceinline__ void solve_LT_vec_pipelined(const float* Lp, int dj, int dj2, float& yl, float& y2) {
+    float l1[LTGroup<0>::N], l2[LTGroup<0>::N];
+    lt_group_load<LTGroup<0>::S0, 0, LTGroup<0>::N>(Lp, dj, dj2, l1, l2);
+    solve_LT_vec_pipe<0>(Lp, dj, dj2, yl, y2, l1, l2);
+}
+
 template <int G>
 __device__ __forceinline__ void solve_LT_vec_groups(const float* Lp, int dj, int dj2, float& yl, float& y2) {
     if constexpr (G < kLTGroups.count) {
