@@ -100,7 +100,7 @@ struct Lds {
 #define HE_DELASSUS48 1
 #endif
 #ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
-#define HE_PRED_LEVELS 0
+#define HE_PRED_LEVELS 1
 #endif
 #ifndef HE_PRED_LT_GROUPS  // the midpoint bias's L^-T pass: in groups of independent pivots with the row loads
 #define HE_PRED_LT_GROUPS 2  // one group ahead (2), in groups (1), one pivot at a time (0): 2 is +4.3 % (r03 A/B)
@@ -1316,7 +1316,9 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
     sync();
     STAMP(26);
 #if HE_PRED_LEVELS
-    // subtree sums of the new body forces, in place by body levels (as the first bias's)
+    // subtree sums of the new body forces, in place by body levels (as the first bias's): +4.8 %
+    // against the per-dof-lane sums below (r03 A/B, profiles/r03/ab_pred_levels.txt, under the
+    // two-wave bound that lets it fit)
     subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.Acc[0][0], nullptr, lane);
     auto corr = [&](int i) {
         const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
@@ -1324,8 +1326,7 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
     };
 #else
     // lane = dof (then dofs 64..74 on lanes 0..10): dc_i = dt (S_i . F_b(u0) - S_i . F_b(um)) with the
-    // subtree sums of the new body forces (the level-parallel sums measured 2 VGPRs over the
-    // kernel's 2-waves budget)
+    // subtree sums of the new body forces, 24 masked body reads per lane
     auto corr = [&](int i) {
         const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
         const uint32_t sm = T.sub_mask[bi];

@@ -165,6 +165,13 @@ def set_drop_gap_out(arr=None):
     lib().ho_set_drop_gap_out(None if arr is None else arr.ctypes.data_as(C.POINTER(C.c_float)))
 
 
+def set_row_weight_out(arr=None):
+    """Diagnostics only: float32 [N, HE_MAX_ROWS] that the following physics_step calls fill with the
+    friction bound weight of every solver row of each env's last substep (mu tangential, mu r_patch
+    torsional, 0 normal / limit), in the warm-start cache's row order; None turns it off."""
+    lib().ho_set_row_weight_out(None if arr is None else arr.ctypes.data_as(C.POINTER(C.c_float)))
+
+
 def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, dof_state, targets, substeps=2,
                  mass_scale=None, friction=None, terrain_kind=None, cache=None):
     """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays) and on the warm-start

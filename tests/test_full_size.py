@@ -112,7 +112,7 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     widening (8 probes)."""
     import cases
     from humanoid_amd import _abi
-    from test_gpu_parity import CondStats, _cond_close, contact_keys, friction_states
+    from test_gpu_parity import CondStats, _cond_close, contact_keys, friction_states, torsion_weights
     ro = _rollout("dr", model)
     for _ in range(5):
         ro.step()
@@ -133,14 +133,20 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     for step in range(30):
         ro.eng.step_actions(zero, 2)
         tgt = ro.eng.dof_targets.cpu().numpy()[idx].copy()
-        out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o, **props)
+        rw = np.zeros((len(idx), _abi.MAX_ROWS), np.float32)  # the oracle's row bound weights (torsion)
+        O.set_row_weight_out(rw)
+        try:
+            out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=c_o, **props)
+        finally:
+            O.set_row_weight_out(None)
         for k, pr in enumerate(probes):  # fp32-level noise in every step
             pr[3] = cases.probe_physics_step(he_model, sp, pr[0], pr[1], tgt, 2, pr[2], 123 + 1000 * k + step, **props)
         torch.cuda.synchronize()
         cg = ro.eng.contact_cache.cpu().numpy()[idx]
         mism |= np.array([a != b for a, b in zip(contact_keys(cg), contact_keys(c_o))])
-        slip |= np.array([a != b for a, b in zip(friction_states(cg, props["friction"]),
-                                                 friction_states(c_o, props["friction"]))])
+        tw = torsion_weights(rw, c_o)
+        slip |= np.array([a != b for a, b in zip(friction_states(cg, props["friction"], tw),
+                                                 friction_states(c_o, props["friction"], tw))])
         hist.append((ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy(),
                      ro.eng.rb_state.view(4096, 24, 13).cpu().numpy()[idx].copy(), dof.copy(),
                      out["rb_state"].copy(), [p[1].copy() for p in probes], [p[3]["rb_state"].copy() for p in probes]))

@@ -369,15 +369,24 @@ def contact_keys(cache):
     return [tuple(sorted(int(k) for k in keys[e, :n[e]] if (k >> 14) == 0)) for e in range(keys.shape[0])]
 
 
-def friction_states(cache, mu):
-    """Per env: the stick / slip state of every tangential friction row of the last solve, from a
-    warm-start cache: sorted (key, s) with s = +1 / -1 when the impulse sits on its bound
-    +-mu (sum of its patch's normal impulses) (within 1e-6 of it: the clamp acted, sliding), 0
-    inside (sticking); patches with no normal impulse left out (torsional rows too: their bound's
-    patch radius is not in the cache). A friction row crossing its bound is a discontinuity of the
-    step like a contact entering the set: where the fp32 engine and the fp64 oracle land on
-    different sides, their trajectories part by the slip, so such envs are excluded like
-    contact-set mismatches."""
+def torsion_weights(weights, cache):
+    """Per env: {row key: friction bound weight} of the torsional rows, from the oracle's row-weight
+    diagnostic (oracle.set_row_weight_out) [N, HE_MAX_ROWS] and its warm-start cache (same row order)."""
+    n, keys, _ = _abi.cache_rows(cache)
+    return [{int(keys[e, r]): float(weights[e, r]) for r in range(n[e]) if (keys[e, r] >> 14) == 3}
+            for e in range(keys.shape[0])]
+
+
+def friction_states(cache, mu, tw=None):
+    """Per env: the stick / slip state of every friction row of the last solve, from a warm-start
+    cache: sorted (key, s) with s = +1 / -1 when the impulse sits on its bound (within 1e-5 of it:
+    the clamp acted, sliding), 0 inside (sticking); patches with no normal impulse left out. A
+    tangential row's bound is mu (sum of its patch's normal impulses); a torsional row's is its
+    weight mu r_patch times that sum, the weight from `tw` (torsion_weights of the oracle's solve:
+    the patch radius is not in the cache; without `tw` the torsional rows are left out). A friction
+    row crossing its bound is a discontinuity of the step like a contact entering the set: where the
+    fp32 engine and the fp64 oracle land on different sides, their trajectories part by the slip, so
+    such envs are excluded like contact-set mismatches."""
     n, keys, lam = _abi.cache_rows(cache)
     mu = np.broadcast_to(np.asarray(mu, np.float32), (keys.shape[0],))
     out = []
@@ -386,7 +395,7 @@ def friction_states(cache, mu):
         ks = [int(k) for k in keys[e, :n[e]]]
         for r, key in enumerate(ks):
             b0, b1, sub, kind = _abi.key_fields(key)
-            if kind not in (1, 2):
+            if kind == 0 or (kind == 3 and (tw is None or key not in tw[e])):
                 continue
             if sub == _abi.KEY_PATCH:  # the body's terrain patch: its normal rows
                 ln = sum(float(lam[e, j]) for j, k2 in enumerate(ks)
@@ -395,7 +404,8 @@ def friction_states(cache, mu):
                 ln = sum(float(lam[e, j]) for j, k2 in enumerate(ks) if k2 == (key & 0x3FFF))
             if ln <= 1e-5:
                 continue
-            bound = float(mu[e]) * ln * (1.0 - 1e-6)
+            w = float(mu[e]) if kind < 3 else tw[e][key]
+            bound = w * ln * (1.0 - 1e-5)
             st.append((key, int(np.sign(lam[e, r])) if abs(lam[e, r]) >= bound else 0))
         out.append(tuple(sorted(st)))
     return out
@@ -448,7 +458,12 @@ def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-
     slip = np.zeros(n, bool)
     for step in range(steps):
         eng.simulate(calls)
-        out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, calls, cache=c_o, **props)
+        rw = np.zeros((n, _abi.MAX_ROWS), np.float32)  # the oracle's row bound weights (torsion stick / slip)
+        O.set_row_weight_out(rw)
+        try:
+            out = O.physics_step(eng.he_model, sp, r_o, d_o, targets, calls, cache=c_o, **props)
+        finally:
+            O.set_row_weight_out(None)
         for k, pr in enumerate(probes):
             pr[2] = cases.probe_physics_step(eng.he_model, sp, pr[0], pr[1], targets, calls, pr[3], 123 + 1000 * k + step,
                                              **props)
@@ -458,7 +473,8 @@ def _physics_compare(he_model, root, dof, targets, calls=2, steps=1, pos_tol=1e-
         ko = contact_keys(c_o)
         mismatch |= np.array([a != b for a, b in zip(kg, ko)])
         mu = props["friction"] if "friction" in props else sp.friction
-        slip |= np.array([a != b for a, b in zip(friction_states(cg, mu), friction_states(c_o, mu))])
+        tw = torsion_weights(rw, c_o)
+        slip |= np.array([a != b for a, b in zip(friction_states(cg, mu, tw), friction_states(c_o, mu, tw))])
         mismatch |= eng.num_contacts.cpu().numpy() != out["num_contacts"]
         mismatch |= eng.dropped_contacts.cpu().numpy() != out["dropped"]
     excl = mismatch | (slip if max_slip > 0 else False)
