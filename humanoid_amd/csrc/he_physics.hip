@@ -99,6 +99,9 @@ struct Lds {
 #ifndef HE_DELASSUS48
 #define HE_DELASSUS48 1
 #endif
+#ifndef HE_PGS_OPAQUE_MASK  // PGS bound weights formed per row (1) or hoisted by the compiler (0)
+#define HE_PGS_OPAQUE_MASK 0
+#endif
 #ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
 #define HE_PRED_LEVELS 1
 #endif
@@ -2146,7 +2149,17 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 // lane-mask pairs (SGPR spills)
                 int nrs = nru;
                 asm volatile("" : "+s"(nrs));
+#if HE_PGS_OPAQUE_MASK
+                // the patch masks and weights through opaque copies per sweep: the per-row bound
+                // weights are formed in the sweep (2 VALU per row) instead of being hoisted out of
+                // the loop as 63 VGPRs
+                uint32_t mlo_ = mlo, mhi_ = mhi;
+                float muw_ = muw;
+                asm volatile("" : "+v"(mlo_), "+v"(mhi_), "+v"(muw_));
+                pgs_sweep<0>(cd, dvec, lo, hi, acol, mlo_, mhi_, muw_, nrs);
+#else
                 pgs_sweep<0>(cd, dvec, lo, hi, acol, mlo, mhi, muw, nrs);
+#endif
                 // the bound at the sweep's end: B = hi + lambda(start); then the bounds about the new impulse
                 const float bn = hi + lamv;
                 lamv += dvec;

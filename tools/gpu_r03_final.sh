@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-3 final measurement session: the default bench (CPU baseline, PHCPufferEnv level, tracking,
+# round 2's scheme), the configs[2] and configs[4] bench lines, rocprofv3 kernel stats of the quick
+# bench command, the phase profile, action regimes, contact histograms and every PMC pass.
+# Each GPU step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:-r03f}
+Q="bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-puffer-level --no-tracking"
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_full_$TAG.log 2>&1 &&
+timeout -k 10 200 python -u bench.py --config imitation --no-cpu-baseline --no-puffer-level > gpurun_out/bench_imit_$TAG.log 2>&1 &&
+timeout -k 10 200 python -u bench.py --config dr --no-cpu-baseline --no-puffer-level --no-tracking > gpurun_out/bench_dr_$TAG.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 $Q > gpurun_out/bench_prof_$TAG.log 2>&1 &&
+timeout -k 10 300 python tools/phase_profile.py > gpurun_out/phases_$TAG.json 2> gpurun_out/phases_$TAG.err &&
+timeout -k 10 300 python -u tools/action_regimes.py > gpurun_out/action_regimes_$TAG.json 2> gpurun_out/action_regimes_$TAG.err &&
+timeout -k 10 200 python -u tools/contact_histogram.py > gpurun_out/contact_histogram_$TAG.json 2> gpurun_out/contact_histogram_$TAG.err &&
+bash tools/gpu_pmc_all.sh $TAG
+rc=$?
+tail -1 gpurun_out/bench_full_$TAG.log | cut -c1-600
+find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \; 2>/dev/null | head -3 | cut -c1-150
+tail -7 gpurun_out/action_regimes_$TAG.err
+exit $rc
