@@ -64,6 +64,7 @@ struct he_engine {
     int32_t* dropped = nullptr;
     float* cache = nullptr;
     float* init_root = nullptr;     // [N,13] HE_BUF_INIT_ROOT_STATE
+    int32_t* meta_cache = nullptr;  // [N,8] the imitation kernel's per-env motion-metadata cache
     float* d_rest = nullptr;        // [24,3] zero-pose body origins in the root frame
     bool component_limits = false;  // a dof bound inside (-pi + guard, pi - guard): not implemented
     int fused_step = -1;            // he_env_step as one launch: 1 / 0 (he_set_fused_step), -1 auto
@@ -194,6 +195,8 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     HE_CHECK(hipMemset(h->num_contacts, 0, (size_t)N * sizeof(int32_t)));
     HE_CHECK(hipMemset(h->dropped, 0, (size_t)N * sizeof(int32_t)));
     HE_CHECK(hipMemset(h->cache, 0, (size_t)N * HE_CACHE_WORDS * sizeof(float)));
+    HE_CHECK(dalloc(&h->meta_cache, (size_t)N * 8));
+    HE_CHECK(hipMemset(h->meta_cache, 0xFF, (size_t)N * 8 * sizeof(int32_t)));  // motion -1: empty
     h->num_envs = N;
     return 0;
 }
@@ -202,7 +205,7 @@ int he_destroy(he_engine* h) {
     if (!h) return 0;
     hipSetDevice(h->device);
     void* ptrs[] = {h->d_model, h->d_topo, h->root, h->dof_state, h->rb, h->cf, h->dof_force, h->targets,
-                    h->num_contacts, h->dropped, h->cache, h->init_root, h->d_rest, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
+                    h->num_contacts, h->dropped, h->cache, h->init_root, h->meta_cache, h->d_rest, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
                     h->m_dt, h->m_starts, h->m_nframes};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -357,6 +360,12 @@ int he_refresh(he_engine* h, void* stream) {
     return 0;
 }
 
+// new motion tables: the imitation kernel's per-env metadata cache (keyed by motion id) is stale
+static hipError_t invalidate_meta_cache(he_engine* h) {
+    if (!h->meta_cache) return hipSuccess;
+    return hipMemset(h->meta_cache, 0xFF, (size_t)h->num_envs * 8 * sizeof(int32_t));
+}
+
 int he_load_motions(he_engine* h, int64_t F, int M, const float* gts, const float* grs, const float* lrs,
                     const float* gvs, const float* gavs, const float* dvs, const int64_t* length_starts,
                     const int64_t* num_frames, const float* lengths, const float* dt) {
@@ -404,6 +413,7 @@ int he_load_motions(he_engine* h, int64_t F, int M, const float* gts, const floa
     HE_CHECK(hipMemcpy(h->m_nframes, num_frames, M * sizeof(int64_t), hipMemcpyHostToDevice));
     h->m_frames = F;
     h->m_motions = M;
+    HE_CHECK(invalidate_meta_cache(h));
     return 0;
 }
 
@@ -477,6 +487,7 @@ int he_ingest_clips(he_engine* h, int num_clips, const int64_t* host_num_frames,
     HE_CHECK(e2);
     h->m_frames = F;
     h->m_motions = num_motions;
+    HE_CHECK(invalidate_meta_cache(h));
     return 0;
 }
 
@@ -509,6 +520,7 @@ static int imit_common(he_engine* h, const he_imitation_params* p, const he_env_
     a.has_eval = h->has_eval;
     a.init_root = h->init_root;
     a.rest_pos = h->d_rest;
+    a.meta_cache = h->meta_cache;
     if (p->state_init < HE_STATE_INIT_DEFAULT || p->state_init > HE_STATE_INIT_HYBRID)
         return fail("%s: state_init %d is not a StateInit (0 Default, 1 Start, 2 Random, 3 Hybrid)", what, p->state_init);
     if (p->state_init == HE_STATE_INIT_HYBRID && !(p->hybrid_init_prob >= 0.f && p->hybrid_init_prob <= 1.f))

@@ -179,8 +179,15 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
     // Dependent global round trips are the cost of this kernel, so every load that does not depend
     // on a motion-table index is issued first, and both motion samples (t for reward/reset, t+dt
     // for the observation) are selected from one metadata read and loaded together before any store.
-    // trip 1: env bookkeeping, the simulated body row, the power-reward operands
+    // trip 1: env bookkeeping, the env's motion-metadata cache, the simulated body row, the
+    // power-reward operands
     const int64_t mid = clamp_mid(a.m, a.motion_ids[e]);
+    int4 mc0 = make_int4(-1, -1, 0, 0), mc1 = make_int4(0, 0, 0, 0);
+    if (a.meta_cache) {
+        const int4* mc = reinterpret_cast<const int4*>(a.meta_cache + (size_t)e * 8);
+        mc0 = mc[0];
+        mc1 = mc[1];
+    }
     f3 off = f3{a.global_offset[3 * e], a.global_offset[3 * e + 1], a.global_offset[3 * e + 2]};
     float start = a.start_times[e], soff = a.start_offsets[e];
     int prog = a.progress[e];
@@ -191,7 +198,23 @@ __global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
         const float* v = a.dof_state + ((size_t)e * ND + 3 * lane) * 2 + 1;
         pw = power_term(f, v, 2);
     }
-    imitation_group<EVAL>(a, slot, e, lane, lane == 0, mid, off, start, soff, prog, s, pw);
+    // trip 2 (only when the env's motion changed since its last step, or the tables were reloaded:
+    // the cache is keyed by the motion id and cleared on a load): the motion's metadata
+    auto i64 = [](int lo, int hi) { return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo); };
+    MotionMeta mm;
+    if (a.meta_cache && i64(mc0.x, mc0.y) == mid) {  // uniform in the env's group
+        mm = MotionMeta{__int_as_float(mc0.z), __int_as_float(mc0.w), i64(mc1.x, mc1.y), i64(mc1.z, mc1.w)};
+    } else {
+        mm = motion_meta(a.m, mid);
+        if (a.meta_cache && lane == 0) {
+            int4* mc = reinterpret_cast<int4*>(a.meta_cache + (size_t)e * 8);
+            mc[0] = make_int4((int)(uint32_t)mid, (int)((uint64_t)mid >> 32), __float_as_int(mm.len), __float_as_int(mm.dt));
+            mc[1] = make_int4((int)(uint32_t)mm.nf, (int)((uint64_t)mm.nf >> 32), (int)(uint32_t)mm.start,
+                              (int)((uint64_t)mm.start >> 32));
+        }
+    }
+    imitation_finish<EVAL>(a, slot, e, lane, lane == 0,
+                           imitation_frames(a, lane, ImitBook{mid, off, start, soff, prog, mm}), s, pw);
 }
 
 // MotionLibBase.get_motion_state for K queries (motion_lib.py:549-626)

@@ -50,6 +50,8 @@ struct ImitArgs {
     int has_eval;
     const float* init_root;  // [N,13] HE_BUF_INIT_ROOT_STATE (the Default / Hybrid state init)
     const float* rest_pos;   // [24,3] body origins of the zero pose in the root frame (model)
+    int32_t* meta_cache;     // [N,8] per-env motion metadata (motion id, length, dt, frames, start) of the
+                             // last step; null = read the motion tables every step
 };
 
 // AMP observation update, launched after an imitation launch

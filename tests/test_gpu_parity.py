@@ -116,6 +116,48 @@ def _load_env_state(eng, g):
     eng.dof_force.copy_(cu(g["dof_force"].reshape(-1)))
 
 
+def test_motion_reload_invalidates_metadata_cache(he_model, golden):
+    """The imitation kernel keeps each env's motion metadata (length, dt, frame count, start) from its
+    last step, keyed by the motion id (he_engine meta cache). A motion-table reload must not reuse
+    it: after a step on the golden tables, a reload with the motions' order reversed (same ids, other
+    clips), then a step, equals that step on a fresh engine that only ever saw the reversed tables."""
+    from humanoid_amd.motion_lib import MotionTables
+    g = golden("env_step")
+    n = g["rb_state"].shape[0]
+    t = tables_from_golden(g)
+    M = len(t.num_frames)
+    if M < 2:
+        pytest.skip("the golden env step has one motion")
+    rev = np.arange(M)[::-1]
+    lens, starts = np.asarray(t.num_frames), np.asarray(t.length_starts)
+    order = np.concatenate([np.arange(starts[m], starts[m] + lens[m]) for m in rev])
+    F = lambda x: np.asarray(x)[order]  # noqa: E731
+    t2 = MotionTables(gts=F(t.gts), grs=F(t.grs), lrs=F(t.lrs), gvs=F(t.gvs), gavs=F(t.gavs), dvs=F(t.dvs),
+                      num_frames=lens[rev], length_starts=np.concatenate([[0], np.cumsum(lens[rev])[:-1]]),
+                      lengths=np.asarray(t.lengths)[rev], dt=np.asarray(t.dt)[rev], fps=np.asarray(t.fps)[rev])
+
+    def step(eng):
+        _load_env_state(eng, g)
+        em = eng.env_motion(cu(g["motion_ids"], torch.int64), cu(g["start_times"]), cu(g["start_offsets"]),
+                            cu(g["global_offset"]), cu(g["progress_in"], torch.int16))
+        out = [torch.zeros(n, 934, device="cuda:0"), torch.zeros(n, device="cuda:0"), torch.zeros(n, 5, device="cuda:0"),
+               torch.zeros(n, dtype=torch.uint8, device="cuda:0"), torch.zeros(n, dtype=torch.uint8, device="cuda:0")]
+        eng.imitation_step(_abi.imitation_params(), em, *out)
+        torch.cuda.synchronize()
+        return [o.cpu().numpy() for o in out]
+
+    e1 = make_engine(he_model, n)
+    e1.load_motions(t)
+    step(e1)
+    e1.load_motions(t2)
+    got = step(e1)
+    e2 = make_engine(he_model, n)
+    e2.load_motions(t2)
+    want = step(e2)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_imitation_step_matches_golden_and_oracle(he_model, golden):
     g = golden("env_step")
     n = g["rb_state"].shape[0]
