@@ -77,6 +77,28 @@ def center_of_mass(model, rb_state):
     return (com_w * m[None, :, None]).sum(1) / m.sum()
 
 
+def com_velocity(model, rb_state):
+    """Mass-weighted centre-of-mass velocity [N,3] from rigid-body rows [N,24,13] (origin velocity
+    v, angular velocity w: each body's COM moves at v + w x R com)."""
+    rb = np.asarray(rb_state, np.float64)
+    R = _qmat(rb[..., 3:7])
+    r = np.einsum("nbij,bj->nbi", R, np.asarray(model.com, np.float64))
+    vc = rb[..., 7:10] + np.cross(rb[..., 10:13], r)
+    m = np.asarray(model.mass, np.float64)
+    return (vc * m[None, :, None]).sum(1) / m.sum()
+
+
+def sliding_deceleration(vx, dt, v_min=0.5):
+    """Fitted slope of the x velocity [T, N] over the samples while the env still slides (v > v_min),
+    per env (nan with fewer than 4 such samples)."""
+    t = (np.arange(vx.shape[0]) + 1) * dt
+    out = []
+    for e in range(vx.shape[1]):
+        on = vx[:, e] > v_min
+        out.append(np.polyfit(t[on], vx[on, e], 1)[0] if on.sum() > 3 else np.nan)
+    return np.array(out)
+
+
 def ground_gaps(model, rb_state):
     """Signed distance to the z=0 plane of every terrain contact candidate of each body (sphere
     centre, capsule end points, box corners, minus the radius) -> min over candidates [N,24]."""

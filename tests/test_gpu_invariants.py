@@ -182,3 +182,32 @@ def test_gpu_moderate_random_actions_stay_physical(he_model, model):
     q = eng.dof_state.view(n, 69, 2)[..., 0].reshape(n, 23, 3).norm(dim=-1)
     assert vmax < 10.0, vmax
     assert float(q.max()) < np.pi - 0.01
+
+
+def test_gpu_sliding_bodies_decelerate_at_mu_g(he_model, model):
+    """The engine side of tests/test_physics_invariants.py::test_sliding_body_decelerates_at_mu_g at
+    1024 envs: lying bodies, settled, given 3 m/s along x, decelerate at mu g while they slide on
+    their contact patches (per-env friction 0.25 / 0.5 / 0.75 / 1.0). Per friction, the median fitted
+    deceleration within 5 % of mu g, and at least 75 % of the envs within 5 % (bodies that tip and
+    roll decelerate less)."""
+    n = 1024
+    rng = np.random.default_rng(3)
+    root, dof = cases.lying_state(n, rng, on_floor=True, model=model)
+    eng = _engine(he_model, n)
+    _load(eng, root, dof, dof[..., 0])
+    for _ in range(45):  # settle 1.5 s
+        eng.simulate(2)
+    mus = np.array([0.25, 0.5, 0.75, 1.0], np.float32)[np.arange(n) % 4]
+    eng.set_env_properties(None, torch.as_tensor(mus, device="cuda:0"), None)
+    eng.root_states[:, 7] += 3.0
+    vs = []
+    for _ in range(30):
+        eng.simulate(2)
+        vs.append(cases.com_velocity(model, eng.rb_state.view(n, 24, 13).cpu().numpy())[:, 0])
+    dec = cases.sliding_deceleration(np.array(vs), 1.0 / 30.0)
+    for mu in (0.25, 0.5, 0.75, 1.0):
+        d = dec[mus == mu]
+        good = np.abs(d + mu * 9.81) < 0.05 * mu * 9.81
+        print(f"mu {mu}: median deceleration {np.nanmedian(d):.3f} (mu g {mu * 9.81:.3f}), within 5%: {good.mean():.2f}")
+        assert abs(np.nanmedian(d) + mu * 9.81) < 0.05 * mu * 9.81
+        assert good.mean() >= 0.75

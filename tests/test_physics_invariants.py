@@ -253,3 +253,30 @@ def test_saturated_random_actions_stay_physical(he_model, model):
     assert q.max() <= np.pi - 0.01 + 1e-5  # the limit backstop's cap at most
     vexp, _, _ = _random_action_run(he_model, model, 1.0, 32, 60, bias_midpoint=0)
     assert (vexp > 10.0).sum() > 8, vexp  # the explicit scheme's runaway in the same run
+
+
+@pytest.mark.parametrize("mu", [0.25, 0.5])
+def test_sliding_body_decelerates_at_mu_g(he_model, model, mu):
+    """Coulomb friction with patch friction rows: a lying body, settled, then given
+    3 m/s along x (every body), slides on its contact patches and decelerates at mu g while it
+    slides (the tangent basis of the plane's normal has t1 = x, so the pyramid bound is mu lambda_n
+    along the motion). Median over 8 envs of the fitted deceleration within 5 % of mu g (an env
+    that tips and rolls decelerates less; at most 2 of 8 may)."""
+    rng = np.random.default_rng(3)
+    n = 8
+    root, dof = cases.lying_state(n, rng, on_floor=True, model=model)
+    tgt = dof[..., 0].copy()
+    sp = _abi.default_sim_params()
+    cache = O.new_cache(n)
+    for _ in range(45):  # settle 1.5 s
+        O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache)
+    root[:, 7] += 3.0
+    fr = np.full(n, mu, np.float32)
+    vs = []
+    for _ in range(30):
+        out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache, friction=fr)
+        vs.append(cases.com_velocity(model, out["rb_state"])[:, 0])
+    dec = cases.sliding_deceleration(np.array(vs), 1.0 / 30.0)
+    good = np.abs(dec + mu * 9.81) < 0.05 * mu * 9.81
+    assert abs(np.nanmedian(dec) + mu * 9.81) < 0.05 * mu * 9.81, dec
+    assert good.sum() >= n - 2, dec
