@@ -240,3 +240,68 @@ def test_limit_force_is_part_of_dof_force(he_model, model):
     o2 = O.physics_step(he_model, sp, r2, d2, targets, 2, cache=O.new_cache(n))
     f = o2["dof_force"][:, [4, 16]]
     assert (np.abs(f) > 100.0).all(), f
+
+
+def test_patch_friction_rows(he_model, model):
+    """Patch friction: a standing body's 16 box corners are 4 patches (feet and toes), so
+    its solve has 16 normal rows, then per patch 2 tangential rows and 1 torsional row: 28 rows. The
+    row keys: the normal rows carry their corner keys, a patch's friction rows the body's patch key
+    (HE_KEY_PATCH) with kinds 1, 2, 3. The torsional rows' bound weight is mu times the corners'
+    mean distance from their centroid (the oracle's row-weight diagnostic), between the foot boxes'
+    half-widths and half-diagonals."""
+    rng = np.random.default_rng(4)
+    n = 3
+    root, dof = cases.standing_state(model, n, rng)
+    sp = _abi.default_sim_params()
+    cache = O.new_cache(n)
+    for _ in range(3):
+        O.physics_step(he_model, sp, root, dof, np.zeros((n, 69), np.float32), 2, cache=cache)
+    rw = np.zeros((n, _abi.MAX_ROWS), np.float32)
+    O.set_row_weight_out(rw)
+    try:
+        O.physics_step(he_model, sp, root, dof, np.zeros((n, 69), np.float32), 2, cache=cache)
+    finally:
+        O.set_row_weight_out(None)
+    cnt, keys, lam = _abi.cache_rows(cache)
+    assert cnt.tolist() == [28] * n
+    for e in range(n):
+        f = [_abi.key_fields(k) for k in keys[e, :28]]
+        normals = [x for x in f if x[3] == 0]
+        friction = [x for x in f if x[3] > 0]
+        assert len(normals) == 16 and all(x[1] == -1 and x[2] < 8 for x in normals)
+        assert sorted({x[0] for x in normals}) == sorted({x[0] for x in friction})  # 4 bodies
+        assert all(x[2] == _abi.KEY_PATCH for x in friction)
+        assert sorted(x[3] for x in friction) == [1] * 4 + [2] * 4 + [3] * 4
+        # Gauss-Seidel order: each patch's normal rows, then its friction rows
+        for r in range(1, 28):
+            if f[r][3] == 0 and f[r - 1][3] == 0:
+                assert f[r][0] == f[r - 1][0]  # consecutive normals belong to one patch
+        tors = rw[e, :28][[x[3] == 3 for x in f]]
+        assert ((tors > 0.02) & (tors < 0.2)).all(), tors  # mu = 1: r_patch in metres
+        assert (lam[e, :28][[x[3] == 0 for x in f]] >= 0).all()
+
+
+def test_row_budget_caps_the_solve_at_63_rows(he_model, model):
+    """Lying bodies generate up to ~30 contacts, more rows than one wave holds: the reduction keeps
+    the deepest contacts while their rows fit (3 for a body's first terrain point or a self pair, 2
+    for its second, 1 after), so every cached solve has at most 63 rows, and the envs that overflow
+    drop only speculative contacts (gap > 0) once settled."""
+    rng = np.random.default_rng(5)
+    n = 32
+    root, dof = cases.lying_state(n, rng, on_floor=True, model=model)
+    sp = _abi.default_sim_params()
+    cache = O.new_cache(n)
+    tgt = dof[..., 0].copy()
+    for _ in range(40):
+        out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache)
+    gaps = np.full(n, np.inf, np.float32)
+    O.set_drop_gap_out(gaps)
+    try:
+        out = O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache)
+    finally:
+        O.set_drop_gap_out(None)
+    cnt = cache[:, 7].view(np.int32)
+    assert (cnt <= _abi.MAX_ROWS).all() and (out["num_contacts"] <= _abi.MAX_CONTACTS).all()
+    dropping = out["dropped"] > 0
+    assert dropping.any(), "the case must overflow the row budget"
+    assert (gaps[dropping] > 5e-3).all(), gaps[dropping]  # only speculative contacts go
