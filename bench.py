@@ -52,6 +52,8 @@ def parse(argv=None):
                     help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 sweeps, "
                          "link world angular-velocity clamp; r02 = round 2's energy-unstable step (2 x 1/60 s, "
                          "explicit bias, 8 sweeps) with round 3's clamps, for the cost comparison only (DESIGN §5)")
+    ap.add_argument("--solver-tolerance", type=float, default=None,
+                    help="he_sim_params.solver_tolerance override (m/s; 0 = every sweep runs)")
     ap.add_argument("--no-puffer-level", action="store_true",
                     help="skip the PHCPufferEnv.step-level rate (numpy actions in, host bookkeeping)")
     ap.add_argument("--puffer-steps", type=int, default=50)
@@ -254,10 +256,13 @@ def sim_substeps(args):
 
 
 def scheme_params(args):
-    """he_sim_params overrides of the --scheme."""
+    """he_sim_params overrides of the --scheme and --solver-tolerance."""
+    out = {}
     if getattr(args, "scheme", "default") == "r02":
-        return dict(substeps=1, bias_midpoint=0, solver_iterations=8)
-    return {}
+        out = dict(substeps=1, bias_midpoint=0, solver_iterations=8)
+    if getattr(args, "solver_tolerance", None) is not None:
+        out["solver_tolerance"] = args.solver_tolerance
+    return out
 
 
 def scheme_leg(args, model, device_index, scheme="r02", steps=50, warmup=10):
