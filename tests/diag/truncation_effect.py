@@ -1,9 +1,10 @@
 """The contact-capacity truncation made visible on the oracle: the same
-fallen / tumbling bodies stepped with the engine's capacity (max_contacts 20, deepest-first
-reduction) and with the oracle's own 64-contact capacity, and the difference reported:
+fallen / tumbling bodies stepped with the engine's capacity (40 slots / 63 solver rows,
+deepest-first row-budgeted reduction) and with the oracle's own 64-slot capacity (no row budget),
+and the difference reported:
 penetration (lowest contact-candidate gap), CoM trajectory, contacts dropped.
 
-  python tests/diag/truncation_effect.py [--envs 128] [--steps 60] > profiles/r02/truncation_effect.json
+  python tests/diag/truncation_effect.py [--envs 128] [--steps 60] > profiles/r03/truncation_effect.json
 """
 import argparse
 import json
@@ -48,22 +49,23 @@ def main():
         rng = np.random.default_rng(11)
         root, dof = cases.lying_state(args.envs, rng, on_floor=on_floor, model=model)
         targets = np.broadcast_to(off, (args.envs, 69)).astype(np.float32).copy()
-        g20, c20, d20, s20 = run(hm, model, root, dof, targets, 20, args.steps)
+        g40, c40, d40, s40 = run(hm, model, root, dof, targets, _abi.MAX_CONTACTS, args.steps)
         g64, c64, d64, s64 = run(hm, model, root, dof, targets, 64, args.steps)
-        com_diff = np.linalg.norm(c20 - c64, axis=-1)
+        com_diff = np.linalg.norm(c40 - c64, axis=-1)
         res[name] = {
             "envs": args.envs, "steps": args.steps,
-            "cap20": {"envs_dropping_any_step": int((d20 > 0).any(0).sum()), "dropped_mean": float(d20.mean()),
-                      "dropped_max": int(d20.max()), "slots_mean": float(s20.mean()),
-                      "min_gap_m": float(g20.min()), "min_gap_p01_m": float(np.percentile(g20.min(0), 1))},
+            "cap40": {"envs_dropping_any_step": int((d40 > 0).any(0).sum()), "dropped_mean": float(d40.mean()),
+                      "dropped_max": int(d40.max()), "slots_mean": float(s40.mean()),
+                      "min_gap_m": float(g40.min()), "min_gap_p01_m": float(np.percentile(g40.min(0), 1))},
             "cap64": {"dropped_max": int(d64.max()), "slots_mean": float(s64.mean()), "slots_max": int(s64.max()),
                       "min_gap_m": float(g64.min()), "min_gap_p01_m": float(np.percentile(g64.min(0), 1))},
             "com_diff_m": {"mean_final": float(com_diff[-1].mean()), "p90_final": float(np.percentile(com_diff[-1], 90)),
                            "max_final": float(com_diff[-1].max())},
         }
     res["definition"] = ("oracle (fp64) lying_state seed 11, PD targets at the action offset (actions 0), 2 substeps; "
-                         "cap20 = the engine's capacity with the deepest-first reduction, cap64 = the oracle's own "
-                         "capacity (no drops; its warm start covers the cache's first 21 slots); min_gap over every body's contact candidates and steps")
+                         "cap40 = the engine's capacity (40 slots, 63 rows) with the deepest-first reduction, cap64 = "
+                         "the oracle's own capacity (64 slots, no row budget; its warm start covers the first 63 rows "
+                         "the cache holds); min_gap over every body's contact candidates and steps")
     print(json.dumps(res, indent=1))
 
 

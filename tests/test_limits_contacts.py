@@ -4,8 +4,9 @@
   as unilateral rows on the exp-map coordinates. The knee-y PD scale is 5 rad (humanoid_phc.py:441-446),
   so a saturated action targets +-5 rad, past the +-pi range: without limits the knee is driven through
   pi, its exp-map coordinate wraps to -pi and the drive keeps spinning it; with limits it stops at pi.
-* Capacity: the engine has HE_MAX_CONTACTS = 21 slots (3 rows each, one wave). Overflow is counted
-  (`dropped`) and the slots go to the deepest contacts, so a lying body's hand keeps its penetrating
+* Capacity: the engine has HE_MAX_CONTACTS = 40 contact slots and HE_MAX_ROWS = 63 solver rows (one
+  wave; patch friction: a normal row per slot, 3 rows per body-ground patch, 3 per self pair). Overflow
+  is counted (`dropped`) and the row budget goes to the deepest contacts first, so a lying body's hand keeps its penetrating
   contact (round 1 truncated in body order: the right arm sank).
 * Warm start: the solve starting from the previous impulses converges where the cold 8-iteration PGS
   does not (stand-still jitter, lying-body residual).
