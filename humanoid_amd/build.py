@@ -29,7 +29,7 @@ SOURCES = [
     ("he_rollout.hip", ["-ffp-contract=off"]),  # GAE: the Cython module's float32 rounding
     ("he_engine.cpp", ["-x", "hip"]),
 ]
-HEADERS = ["he_kernels.h", "he_math.h", "he_topo.h", "he_regla.h", "he_smpl_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h"),
+HEADERS = ["he_kernels.h", "he_math.h", "he_imitation_env.h", "he_topo.h", "he_regla.h", "he_smpl_topo.h", os.path.join("..", "..", "include", "humanoid_engine.h"),
            os.path.join("..", "..", "include", "humanoid_rollout.h")]
 
 

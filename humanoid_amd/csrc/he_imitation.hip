@@ -167,8 +167,14 @@ HE_DEV void eval_record(const he_eval_buffers& ev, int e, int lane, bool act, f3
 
 // EVAL: eval recording compiled in (its fp64 Procrustes solve would otherwise set the register
 // budget of every launch)
+#ifndef HE_IMIT_THREADS  // threads per workgroup of the imitation kernel
+#define HE_IMIT_THREADS 256
+#endif
+#ifndef HE_IMIT_MIN_WAVES  // waves per SIMD the register budget must allow (launch bound)
+#define HE_IMIT_MIN_WAVES 1
+#endif
 template <bool EVAL>
-__global__ void __launch_bounds__(256) imitation_kernel(ImitArgs a) {
+__global__ void __launch_bounds__(HE_IMIT_THREADS, HE_IMIT_MIN_WAVES) imitation_kernel(ImitArgs a) {
     const int lane = threadIdx.x & (GROUP - 1);
     const int slot = (blockIdx.x * blockDim.x + threadIdx.x) / GROUP;
     if (slot >= a.count) return;  // whole 32-lane group leaves together
@@ -396,7 +402,7 @@ __global__ void __launch_bounds__(256) amp_function_kernel(AmpArgs a) {
 
 hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream) {
     if (a.count <= 0) return hipSuccess;
-    int threads = 256;
+    int threads = HE_IMIT_THREADS;
     int blocks = (a.count * GROUP + threads - 1) / threads;
     if (a.has_eval && a.mode != 2)
         imitation_kernel<true><<<blocks, threads, 0, stream>>>(a);

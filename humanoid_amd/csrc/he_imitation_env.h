@@ -9,6 +9,15 @@
 // Mapping: lane b = body b (24 of 32 lanes active); per-env reductions are xor-shuffles inside the
 // group; the root pose is broadcast from lane 0.
 
+// diagnostics only (tools/build_variant.py --tu he_imitation.hip -DHE_IMIT_DIAG=...): bit 0 drops
+// the observation math and stores, bit 1 reads the frame records at fixed indices (no dependent
+// round trip), bit 2 drops the reward / termination math, bit 3 the frame blends, bit 4 the angle
+// term, bit 5 the termination test, bit 6 the device reset of mode 1, bit 7 keeps the reset code but resets no env, to time the rest
+// of the step; the product build has 0
+#ifndef HE_IMIT_DIAG
+#define HE_IMIT_DIAG 0
+#endif
+
 HE_DEV float norm3_im(f3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
 
 HE_DEV float group_sum(float v) {
@@ -96,6 +105,13 @@ HE_DEV BodyRef body_ref_blend(const RefRows& x, f3 off) {
     const float* r1 = x.r1;
     float bl = x.blend, a = 1.0f - bl;
     BodyRef o;
+#if HE_IMIT_DIAG & 8  // no blend: the first frame's record
+    o.pos = f3{r0[0] + off.x, r0[1] + r1[1], r0[2]};
+    o.rot = f4{r0[3], r0[4], r0[5], r0[6] + bl};
+    o.vel = f3{r0[7], r0[8], r0[9]};
+    o.ang = f3{r0[10], r0[11], r0[12]};
+    return o;
+#endif
     o.pos = f3{a * r0[0] + bl * r1[0], a * r0[1] + bl * r1[1], a * r0[2] + bl * r1[2]};
     o.pos = o.pos + off;
     o.rot = slerp_ref(f4{r0[3], r0[4], r0[5], r0[6]}, f4{r1[3], r1[4], r1[5], r1[6]}, bl);
@@ -107,14 +123,28 @@ HE_DEV BodyRef body_ref(const MotionDev& m, const FrameSel& fs, int b, f3 off) {
     return body_ref_blend(body_ref_load(m, fs, b), off);
 }
 
-// local rotation slerp -> exp-map dof pos, dof vel lerp (motion_lib.py:562-606, 670-673)
-HE_DEV void body_dof_ref(const MotionDev& m, const FrameSel& fs, int b, f3& dpos, f3& dvel) {
+struct ColdRows {
+    float c0[COLD], c1[COLD];
+    float blend;
+};
+HE_DEV ColdRows body_cold_load(const MotionDev& m, const FrameSel& fs, int b) {
+    ColdRows x;
     const float* c0 = m.cold + (fs.g0 * NB + b) * COLD;
     const float* c1 = m.cold + (fs.g1 * NB + b) * COLD;
-    float bl = fs.blend, a = 1.0f - bl;
-    f4 lr = slerp_ref(f4{c0[0], c0[1], c0[2], c0[3]}, f4{c1[0], c1[1], c1[2], c1[3]}, bl);
+#pragma unroll
+    for (int c = 0; c < COLD; ++c) { x.c0[c] = c0[c]; x.c1[c] = c1[c]; }
+    x.blend = fs.blend;
+    return x;
+}
+// local rotation slerp -> exp-map dof pos, dof vel lerp (motion_lib.py:562-606, 670-673)
+HE_DEV void body_dof_blend(const ColdRows& x, f3& dpos, f3& dvel) {
+    const float bl = x.blend, a = 1.0f - bl;
+    const f4 lr = slerp_ref(f4{x.c0[0], x.c0[1], x.c0[2], x.c0[3]}, f4{x.c1[0], x.c1[1], x.c1[2], x.c1[3]}, bl);
     dpos = q_to_exp_map(lr);
-    dvel = f3{a * c0[4] + bl * c1[4], a * c0[5] + bl * c1[5], a * c0[6] + bl * c1[6]};
+    dvel = f3{a * x.c0[4] + bl * x.c1[4], a * x.c0[5] + bl * x.c1[5], a * x.c0[6] + bl * x.c1[6]};
+}
+HE_DEV void body_dof_ref(const MotionDev& m, const FrameSel& fs, int b, f3& dpos, f3& dvel) {
+    body_dof_blend(body_cold_load(m, fs, b), dpos, dvel);
 }
 
 HE_DEV float env_time(int progress, float cdt, float start, float off) {
@@ -172,15 +202,15 @@ HE_DEV void write_obs(float* o, int b, const SimBody& s, f3 root_pos, f4 hinv, f
 }
 
 // humanoid_phc.py:694-731 + 747-780 + 901-931 for body b of env e: set the env to the
-// reference state at time t (offset = the env's pre-reset global offset, :858-860)
-HE_DEV void reset_body(const ImitArgs& a, int e, int b, int64_t mid, float t, f3 off) {
-    FrameSel fs = frame_select(a.m, mid, t);
-    BodyRef r = body_ref(a.m, fs, b, off);
+// reference state `r` (the blend at the reset time, offset = the env's pre-reset global offset,
+// :858-860) and the dof state of the cold records `c` at the same frames. Every value written comes
+// from registers: nothing is read back, so a reset costs no store -> load round trip.
+HE_DEV void reset_body_write(const ImitArgs& a, int e, int b, const BodyRef& r, const ColdRows& x) {
     float* rb = a.rb_state + ((size_t)e * NB + b) * 13;
-    rb[0] = r.pos.x; rb[1] = r.pos.y; rb[2] = r.pos.z;
-    rb[3] = r.rot.x; rb[4] = r.rot.y; rb[5] = r.rot.z; rb[6] = r.rot.w;
-    rb[7] = r.vel.x; rb[8] = r.vel.y; rb[9] = r.vel.z;
-    rb[10] = r.ang.x; rb[11] = r.ang.y; rb[12] = r.ang.z;
+    const float row[13] = {r.pos.x, r.pos.y, r.pos.z, r.rot.x, r.rot.y, r.rot.z, r.rot.w,
+                           r.vel.x, r.vel.y, r.vel.z, r.ang.x, r.ang.y, r.ang.z};
+#pragma unroll
+    for (int c = 0; c < 13; ++c) rb[c] = row[c];
     if (a.contact_forces) {
         float* cf = a.contact_forces + ((size_t)e * NB + b) * 3;
         cf[0] = cf[1] = cf[2] = 0.0f;
@@ -188,10 +218,10 @@ HE_DEV void reset_body(const ImitArgs& a, int e, int b, int64_t mid, float t, f3
     if (b == 0) {
         float* rs = a.root_states + (size_t)e * 13;
 #pragma unroll
-        for (int c = 0; c < 13; ++c) rs[c] = rb[c];
+        for (int c = 0; c < 13; ++c) rs[c] = row[c];
     } else {
         f3 dp, dv;
-        body_dof_ref(a.m, fs, b, dp, dv);
+        body_dof_blend(x, dp, dv);
         int d = 3 * (b - 1);
         float* ds = a.dof_state + ((size_t)e * ND + d) * 2;
         ds[0] = dp.x; ds[1] = dv.x; ds[2] = dp.y; ds[3] = dv.y; ds[4] = dp.z; ds[5] = dv.z;
@@ -221,9 +251,12 @@ HE_DEV bool resolve_init(const he_imitation_params& p, float u, float& ph) {
 // row of HE_BUF_INIT_ROOT_STATE, zero dof positions / velocities / targets, and the rigid-body row of
 // that pose (every local rotation the identity: the root rotation, origin root + R rest_pos[b]; the
 // velocities of the initial root state, which the reference zeroes), zero contact force.
-HE_DEV void default_reset_body(const ImitArgs& a, int e, int b) {
+HE_DEV SimBody default_reset_body(const ImitArgs& a, int e, int b, bool act) {
 #pragma clang fp contract(off)
-    const float* ir = a.init_root + (size_t)e * 13;
+    const float* irp = a.init_root + (size_t)e * 13;
+    float ir[13];
+#pragma unroll
+    for (int c = 0; c < 13; ++c) ir[c] = irp[c];
     const f3 rp = f3{ir[0], ir[1], ir[2]};
     const f4 rq = f4{ir[3], ir[4], ir[5], ir[6]};
     const f3 v = f3{ir[7], ir[8], ir[9]}, w = f3{ir[10], ir[11], ir[12]};
@@ -231,28 +264,31 @@ HE_DEV void default_reset_body(const ImitArgs& a, int e, int b) {
     const f3 ro = qrot_ref(rq, lo);
     const f3 pos = rp + ro;
     const f3 vel = v + f3{w.y * ro.z - w.z * ro.y, w.z * ro.x - w.x * ro.z, w.x * ro.y - w.y * ro.x};
-    float* rb = a.rb_state + ((size_t)e * NB + b) * 13;
-    rb[0] = pos.x; rb[1] = pos.y; rb[2] = pos.z;
-    rb[3] = rq.x; rb[4] = rq.y; rb[5] = rq.z; rb[6] = rq.w;
-    rb[7] = vel.x; rb[8] = vel.y; rb[9] = vel.z;
-    rb[10] = w.x; rb[11] = w.y; rb[12] = w.z;
-    if (a.contact_forces) {
-        float* cf = a.contact_forces + ((size_t)e * NB + b) * 3;
-        cf[0] = cf[1] = cf[2] = 0.0f;
-    }
-    if (b == 0) {
-        float* rs = a.root_states + (size_t)e * 13;
+    if (act) {
+        float* rb = a.rb_state + ((size_t)e * NB + b) * 13;
+        rb[0] = pos.x; rb[1] = pos.y; rb[2] = pos.z;
+        rb[3] = rq.x; rb[4] = rq.y; rb[5] = rq.z; rb[6] = rq.w;
+        rb[7] = vel.x; rb[8] = vel.y; rb[9] = vel.z;
+        rb[10] = w.x; rb[11] = w.y; rb[12] = w.z;
+        if (a.contact_forces) {
+            float* cf = a.contact_forces + ((size_t)e * NB + b) * 3;
+            cf[0] = cf[1] = cf[2] = 0.0f;
+        }
+        if (b == 0) {
+            float* rs = a.root_states + (size_t)e * 13;
 #pragma unroll
-        for (int c = 0; c < 13; ++c) rs[c] = ir[c];
-    } else {
-        const int d = 3 * (b - 1);
-        float* ds = a.dof_state + ((size_t)e * ND + d) * 2;
-        ds[0] = ds[1] = ds[2] = ds[3] = ds[4] = ds[5] = 0.0f;
-        if (a.dof_targets) {
-            float* tg = a.dof_targets + (size_t)e * ND + d;
-            tg[0] = tg[1] = tg[2] = 0.0f;
+            for (int c = 0; c < 13; ++c) rs[c] = ir[c];
+        } else {
+            const int d = 3 * (b - 1);
+            float* ds = a.dof_state + ((size_t)e * ND + d) * 2;
+            ds[0] = ds[1] = ds[2] = ds[3] = ds[4] = ds[5] = 0.0f;
+            if (a.dof_targets) {
+                float* tg = a.dof_targets + (size_t)e * ND + d;
+                tg[0] = tg[1] = tg[2] = 0.0f;
+            }
         }
     }
+    return SimBody{pos, vel, w, rq};
 }
 
 // eval recording (he_imitation.hip; only the stand-alone kernel instantiates EVAL = true)
@@ -301,8 +337,13 @@ HE_DEV ImitRaw imitation_frames_load(const ImitArgs& a, int lane, const ImitBook
     if (a.mode != 2) prog += 1;  // post-physics half of HumanoidPHC.step (humanoid_phc.py:138-149)
     x.prog = prog;
     x.t = env_time(prog, p.control_dt, k.start, k.soff);
+#if HE_IMIT_DIAG & 2  // frames at fixed indices: no dependent round trip
+    x.s1 = body_ref_load(a.m, FrameSel{0, 1, x.t * 1e-9f}, b);
+    x.s2 = body_ref_load(a.m, FrameSel{1, 2, x.t * 1e-9f}, b);
+#else
     x.s1 = body_ref_load(a.m, frame_select(k.mm, x.t), b);
     x.s2 = body_ref_load(a.m, frame_select(k.mm, env_time(prog + 1, p.control_dt, k.start, k.soff)), b);
+#endif
     return x;
 }
 HE_DEV ImitRef imitation_frames_blend(const ImitRaw& w) {
@@ -339,7 +380,14 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
     bool do_reset = false, ref_init = true;
     float reset_time = 0.0f;
 
+#if HE_IMIT_DIAG & 4  // no reward / termination math
     if (a.mode != 2) {
+        if (leader) { a.rew[e] = r.pos.x + s.pos.x + pw + t; a.progress[e] = (int16_t)prog; }
+    } else
+#else
+    if (a.mode != 2) {
+#endif
+#if !(HE_IMIT_DIAG & 4)
         // reward terms, common.py:298-317
         f3 d = r.pos - s.pos;
         float dp = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
@@ -347,7 +395,11 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
         float dv = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
         d = r.ang - s.ang;
         float da = act ? (d.x * d.x + d.y * d.y + d.z * d.z) / 3.0f : 0.0f;
+#if HE_IMIT_DIAG & 16
+        float ang = qmul_ref(r.rot, qconj(s.rot)).w;
+#else
         float ang = q_angle_axis(qmul_ref(r.rot, qconj(s.rot)), nullptr);
+#endif
         float dr = act ? ang * ang : 0.0f;
         dp = group_sum(dp) / NB;
         dv = group_sum(dv) / NB;
@@ -365,7 +417,7 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
         // termination, common.py:325-364 + humanoid_phc.py:1313-1335
         bool pass_time = t >= mm.len;
         bool fallen = false;
-        if (p.enable_early_termination) {
+        if (p.enable_early_termination && !(HE_IMIT_DIAG & 32)) {
             bool inset = act && ((p.reset_body_mask >> b) & 1);
             float dist = norm3_im(s.pos - r.pos);  // no contraction in either TU (torch rounding)
             if (p.eval_mode) {
@@ -379,6 +431,9 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
             fallen = fallen && prog > 1;
         }
         bool reset = pass_time || fallen;
+#if HE_IMIT_DIAG & 128  // no env resets at run time (the code stays)
+        reset = reset && a.seed == 0x123456789abcdefull;
+#endif
         if constexpr (EVAL) eval_record(a.ev, e, lane, act, s.pos, r.pos);  // before any fused reset
         if (leader) {
             a.rew[e] = rew;
@@ -388,7 +443,7 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
             a.terminate[e] = fallen;
             a.progress[e] = (int16_t)prog;
         }
-        if (a.mode == 1 && reset) {
+        if (a.mode == 1 && reset && !(HE_IMIT_DIAG & 64)) {
             do_reset = true;
             // the reset's draw: a hashed uniform, resolved by the state init (humanoid_phc.py:679-692,
             // 733-745, 848-856)
@@ -397,23 +452,36 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
             reset_time = ref_init ? sample_time_interval(ph, mm.len) : 0.0f;
         }
     } else {
-        do_reset = true;
+#else
+    {
+#endif
+        do_reset = !(HE_IMIT_DIAG & 64);
         float ph;
         ref_init = resolve_init(a.p, a.phases[slot], ph);
         reset_time = ref_init ? sample_time_interval(ph, mm.len) : 0.0f;
     }
 
     if (do_reset && !ref_init) {  // _reset_default: the motion bookkeeping stays (the group is uniform)
-        if (act) default_reset_body(a, e, b);
+        // the next observation's frames are loaded alongside the initial pose (one round trip)
+        const RefRows n2 = body_ref_load(a.m, frame_select(mm, env_time(1, p.control_dt, start, soff)), b);
+        s = default_reset_body(a, e, b, act);  // the row this lane wrote
+        r2 = body_ref_blend(n2, off);
         prog = 0;
         if (leader) {
             a.progress[e] = 0;
             if (a.mode == 2) { a.reset[e] = 0; a.terminate[e] = 0; }
         }
-        s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);  // the row this lane just wrote
-        r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
     } else if (do_reset) {  // the group's branch is uniform
-        if (act) reset_body(a, e, b, mid, reset_time, off);
+        // the reset frames (hot and cold records) and the next observation's frames, loaded
+        // together: one round trip (the metadata is the step's)
+        const FrameSel fs = frame_select(mm, reset_time);
+        const RefRows h0 = body_ref_load(a.m, fs, b);
+        const ColdRows c0 = body_cold_load(a.m, fs, b);
+        const RefRows n2 = body_ref_load(a.m, frame_select(mm, env_time(1, p.control_dt, reset_time, 0.0f)), b);
+        const BodyRef r0 = body_ref_blend(h0, off);
+        if (act) reset_body_write(a, e, b, r0, c0);
+        s = SimBody{r0.pos, r0.vel, r0.ang, r0.rot};  // the row this lane wrote (lane b = 0's on idle lanes)
+        r2 = body_ref_blend(n2, f3{0.f, 0.f, 0.f});
         off = f3{0.f, 0.f, 0.f};
         start = reset_time;
         soff = 0.0f;
@@ -425,8 +493,6 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
             a.progress[e] = 0;
             if (a.mode == 2) { a.reset[e] = 0; a.terminate[e] = 0; }
         }
-        s = load_body(a.rb_state + ((size_t)e * NB + b) * 13);  // the row this lane just wrote
-        r2 = body_ref(a.m, frame_select(mm, env_time(prog + 1, p.control_dt, start, soff)), b, off);
     }
 
     // ---------------- observations for the next step (humanoid_phc.py:937-961, 1063-1067)
@@ -436,7 +502,11 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
     // quat_from_angle_axis(+-h, z): sinf is odd and cosf even (both evaluate |x| and restore the
     // sign), so the heading rotation is the inverse's z negated, bit for bit
     const f4 hinv = heading_quat(-h), hq = f4{0.f, 0.f, -hinv.z, hinv.w};
+#if !(HE_IMIT_DIAG & 1)
     if (act) write_obs(a.obs + (size_t)e * HE_OBS_DIM, b, s, root_pos, hinv, hq, r2);
+#else
+    if (act && b == 0) a.obs[(size_t)e * HE_OBS_DIM] = hinv.z + root_pos.z + r2.pos.x + s.vel.x;
+#endif
 }
 
 template <bool EVAL>

@@ -99,6 +99,9 @@ struct Lds {
 #ifndef HE_DELASSUS48
 #define HE_DELASSUS48 1
 #endif
+#ifndef HE_PGS_PACKED_BOUNDS  // a PGS row's two bound updates as one packed FMA (1) or two FMAs (0)
+#define HE_PGS_PACKED_BOUNDS 1
+#endif
 #ifndef HE_PGS_OPAQUE_MASK  // PGS bound weights formed per row (1) or hoisted by the compiler (0)
 #define HE_PGS_OPAQUE_MASK 0
 #endif
@@ -574,6 +577,20 @@ HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uin
 // a normal row of lane r's patch (bit R of the lane's patch mask), lane r's bounds widen by muw_r d
 // right away -- the patch's normal rows come before its friction rows, so a friction row sees this
 // sweep's normal impulses (Gauss-Seidel, as the oracle's bound from the current impulses).
+// Packed form (HE_PGS_PACKED_BOUNDS): lane r holds the pair (acolp[R], kk_R) per row -- kk_R = muw_r
+// where R is a normal row of its patch, else 0 -- and its (cd, hi) pair, so that a row's change goes
+// to cd and hi in one v_pk_fma_f32 (lo: one FMA with the pair's weight negated). Five VALU per row.
+template <int R>
+HE_DEV void pgs_sweep_pk(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
+    if constexpr (R < MAXR) {
+        if (R >= nr) return;
+        const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
+        ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
+        lo = fmaf(-ak[R].y, d, lo);
+        dvec = regla::wrlane<R>(d, dvec);
+        pgs_sweep_pk<R + 1>(ch, dvec, lo, ak, nr);
+    }
+}
 template <int R>
 HE_DEV void pgs_sweep(float& cd, float& dvec, float& lo, float& hi, const float (&acolp)[MAXR], uint32_t mlo,
                       uint32_t mhi, float muw, int nr) {
@@ -2136,6 +2153,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 }
                 bnd *= muw;
             }
+#if HE_PGS_PACKED_BOUNDS
+            regla::f2v ak[MAXR];
+#pragma unroll
+            for (int r = 0; r < MAXR; ++r) {
+                const int sel = __builtin_amdgcn_sbfe((int)(r < 32 ? mlo : mhi), r & 31, 1);
+                ak[r] = regla::f2v{acol[r], __int_as_float(sel & __float_as_int(muw))};
+            }
+#endif
             const float kInf = __builtin_inff();
             float lo = isn ? -lamv : -bnd - lamv;
             float hi = isn ? kInf : bnd - lamv;
@@ -2149,7 +2174,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 // lane-mask pairs (SGPR spills)
                 int nrs = nru;
                 asm volatile("" : "+s"(nrs));
-#if HE_PGS_OPAQUE_MASK
+#if HE_PGS_PACKED_BOUNDS
+                regla::f2v ch = {cd, hi};
+                pgs_sweep_pk<0>(ch, dvec, lo, ak, nrs);
+                cd = ch.x;
+                hi = ch.y;
+#elif HE_PGS_OPAQUE_MASK
                 // the patch masks and weights through opaque copies per sweep: the per-row bound
                 // weights are formed in the sweep (2 VALU per row) instead of being hoisted out of
                 // the loop as 63 VGPRs

@@ -40,6 +40,19 @@ def test_library_exports_every_declared_symbol():
         assert lib.he_hash_uniform(s, st, e) == O.hash_uniform(s, st, e)
 
 
+def test_build_tracks_every_kernel_header():
+    """build.build() rebuilds when a header changes only if the header is in build.HEADERS: every
+    header a kernel source includes must be listed (an unlisted one once left a stale library)."""
+    import glob
+    from humanoid_amd import build
+    csrc = os.path.join(ROOT, "humanoid_amd", "csrc")
+    tracked = {os.path.normpath(os.path.join(csrc, h)) for h in build.HEADERS}
+    for src in glob.glob(os.path.join(csrc, "*")):
+        for inc in re.findall(r'#include\s+"([^"]+)"', open(src).read()):
+            path = os.path.normpath(os.path.join(csrc, inc))
+            assert path in tracked, f"{os.path.basename(src)} includes {inc}, not in build.HEADERS"
+
+
 def test_errors_are_reported_without_gpu():
     from humanoid_amd import _abi, engine
     lib = engine.load_library()
