@@ -102,6 +102,11 @@ struct Lds {
 #ifndef HE_PGS_PACKED_BOUNDS  // a PGS row's two bound updates as one packed FMA (1) or two FMAs (0)
 #define HE_PGS_PACKED_BOUNDS 1
 #endif
+#ifndef HE_PGS_FORM  // packed PGS sweep form: 3 = branch-free up to the row-count class (32/48/63;
+// +0.65 % physics A/B, bit-identical), 0 = a row-count branch per row, 1 = rows in pairs, 2 = rows in
+// DPP quads (1 and 2: bit-identical, -0.3 % and -0.9 %; profiles/r03/ab_pgs_form.txt)
+#define HE_PGS_FORM 3
+#endif
 #ifndef HE_PGS_OPAQUE_MASK  // PGS bound weights formed per row (1) or hoisted by the compiler (0)
 #define HE_PGS_OPAQUE_MASK 0
 #endif
@@ -589,6 +594,102 @@ HE_DEV void pgs_sweep_pk(regla::f2v& ch, float& dvec, float& lo, const regla::f2
         lo = fmaf(-ak[R].y, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
         pgs_sweep_pk<R + 1>(ch, dvec, lo, ak, nr);
+    }
+}
+// Branch-free form (HE_PGS_FORM 3): every row up to a compile-time class bound N (32, 48, 63) by
+// the row count, with no per-row row-count branch; rows nr..N-1 are empty rows (zero columns and
+// bound weights in every lane, zero cd and bounds in their own lanes: a +-0 change).
+template <int R, int N>
+HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR]) {
+    if constexpr (R < N) {
+        const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
+        ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
+        lo = fmaf(-ak[R].y, d, lo);
+        dvec = regla::wrlane<R>(d, dvec);
+        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak);
+    }
+}
+// Paired form (HE_PGS_FORM): rows R, R+1 (R even) per step. Lane R+1 takes row R's change from
+// its neighbour by DPP (row_shr:1 -- R+1 is odd, so never the first lane of a DPP row) and applies
+// it to its own (cd, hi) and lo exactly as the full-wave update would (the same FMAs on the same
+// operands), so its clamp is row R+1's Gauss-Seidel change bit for bit; the two v_readlane
+// broadcasts then update every lane in row order. One readlane -> FMA link per two rows leaves the
+// dependent chain: med3 -> dpp -> pk_fma -> med3 -> readlane -> pk_fma.
+template <int R>
+HE_DEV void pgs_sweep_pk2(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
+    if constexpr (R < MAXR) {
+        if (R >= nr) return;
+        if constexpr (R + 1 < MAXR) {
+            // row R + 1 == nr is an empty row (its column and bound weights are 0 in every lane, its
+            // own cd and bounds 0): its change is +-0 and leaves every lane's values as they were
+            const float x1 = __builtin_amdgcn_fmed3f(ch.x, lo, ch.y);
+            const float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x1), 0x111, 0xf, 0xf, true));
+            const regla::f2v c2 = __builtin_elementwise_fma(ak[R], regla::f2v{t, t}, ch);
+            const float lo2 = fmaf(-ak[R].y, t, lo);
+            const float d0 = regla::rdlane(x1, R);
+            const float d1 = regla::rdlane(__builtin_amdgcn_fmed3f(c2.x, lo2, c2.y), R + 1);
+            ch = __builtin_elementwise_fma(ak[R], regla::f2v{d0, d0}, ch);
+            lo = fmaf(-ak[R].y, d0, lo);
+            ch = __builtin_elementwise_fma(ak[R + 1], regla::f2v{d1, d1}, ch);
+            lo = fmaf(-ak[R + 1].y, d1, lo);
+            dvec = regla::wrlane<R>(d0, dvec);
+            dvec = regla::wrlane<R + 1>(d1, dvec);
+            asm volatile("" : "+v"(lo));  // the bound chain in this block, not sunk past the row-count branch
+            pgs_sweep_pk2<R + 2>(ch, dvec, lo, ak, nr);
+        } else {
+            const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
+            ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
+            lo = fmaf(-ak[R].y, d, lo);
+            dvec = regla::wrlane<R>(d, dvec);
+        }
+    }
+}
+// Quad form (HE_PGS_FORM 2): rows R..R+3 (R % 4 == 0) per step, Gauss-Seidel inside the DPP quad
+// of lanes R..R+3 (each change broadcast to the quad by quad_perm, applied to a local copy with the
+// full-wave FMAs' operands), then four readlane broadcasts update every lane in row order. Lanes
+// outside the quad compute garbage local copies that are discarded.
+template <int K>
+HE_DEV float quad_bcast(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), K * 0x55, 0xf, 0xf, false));
+}
+template <int R>
+HE_DEV void pgs_sweep_pk4(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
+    if constexpr (R < MAXR) {
+        if (R >= nr) return;
+        if constexpr (R + 3 < MAXR) {
+            // rows R + k >= nr are empty rows (zero columns and bound weights, zero cd and bounds)
+            const float x0 = __builtin_amdgcn_fmed3f(ch.x, lo, ch.y);
+            const float t0 = quad_bcast<0>(x0);
+            const regla::f2v c1 = __builtin_elementwise_fma(ak[R], regla::f2v{t0, t0}, ch);
+            const float l1 = fmaf(-ak[R].y, t0, lo);
+            const float x1 = __builtin_amdgcn_fmed3f(c1.x, l1, c1.y);
+            const float t1 = quad_bcast<1>(x1);
+            const regla::f2v c2 = __builtin_elementwise_fma(ak[R + 1], regla::f2v{t1, t1}, c1);
+            const float l2 = fmaf(-ak[R + 1].y, t1, l1);
+            const float x2 = __builtin_amdgcn_fmed3f(c2.x, l2, c2.y);
+            const float t2 = quad_bcast<2>(x2);
+            const regla::f2v c3 = __builtin_elementwise_fma(ak[R + 2], regla::f2v{t2, t2}, c2);
+            const float l3 = fmaf(-ak[R + 2].y, t2, l2);
+            const float x3 = __builtin_amdgcn_fmed3f(c3.x, l3, c3.y);
+            const float d0 = regla::rdlane(x0, R), d1 = regla::rdlane(x1, R + 1);
+            const float d2 = regla::rdlane(x2, R + 2), d3 = regla::rdlane(x3, R + 3);
+            ch = __builtin_elementwise_fma(ak[R], regla::f2v{d0, d0}, ch);
+            lo = fmaf(-ak[R].y, d0, lo);
+            ch = __builtin_elementwise_fma(ak[R + 1], regla::f2v{d1, d1}, ch);
+            lo = fmaf(-ak[R + 1].y, d1, lo);
+            ch = __builtin_elementwise_fma(ak[R + 2], regla::f2v{d2, d2}, ch);
+            lo = fmaf(-ak[R + 2].y, d2, lo);
+            ch = __builtin_elementwise_fma(ak[R + 3], regla::f2v{d3, d3}, ch);
+            lo = fmaf(-ak[R + 3].y, d3, lo);
+            dvec = regla::wrlane<R>(d0, dvec);
+            dvec = regla::wrlane<R + 1>(d1, dvec);
+            dvec = regla::wrlane<R + 2>(d2, dvec);
+            dvec = regla::wrlane<R + 3>(d3, dvec);
+            asm volatile("" : "+v"(lo));  // the bound chain in this block, not sunk past the row-count branch
+            pgs_sweep_pk4<R + 4>(ch, dvec, lo, ak, nr);
+        } else {
+            pgs_sweep_pk2<R>(ch, dvec, lo, ak, nr);
+        }
     }
 }
 template <int R>
@@ -2176,7 +2277,17 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 asm volatile("" : "+s"(nrs));
 #if HE_PGS_PACKED_BOUNDS
                 regla::f2v ch = {cd, hi};
+#if HE_PGS_FORM == 3
+                if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak);
+                else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak);
+                else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak);
+#elif HE_PGS_FORM == 2
+                pgs_sweep_pk4<0>(ch, dvec, lo, ak, nrs);
+#elif HE_PGS_FORM
+                pgs_sweep_pk2<0>(ch, dvec, lo, ak, nrs);
+#else
                 pgs_sweep_pk<0>(ch, dvec, lo, ak, nrs);
+#endif
                 cd = ch.x;
                 hi = ch.y;
 #elif HE_PGS_OPAQUE_MASK
