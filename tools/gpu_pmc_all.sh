@@ -8,5 +8,5 @@ CONFIG=imitation bash tools/gpu_mfma.sh ${TAG}_imit > gpurun_out/pmc_all_mfma_im
 bash tools/gpu_pmc.sh $TAG > gpurun_out/pmc_all_traffic_$TAG.out 2>&1 &&
 CONFIG=imitation bash tools/gpu_pmc.sh ${TAG}_imit > gpurun_out/pmc_all_traffic_imit_$TAG.out 2>&1
 rc=$?
-tail -2 gpurun_out/pmc_all_*_$TAG.out
+tail -n 2 gpurun_out/pmc_all_*_$TAG.out
 exit $rc
