@@ -107,6 +107,9 @@ struct Lds {
 // DPP quads (1 and 2: bit-identical, -0.3 % and -0.9 %; profiles/r03/ab_pgs_form.txt)
 #define HE_PGS_FORM 3
 #endif
+#ifndef HE_PGS_MIN_CLASS  // smallest row-count class of the branch-free sweep (8, 16 or 32)
+#define HE_PGS_MIN_CLASS 16  // +1.3 % configs[2], +1.5 % configs[4] physics A/B (8: less); ab_pgs_form.txt
+#endif
 #ifndef HE_PGS_OPAQUE_MASK  // PGS bound weights formed per row (1) or hoisted by the compiler (0)
 #define HE_PGS_OPAQUE_MASK 0
 #endif
@@ -2278,6 +2281,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #if HE_PGS_PACKED_BOUNDS
                 regla::f2v ch = {cd, hi};
 #if HE_PGS_FORM == 3
+#if HE_PGS_MIN_CLASS <= 8
+                if (nrs <= 8) pgs_sweep_fix<0, 8>(ch, dvec, lo, ak);
+                else
+#endif
+#if HE_PGS_MIN_CLASS <= 16
+                if (nrs <= 16) pgs_sweep_fix<0, 16>(ch, dvec, lo, ak);
+                else
+#endif
                 if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak);
                 else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak);
                 else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak);
