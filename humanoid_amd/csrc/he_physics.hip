@@ -107,6 +107,9 @@ struct Lds {
 // DPP quads (1 and 2: bit-identical, -0.3 % and -0.9 %; profiles/r03/ab_pgs_form.txt)
 #define HE_PGS_FORM 3
 #endif
+#ifndef HE_PGS_CLASS_PREP  // scale the columns and form the packed bound weights for the row class only
+#define HE_PGS_CLASS_PREP 1  // -0.2..-0.4 % physics launch A/B on all three configs, bit-identical
+#endif
 #ifndef HE_PGS_MIN_CLASS  // smallest row-count class of the branch-free sweep (8, 16 or 32)
 #define HE_PGS_MIN_CLASS 16  // +1.3 % configs[2], +1.5 % configs[4] physics A/B (8: less); ab_pgs_form.txt
 #endif
@@ -2224,15 +2227,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     for (int r = 0; r < NRW; ++r) wa[r & 3] = fmaf(acol[r], regla::rdlane(lam0, r), wa[r & 3]);
                     w0 += (wa[0] + wa[1]) + (wa[2] + wa[3]);
                 };
-                if (nr <= 32) aw(std::integral_constant<int, 32>{});
+                if (HE_PGS_CLASS_PREP && nr <= 16) aw(std::integral_constant<int, 16>{});
+                else if (nr <= 32) aw(std::integral_constant<int, 32>{});
                 else if (nr <= 48) aw(std::integral_constant<int, 48>{});
                 else aw(std::integral_constant<int, MAXR>{});
             }
             lamv = lam0;
             float cd = act ? -w0 * invd : 0.f;
             const float ninvd = -invd;
+#if !(HE_PGS_PACKED_BOUNDS && HE_PGS_FORM == 3 && HE_PGS_CLASS_PREP)
 #pragma unroll
             for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
+#endif
             // the row's friction bound weight and its patch's normal rows n0 .. n0 + pc - 1 as a
             // 64-bit lane mask (friction rows only)
             const bool isn = kind == 0;
@@ -2259,11 +2265,32 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             }
 #if HE_PGS_PACKED_BOUNDS
             regla::f2v ak[MAXR];
+#if HE_PGS_FORM == 3 && HE_PGS_CLASS_PREP
+            // the scaled columns acolp[r] = -A[r][lane] / A[lane][lane] and the packed bound weights of
+            // the row-count class's rows only (the branch-free sweep reads no row past its class):
+            // blocks of 16 rows, each behind a wave-uniform row-count test
+            {
+                const int nrb = __builtin_amdgcn_readfirstlane(nr);
+                auto prep = [&](auto r0c) {
+                    constexpr int R0 = decltype(r0c)::value;
+#pragma unroll
+                    for (int r = R0; r < (R0 + 16 < MAXR ? R0 + 16 : MAXR); ++r) {
+                        const int sel = __builtin_amdgcn_sbfe((int)(r < 32 ? mlo : mhi), r & 31, 1);
+                        ak[r] = regla::f2v{acol[r] * ninvd, __int_as_float(sel & __float_as_int(muw))};
+                    }
+                };
+                prep(std::integral_constant<int, 0>{});
+                if (nrb > 16) prep(std::integral_constant<int, 16>{});
+                if (nrb > 32) prep(std::integral_constant<int, 32>{});
+                if (nrb > 48) prep(std::integral_constant<int, 48>{});
+            }
+#else
 #pragma unroll
             for (int r = 0; r < MAXR; ++r) {
                 const int sel = __builtin_amdgcn_sbfe((int)(r < 32 ? mlo : mhi), r & 31, 1);
                 ak[r] = regla::f2v{acol[r], __int_as_float(sel & __float_as_int(muw))};
             }
+#endif
 #endif
             const float kInf = __builtin_inff();
             float lo = isn ? -lamv : -bnd - lamv;
