@@ -107,6 +107,9 @@ struct Lds {
 // DPP quads (1 and 2: bit-identical, -0.3 % and -0.9 %; profiles/r03/ab_pgs_form.txt)
 #define HE_PGS_FORM 3
 #endif
+#ifndef HE_PGS_STRIDE  // branch-free sweep: a row-count exit every HE_PGS_STRIDE rows (0: none)
+#define HE_PGS_STRIDE 4  // -0.7 % standstill, -1.4 % configs[2] physics launch A/B (8: neutral), bit-identical
+#endif
 #ifndef HE_PGS_CLASS_PREP  // scale the columns and form the packed bound weights for the row class only
 #define HE_PGS_CLASS_PREP 1  // -0.2..-0.4 % physics launch A/B on all three configs, bit-identical
 #endif
@@ -606,13 +609,18 @@ HE_DEV void pgs_sweep_pk(regla::f2v& ch, float& dvec, float& lo, const regla::f2
 // the row count, with no per-row row-count branch; rows nr..N-1 are empty rows (zero columns and
 // bound weights in every lane, zero cd and bounds in their own lanes: a +-0 change).
 template <int R, int N>
-HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR]) {
+HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
     if constexpr (R < N) {
+#if HE_PGS_STRIDE
+        if constexpr (R > 0 && R % HE_PGS_STRIDE == 0) {  // a row-count exit every HE_PGS_STRIDE rows
+            if (R >= nr) return;
+        }
+#endif
         const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
         ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
         lo = fmaf(-ak[R].y, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
-        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak);
+        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr);
     }
 }
 // Paired form (HE_PGS_FORM): rows R, R+1 (R even) per step. Lane R+1 takes row R's change from
@@ -2309,16 +2317,16 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 regla::f2v ch = {cd, hi};
 #if HE_PGS_FORM == 3
 #if HE_PGS_MIN_CLASS <= 8
-                if (nrs <= 8) pgs_sweep_fix<0, 8>(ch, dvec, lo, ak);
+                if (nrs <= 8) pgs_sweep_fix<0, 8>(ch, dvec, lo, ak, nrs);
                 else
 #endif
 #if HE_PGS_MIN_CLASS <= 16
-                if (nrs <= 16) pgs_sweep_fix<0, 16>(ch, dvec, lo, ak);
+                if (nrs <= 16) pgs_sweep_fix<0, 16>(ch, dvec, lo, ak, nrs);
                 else
 #endif
-                if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak);
-                else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak);
-                else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak);
+                if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak, nrs);
+                else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak, nrs);
+                else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak, nrs);
 #elif HE_PGS_FORM == 2
                 pgs_sweep_pk4<0>(ch, dvec, lo, ak, nrs);
 #elif HE_PGS_FORM
