@@ -107,6 +107,9 @@ struct Lds {
 // DPP quads (1 and 2: bit-identical, -0.3 % and -0.9 %; profiles/r03/ab_pgs_form.txt)
 #define HE_PGS_FORM 3
 #endif
+#ifndef HE_WCLAMP_BOUND  // skip the world angular-velocity prefix when a norm bound rules the clamp out
+#define HE_WCLAMP_BOUND 1  // -1.1 % standstill physics launch A/B, configs[2] neutral; bit-identical
+#endif
 #ifndef HE_PGS_STRIDE  // branch-free sweep: a row-count exit every HE_PGS_STRIDE rows (0: none)
 #define HE_PGS_STRIDE 4  // -0.7 % standstill, -1.4 % configs[2] physics launch A/B (8: neutral), bit-identical
 #endif
@@ -2472,6 +2475,15 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // the link's WORLD angular velocity (asset max_angular_velocity, PxRigidBody): w_b = w_parent +
         // R_b u_b summed along the chain (Acc is scratch here), clamped link by link; the joint rates
         // are then re-derived, u_b = R_b^T (w'_b - w'_parent) (oracle: the same pass)
+#if HE_WCLAMP_BOUND
+        // no link can be over when |w_root| + (joints on the longest chain) x max_j |u_j| stays under
+        // the cap (triangle inequality; a 1 % margin covers the prefix's rounding): the prefix and
+        // the clamp are then skipped (wave-uniform), with the result they would give
+        const float un = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        const float wroot = regla::rdlane(un, 0);
+        const bool may = bl && !root && un * (float)(smpl::kNumBodyLevels - 1) > 0.99f * p.max_angular_velocity - wroot;
+        if (__ballot(may) != 0ull) {
+#endif
         const f4 qb = bl ? f4{L.qw[lane][0], L.qw[lane][1], L.qw[lane][2], L.qw[lane][3]} : f4{0.f, 0.f, 0.f, 1.f};
         const f3 wr = root ? f3{w[0], w[1], w[2]} : qapply(qb, f3{w[0], w[1], w[2]});
         // chain prefix by pointer jumping (the table stops below the root: its rate is added last)
@@ -2505,6 +2517,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 w[0] = ub.x; w[1] = ub.y; w[2] = ub.z;
             }
         }
+#if HE_WCLAMP_BOUND
+        }
+#endif
     }
     if (bl) {
         L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
