@@ -20,6 +20,46 @@
 
 HE_DEV float norm3_im(f3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
 
+// The 32-lane group reductions and the group broadcast on the VALU (HE_IMIT_DPP): DPP steps inside a
+// 16-lane row (quad perms, half-row and row mirrors) and one v_permlane16_swap across the group's two
+// rows, instead of five LDS-crossbar ds_bpermute round trips; the broadcast by two v_readlane.
+// Every lane of a group must be active (the kernels' groups enter and leave whole).
+#ifndef HE_IMIT_DPP
+#define HE_IMIT_DPP 1
+#endif
+#if HE_IMIT_DPP
+template <int CTRL>
+HE_DEV float im_dpp(float x) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false)); }
+// {v of the group's even row, v of its odd row} on every lane: v_permlane16_swap of v with itself
+HE_DEV void im_rows(float v, float& r0, float& r1) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    r0 = __uint_as_float(r[0]);
+    r1 = __uint_as_float(r[1]);
+}
+HE_DEV float group_sum(float v) {
+    v += im_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += im_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += im_dpp<0x141>(v);  // row_half_mirror: the other quad of the 8
+    v += im_dpp<0x140>(v);  // row_mirror: the other 8 of the row
+    float r0, r1;
+    im_rows(v, r0, r1);     // one of the two is v itself, the other the other row's sum
+    return r0 + r1;
+}
+HE_DEV float group_max(float v) {
+    v = fmaxf(v, im_dpp<0xB1>(v));
+    v = fmaxf(v, im_dpp<0x4E>(v));
+    v = fmaxf(v, im_dpp<0x141>(v));
+    v = fmaxf(v, im_dpp<0x140>(v));
+    float r0, r1;
+    im_rows(v, r0, r1);
+    return fmaxf(r0, r1);
+}
+HE_DEV float bcast0(float v) {
+    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    return (threadIdx.x & 32) ? b : a;
+}
+#else
 HE_DEV float group_sum(float v) {
 #pragma unroll
     for (int o = GROUP / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, GROUP);
@@ -31,6 +71,7 @@ HE_DEV float group_max(float v) {
     return v;
 }
 HE_DEV float bcast0(float v) { return __shfl(v, 0, GROUP); }
+#endif
 
 struct FrameSel {
     int64_t g0, g1;
