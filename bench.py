@@ -60,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--fused", action="store_true",
                     help="he_env_step as one launch (the imitation step in the physics kernel's epilogue); "
                          "at 4096 envs the two launches are faster (DESIGN §4.1)")
+    ap.add_argument("--no-learner", action="store_true",
+                    help="skip the configs[3] per-rank learner leg (rollout into the device Experience, GAE, PPO "
+                         "update of the reference-size policy, RCCL gradient all-reduce)")
     ap.add_argument("--no-tracking", action="store_true",
                     help="skip the configs[2] tracking-action leg (throughput + joint-pose L2 vs ref)")
     return ap.parse_args(argv)
@@ -249,6 +252,95 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
                                   "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x steps"}}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def learner_leg(args, model, device_index):
+    """configs[3] per rank: this rank's 4096 envs x 32 steps into the
+    device Experience with the reference-size policy in the loop (16.98 M params), GAE, then the PPO
+    update (4 epochs x 4 minibatches of 32768, core.py:264-380) with the gradient all-reduce on device
+    tensors between backward and the clip (core.py:366-373). Runs on every rank; at N = 1 the
+    collective runs on a one-rank RCCL group, so the backend the 8-GPU node uses has executed."""
+    import torch
+    import torch.distributed as dist
+    from humanoid_amd import dist as hd, learner as L
+    from humanoid_amd.env import EnvConfig, PHCPufferEnv
+    own_group = False
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(_free_port())
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", device_index))
+        own_group = True
+    backend = dist.get_backend()
+    rank = dist.get_rank()
+    cfg = L.TrainConfig()
+    n = args.num_envs
+    a = argparse.Namespace(**vars(args))
+    a.config = "imitation"
+    clips = make_clips(a, model)
+    pe = PHCPufferEnv(EnvConfig(num_envs=n, motion_file={f"clip{i}": c for i, c in enumerate(clips)},
+                                seed=hd.rank_seed(1, rank)))
+    dev = torch.device("cuda", device_index)
+    torch.manual_seed(0)  # identical initial policy on every rank
+    policy = L.make_policy(dev)
+    opt = torch.optim.Adam(policy.parameters(), lr=cfg.learning_rate, eps=1e-5)  # core.py:89
+    ex = L.make_experience(n, cfg, dev)
+    env_id = np.arange(n)
+    calls = [0]
+    # gradients live in flat 16 MB buckets whose all-reduces start during backward (dist.GradBuckets)
+    buckets = hd.GradBuckets(policy.parameters(), min_world=1)
+
+    def sync_grads(params):
+        calls[0] += buckets.finish()
+
+    obs, _ = pe.reset()
+    for it in range(2):  # iteration 0 is the warm-up (allocations, RCCL communicator setup)
+        ex.reset_collection()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        obs = L.collect(pe, policy, ex, obs, env_id)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        hd.synced_running_norm_update(policy.obs_norm, ex.obs)  # phc_train.py:329-332 on global moments
+        timers = {}
+        calls[0] = 0
+        stats = L.train(policy, opt, ex, cfg, sync_grads=sync_grads, timers=timers)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+    pe.close()
+    # the all-reduce alone, on the 67.9 MB flat gradient (device tensors; 10 repetitions)
+    flat = torch.ones(L.num_trainable(policy), device=dev)
+    dist.all_reduce(flat)
+    torch.cuda.synchronize()
+    tr = time.perf_counter()
+    for _ in range(10):
+        dist.all_reduce(flat)
+    torch.cuda.synchronize()
+    ar_ms = (time.perf_counter() - tr) / 10 * 1e3
+    ok = bool(torch.isfinite(flat).all()) and float(flat[0]) == float(dist.get_world_size()) ** 11
+    out = {"workload": f"configs[3] per rank: {n} envs x {cfg.batch_size // n} steps into the device Experience "
+                       f"(policy in the loop), GAE, PPO update {cfg.update_epochs} epochs x {cfg.num_minibatches} "
+                       f"minibatches of {cfg.minibatch_size}, gradient all-reduce between backward and clip",
+           "backend": backend, "world_size": dist.get_world_size(), "params": L.num_trainable(policy),
+           "rollout_ms": round((t1 - t0) * 1e3, 2), "gae_ms": round(timers["gae_ms"], 3),
+           "update_ms": round(timers["update_ms"], 2), "allreduce_wait_ms_in_update": round(timers["allreduce_ms"], 3),
+           "allreduce_calls": calls[0], "grad_buckets": len(buckets.buckets),
+           "allreduce_overlapped_with_backward": buckets.overlap, "allreduce_67.9MB_ms": round(ar_ms, 3), "allreduce_ok": ok,
+           "iteration_ms": round((t2 - t0) * 1e3, 2),
+           "train_env_steps_per_s_per_rank": round(cfg.batch_size / (t2 - t0), 1),
+           "losses": {k: round(v, 6) for k, v in stats.items() if k != "minibatches"},
+           "minibatches": stats["minibatches"]}
+    if own_group:
+        dist.destroy_process_group()
+    return out
+
+
 def sim_substeps(args):
     """Physics steps per gym.simulate() of the run's scheme (he_sim_params.substeps)."""
     from humanoid_amd import _abi
@@ -427,6 +519,13 @@ def main():
         a1, a2, _ = kernel_pass(EV_STEPS // 2)
         split = (float(np.median(a1)), float(np.median(a2)))
         ro.set_fused(True)
+    # configs[3]'s learner slice on every rank (RCCL; a one-rank RCCL group at N = 1)
+    learner = None
+    if not args.no_learner and args.num_envs == 4096:
+        try:
+            learner = learner_leg(args, model, local)
+        except Exception as exc:  # report, never fake
+            learner = {"value": None, "error": repr(exc)}
     if world > 1:
         t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -523,6 +622,8 @@ def main():
                 line["tracking_configs2"] = tracking_leg(args, model, local)
             except Exception as exc:  # report, never fake
                 line["tracking_configs2"] = {"value": None, "error": repr(exc)}
+        if learner is not None:
+            line["learner_configs3"] = learner
         if not args.no_puffer_level and world == 1:
             try:
                 line["puffer_env_step"] = puffer_level(args, model)

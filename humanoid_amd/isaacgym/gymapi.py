@@ -320,6 +320,10 @@ class Gym:
             rs = torch.zeros(n, 13, device=sim.engine.device)
             rs[:, :7] = torch.from_numpy(poses).to(rs.device)
             sim.engine.set_root_state_indexed(rs, torch.arange(n, dtype=torch.int32, device=rs.device))
+            # _initial_humanoid_root_states (humanoid_phc.py:522-523) is the root state tensor read
+            # right after prepare_sim with the velocities zeroed: the creation poses, which the
+            # Default / Hybrid state init resets to (he_create_envs set it for the z=0.89 pose only)
+            sim.engine.initial_root_states.copy_(rs)
         return True
 
     # -- tensors ----------------------------------------------------------------------------------

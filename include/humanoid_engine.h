@@ -159,9 +159,11 @@ typedef enum he_buf_kind {
     HE_BUF_DROPPED_CONTACTS = 7, /* i32 [N]   contacts generated past the capacity, last substep */
     HE_BUF_CONTACT_CACHE = 8,  /* f32 [N,HE_CACHE_WORDS] solver warm-start cache (see above) */
     HE_BUF_INIT_ROOT_STATE = 9, /* f32 [N,13] _initial_humanoid_root_states (humanoid_phc.py:522-523):
-                                  the creation poses with zero velocities, set by he_create_envs;
-                                  writable (the facade copies the root states after prepare_sim);
-                                  the Default / Hybrid state init resets to it */
+                                  the creation poses with zero velocities, set by he_create_envs
+                                  (z = 0.89, identity rotation, start_xy); writable: the gym
+                                  facade's prepare_sim writes the actors' own creation poses
+                                  here when they differ; the Default / Hybrid state init resets
+                                  to it */
     HE_BUF_COUNT = 10
 } he_buf_kind;
 

@@ -80,6 +80,75 @@ def test_gloo_world2_collectives():
     assert sorted(shards) == list(range(16))  # disjoint cover of the global env ids
 
 
+def _bucket_worker(rank, world, port, q):
+    """GradBuckets (overlapped bucket all-reduce during backward) against allreduce_gradients on
+    the same model and per-rank batches: the averaged gradients are equal, and two steps in a row
+    keep the views (zero_grad(set_to_none=False))."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from humanoid_amd import dist as hd
+    try:
+        hd.init("gloo")
+
+        def model():
+            torch.manual_seed(0)
+            return torch.nn.Sequential(torch.nn.Linear(40, 64), torch.nn.SiLU(), torch.nn.Linear(64, 64),
+                                       torch.nn.LayerNorm(64), torch.nn.Linear(64, 3))
+        g = torch.Generator().manual_seed(10 + rank)
+        xs = [torch.randn(32, 40, generator=g) for _ in range(2)]
+        ref, mine = model(), model()
+        ok = True
+        opt_r = torch.optim.SGD(ref.parameters(), lr=0.1)
+        opt_m = torch.optim.SGD(mine.parameters(), lr=0.1)
+        gb = hd.GradBuckets(mine.parameters(), bucket_bytes=4096, overlap=True)
+        calls = []
+        for x in xs:
+            opt_r.zero_grad()
+            ref(x).square().mean().backward()
+            hd.allreduce_gradients(list(ref.parameters()))
+            opt_m.zero_grad(set_to_none=False)
+            mine(x).square().mean().backward()
+            calls.append(gb.finish())
+            for a, b in zip(ref.parameters(), mine.parameters()):
+                ok = ok and torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-7)
+            opt_r.step()
+            opt_m.step()
+        q.put((rank, ok, calls, len(gb.buckets)))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_gloo_world2_overlapped_grad_buckets():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+        _, ok, calls, nb = r
+        assert ok and nb >= 3 and calls == [nb, nb]
+
+
+def test_grad_buckets_refuse_lost_views():
+    from humanoid_amd import dist as hd
+    m = torch.nn.Linear(4, 2)
+    gb = hd.GradBuckets(m.parameters(), overlap=False)
+    m(torch.ones(1, 4)).sum().backward()
+    assert gb.finish() == 0  # no process group: nothing to reduce
+    m.zero_grad(set_to_none=True)
+    with pytest.raises(RuntimeError, match="bucket view"):
+        gb.finish()
+
+
 def test_single_process_noops():
     from humanoid_amd import dist as hd
     p = torch.nn.Parameter(torch.ones(3))

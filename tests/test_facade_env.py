@@ -41,7 +41,7 @@ def test_gymapi_surface_and_errors():
 
 
 # ----------------------------------------------------------------------------------- GPU
-def _facade_sim(n, self_collision=True):
+def _facade_sim(n, self_collision=True, pose_fn=None):
     from humanoid_amd.isaacgym import gymapi
     from humanoid_amd.model import DEFAULT_MODEL_JSON
     gym = gymapi.acquire_gym()
@@ -58,7 +58,8 @@ def _facade_sim(n, self_collision=True):
     for i in range(n):
         env = gym.create_env(sim, gymapi.Vec3(-5, -5, 0), gymapi.Vec3(5, 5, 5), 4)
         gym.begin_aggregate(env, 160, 160, True)
-        pose = gymapi.Transform(gymapi.Vec3(0.1 * i, 0.0, 0.89), gymapi.Quat(0, 0, 0, 1))
+        pose = (gymapi.Transform(gymapi.Vec3(0.1 * i, 0.0, 0.89), gymapi.Quat(0, 0, 0, 1)) if pose_fn is None
+                else pose_fn(gymapi, i))
         h = gym.create_actor(env, asset, pose, f"humanoid_{i}", i, 0 if self_collision else 1, 0)
         gym.enable_actor_dof_force_sensors(env, h)
         assert abs(sum(p.mass for p in gym.get_actor_rigid_body_properties(env, h)) - 74.0) < 0.1
@@ -105,6 +106,30 @@ def test_facade_matches_direct_engine(he_model):
     # the views alias engine memory: a write through the view is seen by the engine
     root[0, 2] = 5.0
     assert float(sim.engine.root_states[0, 2]) == 5.0
+
+
+@pytest.mark.gpu
+def test_facade_creation_poses_are_the_default_init_pose():
+    """_initial_humanoid_root_states (humanoid_phc.py:522-523) = the root states after prepare_sim
+    with zero velocities: actors created at their own height and heading must land there, in both
+    the root state tensor and the engine's Default-init buffer (HE_BUF_INIT_ROOT_STATE)."""
+    from humanoid_amd.isaacgym import gymtorch
+    n = 6
+
+    def pose(gymapi, i):
+        yaw = 0.3 * i
+        return gymapi.Transform(gymapi.Vec3(0.2 * i, -0.1 * i, 1.0 + 0.05 * i),
+                                gymapi.Quat(0, 0, np.sin(yaw / 2), np.cos(yaw / 2)))
+
+    gym, sim = _facade_sim(n, pose_fn=pose)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim)).cpu().numpy()
+    init = sim.engine.initial_root_states.cpu().numpy()
+    want = np.zeros((n, 13), np.float32)
+    for i in range(n):
+        yaw = 0.3 * i
+        want[i, :7] = [0.2 * i, -0.1 * i, 1.0 + 0.05 * i, 0, 0, np.sin(yaw / 2), np.cos(yaw / 2)]
+    np.testing.assert_allclose(root, want, atol=1e-6)
+    np.testing.assert_allclose(init, want, atol=1e-6)
 
 
 def _clip_dict(model, k=4, frames=90):

@@ -364,6 +364,66 @@ def test_state_init_hybrid_device_reset_matches_oracle(he_model, model, golden):
     assert not np.allclose(a[ref, 1], a[ref, 0])  # reference inits: rows from the motion
 
 
+@pytest.mark.parametrize("kind", ["Default", "Start", "Hybrid"])
+def test_state_init_matches_reference_golden(he_model, golden, kind):
+    """StateInit Default / Start / Hybrid against the reference itself: tests/golden/state_init.npz
+    holds HumanoidPHC._reset_actors (humanoid_phc.py:679-745) + the _reset_env_tensors bookkeeping +
+    _compute_observations(env_ids), run by tools/gen_golden.py. Hybrid's torch.bernoulli mask and
+    the reference inits' sample_time_interval phases are in the fixture; the engine's one draw per
+    env u reproduces them (u = phase * p for a reference init, u >= p for a Default one; p = 0.5, so
+    u / p is exact). Default envs' rb rows: the engine writes the zero pose's rows, and the fixture
+    feeds the reference's observation the same rows made by poselib's FK (the
+    Default-reset decision), so obs parity covers that choice's arithmetic, not the choice."""
+    g = golden("state_init")
+    s = golden("env_step")
+    n = 24
+    np.testing.assert_array_equal(g["motion_lengths"], s["motion_lengths"])  # one motion library
+    eng = make_engine(he_model, n)
+    eng.load_motions(tables_from_golden(s))
+    eng.root_states.copy_(cu(g["root_in"]))
+    eng.dof_state.copy_(cu(g["dof_in"].reshape(n * 69, 2)))
+    eng.rb_state.copy_(cu(g["rb_in"].reshape(n * 24, 13)))
+    eng.initial_root_states.copy_(cu(g["init_root"]))
+    st, so, go = cu(g["start_times_in"]), cu(g["start_offsets_in"]), cu(g["global_offset_in"])
+    prog = cu(g["progress_in"], torch.int16)
+    em = eng.env_motion(cu(g["motion_ids"], torch.int64), st, so, go, prog)
+    p = _abi.imitation_params(state_init=kind, hybrid_init_prob=0.5)
+    k = kind.lower()
+    ids = g["env_ids"].astype(np.int32)
+    mask, ph = g[k + "_ref_mask"], g[k + "_phases"]
+    if kind == "Hybrid":
+        assert mask.any() and not mask.all()
+        u = np.where(mask, ph * np.float32(0.5), np.float32(0.75)).astype(np.float32)
+    else:
+        u = np.full(len(ids), 0.3, np.float32)  # Start: t = 0; Default: no motion sample
+    obs = torch.zeros(n, 934, device="cuda:0")
+    reset = torch.ones(n, dtype=torch.uint8, device="cuda:0")
+    term = torch.ones(n, dtype=torch.uint8, device="cuda:0")
+    eng.contact_forces.fill_(1.0)
+    eng.reset_envs(p, em, cu(ids, torch.int32), cu(u), obs, reset, term)
+    torch.cuda.synchronize()
+    I = ids
+    rs, gr = eng.root_states.cpu().numpy()[I], g[k + "_root"][I]
+    np.testing.assert_allclose(rs[:, :3], gr[:, :3], atol=2e-6)
+    quat_close(rs[:, 3:7], gr[:, 3:7], 5e-6)
+    np.testing.assert_allclose(rs[:, 7:], gr[:, 7:], atol=1e-5)
+    ds, gd = eng.dof_state.view(n, 69, 2).cpu().numpy()[I], g[k + "_dof"][I]
+    cases.assert_expmap_close(ds[..., 0], gd[..., 0])
+    np.testing.assert_allclose(ds[..., 1], gd[..., 1], atol=1e-5)
+    cases.assert_expmap_close(eng.dof_targets.cpu().numpy()[I], gd[..., 0])  # set_dof_position_target (:763-767)
+    rb, grb = eng.rb_state.view(n, 24, 13).cpu().numpy()[I], g[k + "_rb"][I]
+    np.testing.assert_allclose(rb[..., :3], grb[..., :3], atol=2e-6)
+    quat_close(rb[..., 3:7], grb[..., 3:7], 5e-6)
+    np.testing.assert_allclose(rb[..., 7:], grb[..., 7:], atol=1e-5)
+    np.testing.assert_array_equal(st.cpu().numpy(), g[k + "_start_times"])
+    np.testing.assert_array_equal(so.cpu().numpy(), g[k + "_start_offsets"])
+    np.testing.assert_array_equal(go.cpu().numpy(), g[k + "_global_offset"])
+    np.testing.assert_array_equal(prog.cpu().numpy(), g[k + "_progress"])
+    assert (eng.contact_forces.view(n, 24, 3).cpu().numpy()[I] == 0).all()
+    assert (reset.cpu().numpy()[I] == 0).all() and (term.cpu().numpy()[I] == 0).all()
+    np.testing.assert_allclose(obs.cpu().numpy()[I], g[k + "_obs"][I], atol=5e-5, rtol=1e-5)
+
+
 class CondStats:
     """Counts the elements whose tolerance was widened (see _cond_close) over a whole test."""
 

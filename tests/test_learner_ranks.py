@@ -205,3 +205,88 @@ def test_world2_ranks_rollout_and_synced_update():
     assert m0 == m1, "obs normalisers differ across ranks"
     assert not set(s0) & set(s1) and sorted(s0 + s1) == list(range(2 * N_ENVS))  # disjoint env shards
     assert o0 != o1, "ranks must collect different rollouts (seed 1 + rank)"
+
+
+def _rccl_world1_worker(port, q):
+    """configs[3] per-rank slice at the reference's sizes through a one-rank RCCL group."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    try:
+        import torch.distributed as dist
+        from humanoid_amd import dist as hd, learner as L
+        from humanoid_amd.env import EnvConfig, PHCPufferEnv
+        from humanoid_amd.model import load_default_model
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        backend = dist.get_backend()
+        model = load_default_model()
+        n = 4096
+        cfg = L.TrainConfig()
+        pe = PHCPufferEnv(EnvConfig(num_envs=n, motion_file=_clips(model, k=8, frames=150), seed=1))
+        torch.manual_seed(0)
+        policy = L.make_policy(dev)
+        nparams = L.num_trainable(policy)
+        opt = torch.optim.Adam(policy.parameters(), lr=cfg.learning_rate, eps=1e-5)
+        ex = L.make_experience(n, cfg, dev)
+        obs, _ = pe.reset()
+        L.collect(pe, policy, ex, obs, np.arange(n))
+        rows = ex.ptr
+        hd.synced_running_norm_update(policy.obs_norm, ex.obs)
+        before = [p.detach().clone() for p in policy.parameters() if p.requires_grad]
+        seen = {}
+
+        def sync_grads(params):
+            pre = torch.cat([p.grad.reshape(-1) for p in params]).clone()
+            seen["calls"] = hd.allreduce_gradients(params, min_world=1)
+            post = torch.cat([p.grad.reshape(-1) for p in params])
+            seen["identical"] = bool(torch.equal(pre, post))  # sum over one rank / 1 = the gradient itself
+            seen["grad_bytes"] = int(pre.numel() * 4)
+            seen["finite"] = bool(torch.isfinite(pre).all())
+
+        stats = L.train(policy, opt, ex, cfg, sync_grads=sync_grads, epochs=1, max_minibatches=1)
+        # the bucket-view form: all-reduces launched from the backward hooks on the flat buckets
+        gb = hd.GradBuckets(policy.parameters(), min_world=1)
+
+        def sync_buckets(params):
+            pre = torch.cat([p.grad.reshape(-1) for p in params]).clone()
+            seen["bucket_calls"] = gb.finish()
+            seen["bucket_identical"] = bool(torch.equal(pre, torch.cat([p.grad.reshape(-1) for p in params])))
+
+        L.train(policy, opt, ex, cfg, sync_grads=sync_buckets, epochs=1, max_minibatches=1)
+        seen["buckets"] = len(gb.buckets)
+        moved = sum(int(not torch.equal(b, p.detach())) for b, p in
+                    zip(before, [p for p in policy.parameters() if p.requires_grad]))
+        adv_ok = bool(torch.isfinite(ex.b_advantages).all() and torch.isfinite(ex.b_returns).all())
+        q.put(("ok", backend, nparams, rows, seen, stats, moved, adv_ok, tuple(ex.b_obs.shape)))
+        pe.close()
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put(("error", traceback.format_exc()))
+
+
+def test_configs3_rank_slice_through_rccl_world1():
+    """BASELINE configs[3] per rank on one GPU: 4096 envs x 32 steps into the device Experience with
+    the reference-size policy (16,984,134 params, phc_policy.py:23-66) in the loop, GAE, one PPO
+    minibatch step of 32768 rows, and the 67.9 MB gradient all-reduce on device tensors between
+    backward and clip (core.py:366-373) through a one-rank RCCL ("nccl") group."""
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert res[0] == "ok", res[1]
+    _, backend, nparams, rows, seen, stats, moved, adv_ok, bshape = res
+    assert backend == "nccl"
+    assert nparams == 16_984_134
+    assert rows == 131072 and bshape == (4, 4096, 8, 934)
+    assert seen["calls"] == 2 and seen["grad_bytes"] == 67_936_536  # 2 buckets of <= 64 MB
+    assert seen["identical"] and seen["finite"]
+    assert seen["bucket_calls"] == seen["buckets"] >= 4 and seen["bucket_identical"]
+    assert adv_ok and all(np.isfinite(v) for v in (stats["pg_loss"], stats["v_loss"], stats["bound_loss"]))
+    assert moved > 0

@@ -151,6 +151,55 @@ def test_env_reset_glue(golden):
     assert (st["progress"][others] == 7).all()
 
 
+@pytest.mark.parametrize("kind", ["Default", "Start", "Hybrid"])
+def test_state_init_kinds_match_reference(golden, model, kind):
+    """StateInit Default / Start / Hybrid (humanoid_phc.py:679-745, 747-780, 937-961) against the
+    reference's own _reset_actors run (tests/golden/state_init.npz, tools/gen_golden.py). Hybrid's
+    Bernoulli mask and phases come from the fixture: u = phase * p for a reference init, u >= p for
+    a Default one (p = 0.5: u / p exact). Default envs' rb rows are the engine's decision (the zero
+    pose's rows); the fixture made them with poselib's FK, so the rows and the obs read from them
+    are compared too."""
+    g = golden("state_init")
+    s = golden("env_step")
+    np.testing.assert_array_equal(g["motion_lengths"], s["motion_lengths"])
+    mt = _tables(s)
+    n = 24
+    c = lambda x, t=np.float32: np.ascontiguousarray(x, t)  # noqa: E731
+    st = dict(start_times=c(g["start_times_in"]), start_offsets=c(g["start_offsets_in"]),
+              global_offset=c(g["global_offset_in"]), progress=c(g["progress_in"], np.int16),
+              root_states=c(g["root_in"]), dof_state=c(g["dof_in"]), dof_targets=np.zeros((n, 69), np.float32),
+              rb_state=c(g["rb_in"]), contact_forces=np.ones((n, 24, 3), np.float32),
+              obs=np.zeros((n, 934), np.float32), reset=np.ones(n, np.uint8), terminate=np.ones(n, np.uint8),
+              init_root=c(g["init_root"]))
+    k = kind.lower()
+    ids = g["env_ids"]
+    mask, ph = g[k + "_ref_mask"], g[k + "_phases"]
+    if kind == "Hybrid":
+        assert mask.any() and not mask.all()
+        u = np.where(mask, ph * np.float32(0.5), np.float32(0.75)).astype(np.float32)
+    else:
+        u = np.full(len(ids), 0.3, np.float32)
+    p = _abi.imitation_params(state_init=kind, hybrid_init_prob=0.5)
+    O.reset_envs(p, mt, ids, u, g["motion_ids"], st, rest_pos=O.rest_positions(model))
+    rs, gr = st["root_states"][ids], g[k + "_root"][ids]
+    np.testing.assert_allclose(rs[:, :3], gr[:, :3], atol=2e-6)
+    quat_close(rs[:, 3:7], gr[:, 3:7], 5e-6)
+    np.testing.assert_allclose(rs[:, 7:], gr[:, 7:], atol=1e-5)
+    cases.assert_expmap_close(st["dof_state"][ids, :, 0], g[k + "_dof"][ids, :, 0])
+    np.testing.assert_allclose(st["dof_state"][ids, :, 1], g[k + "_dof"][ids, :, 1], atol=1e-5)
+    cases.assert_expmap_close(st["dof_targets"][ids], g[k + "_dof"][ids, :, 0])
+    rb, grb = st["rb_state"][ids], g[k + "_rb"][ids]
+    np.testing.assert_allclose(rb[..., :3], grb[..., :3], atol=2e-6)
+    quat_close(rb[..., 3:7], grb[..., 3:7], 5e-6)
+    np.testing.assert_allclose(rb[..., 7:], grb[..., 7:], atol=1e-5)
+    np.testing.assert_array_equal(st["start_times"], g[k + "_start_times"])
+    np.testing.assert_array_equal(st["start_offsets"], g[k + "_start_offsets"])
+    np.testing.assert_array_equal(st["global_offset"], g[k + "_global_offset"])
+    np.testing.assert_array_equal(st["progress"], g[k + "_progress"])
+    assert (st["contact_forces"][ids] == 0).all()
+    np.testing.assert_allclose(st["obs"][ids], g[k + "_obs"][ids], atol=5e-5, rtol=1e-5)
+
+
 def test_host_motion_loader_matches_reference(golden, model):
     from humanoid_amd.motion_lib import build_tables
     g = golden("motion_lib")

@@ -11,7 +11,8 @@ simulator is called: the env-level fixtures call ``HumanoidPHC._compute_reward``
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
         PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py amp     (one part only)
-Writes: tests/golden/{quat_prims,skeleton,motion_lib,imitation_funcs,env_step,env_reset,pd_targets,amp}.npz
+Writes: tests/golden/{quat_prims,skeleton,motion_lib,imitation_funcs,env_step,env_reset,pd_targets,amp,
+        state_init}.npz
 """
 import os
 import sys
@@ -391,6 +392,115 @@ def gen_pd():
                         scale=t2n(env._pd_action_scale), actions=t2n(a), pd_target=t2n(pd))
 
 
+# --------------------------------------------------------------------------------- StateInit kinds
+def zero_pose_rows(tree, init_root):
+    """Rigid-body rows of the zero local pose at the given root states (the engine's Default-reset
+    rows, an engine decision: the reference leaves the rb tensor to refresh), by the
+    reference's own forward kinematics (poselib SkeletonState)."""
+    from puffer_phc.poselib_skeleton import SkeletonState
+    n = init_root.shape[0]
+    r = torch.zeros(n, 24, 4)
+    r[..., 3] = 1.0
+    r[:, 0] = init_root[:, 3:7]
+    sk = SkeletonState.from_rotation_and_root_translation(tree, r, init_root[:, 0:3], is_local=True)
+    rows = torch.zeros(n, 24, 13)
+    rows[..., 0:3] = sk.global_translation
+    rows[..., 3:7] = sk.global_rotation
+    return rows
+
+
+def gen_state_init(tree, clips):
+    """_reset_actors for StateInit Default / Start / Hybrid (humanoid_phc.py:679-745) followed by the
+    _reset_env_tensors bookkeeping (:747-780) and _compute_observations(env_ids) (:937-961), on one
+    pre-reset state. Hybrid's Bernoulli mask and the reference inits' phases are recorded (the
+    torch RNG draws of torch.bernoulli and sample_time_interval after manual_seed). For Default envs
+    the rb rows fed to the observation are the zero pose's rows at the initial root state (see
+    zero_pose_rows): the reference reads whatever refresh returns there."""
+    g = torch.Generator().manual_seed(13)
+    N = 24
+    lib = build_motion_lib(tree, clips, [i % 5 for i in range(N)])
+    lens = lib._motion_lengths[torch.arange(N)]
+    st0 = ((torch.rand(N, generator=g) * lens) / (1 / 30)).long() * (1 / 30)
+    so0 = torch.where(torch.rand(N, generator=g) < 0.3, torch.rand(N, generator=g) * 0.05, torch.zeros(N))
+    go0 = torch.randn(N, 3, generator=g) * 0.1
+    prog0 = torch.randint(0, 30, (N,), generator=g).to(torch.short)
+    root0 = torch.zeros(N, 13)
+    root0[:, 0:2] = torch.rand(N, 2, generator=g) * 2 - 1
+    root0[:, 2] = 0.9 + 0.2 * torch.rand(N, generator=g)
+    q = torch.randn(N, 4, generator=g)
+    root0[:, 3:7] = q / q.norm(dim=-1, keepdim=True)
+    root0[:, 7:13] = torch.randn(N, 6, generator=g)
+    dof0 = torch.randn(N, 69, 2, generator=g) * 0.3
+    rb0 = torch.randn(N, 24, 13, generator=g)
+    rb0[..., 3:7] = rb0[..., 3:7] / rb0[..., 3:7].norm(dim=-1, keepdim=True)
+    init_root = torch.zeros(N, 13)  # creation poses (start xy jitter, z 0.89, a heading), zero velocity
+    init_root[:, 0:2] = torch.rand(N, 2, generator=g) * 2 - 1
+    init_root[:, 2] = 0.89
+    yaw = (torch.rand(N, generator=g) * 2 - 1) * np.pi
+    init_root[:, 5] = torch.sin(yaw / 2)
+    init_root[:, 6] = torch.cos(yaw / 2)
+    env_ids = torch.tensor([1, 2, 5, 8, 11, 12, 14, 19, 22, 23])
+    out = dict(motion_ids=torch.arange(N), start_times_in=st0, start_offsets_in=so0, global_offset_in=go0,
+               progress_in=prog0, root_in=root0, dof_in=dof0, rb_in=rb0, init_root=init_root, env_ids=env_ids,
+               hybrid_init_prob=torch.tensor(0.5), motion_lengths=lib._motion_lengths, length_starts=lib.length_starts)
+    for kind, seed in ((StateInit.Default, 31), (StateInit.Start, 32), (StateInit.Hybrid, 33)):
+        env = fake_env(lib, tree, N)
+        env._sampled_motion_ids = torch.arange(N)
+        env._motion_start_times[:] = st0
+        env._motion_start_times_offset[:] = so0
+        env._global_offset[:] = go0
+        env.progress_buf[:] = prog0
+        env._root_states[:] = root0
+        env._dof_state.view(N, 69, 2)[:] = dof0
+        env._rigid_body_state.view(N, 24, 13)[:] = rb0
+        env._initial_humanoid_root_states = init_root.clone()
+        env._initial_dof_pos = torch.zeros(N, 69)
+        env._initial_dof_vel = torch.zeros(N, 69)
+        env.cfg.state_init = kind
+        env.cfg.hybrid_init_prob = 0.5
+        seen = {"default": torch.zeros(0, dtype=torch.long), "ref": torch.zeros(0, dtype=torch.long)}
+        rd, rr = env._reset_default, env._reset_ref_state_init
+
+        def rec_default(ids, rd=rd, seen=seen):
+            seen["default"] = ids.clone()
+            return rd(ids)
+
+        def rec_ref(ids, rr=rr, seen=seen):
+            seen["ref"] = ids.clone()
+            return rr(ids)
+
+        env._reset_default, env._reset_ref_state_init = rec_default, rec_ref
+        # the draws the reference makes, in its order (torch.bernoulli, then sample_time_interval)
+        torch.manual_seed(seed)
+        mask = torch.ones(len(env_ids), dtype=torch.bool)
+        phases = torch.zeros(len(env_ids))
+        if kind == StateInit.Hybrid:
+            mask = torch.bernoulli(torch.full((len(env_ids),), 0.5)) == 1.0
+            phases[mask] = torch.rand(int(mask.sum()))
+        elif kind == StateInit.Default:
+            mask[:] = False
+        torch.manual_seed(seed)
+        env._reset_actors(env_ids)
+        assert torch.equal(seen["ref"], env_ids[mask]) and torch.equal(seen["default"], env_ids[~mask])
+        env.progress_buf[env_ids] = 0  # _reset_env_tensors (:775-780)
+        env.reset_buf[env_ids] = 0
+        env._terminate_buf[env_ids] = 0
+        env._contact_forces[env_ids] = 0
+        d = seen["default"]
+        if len(d):
+            env._rigid_body_state.view(N, 24, 13)[d] = zero_pose_rows(tree, init_root[d])
+        env._compute_observations(env_ids)
+        name = str(kind).split(".")[-1].lower()
+        out.update({f"{name}_ref_mask": mask, f"{name}_phases": phases, f"{name}_root": env._root_states.clone(),
+                    f"{name}_dof": env._dof_state.view(N, 69, 2).clone(),
+                    f"{name}_rb": env._rigid_body_state.view(N, 24, 13).clone(),
+                    f"{name}_start_times": env._motion_start_times.clone(),
+                    f"{name}_start_offsets": env._motion_start_times_offset.clone(),
+                    f"{name}_global_offset": env._global_offset.clone(), f"{name}_progress": env.progress_buf.clone(),
+                    f"{name}_obs": env.obs_buf.clone()})
+    np.savez_compressed(os.path.join(OUT, "state_init.npz"), **{k: t2n(v) for k, v in out.items()})
+
+
 # --------------------------------------------------------------------------------- AMP obs (§8f-4)
 def amp_dof_subset():
     # the index list HumanoidPHC._config_robot builds (humanoid_phc.py:186-194); that method also
@@ -494,6 +604,10 @@ def main():
         tree = SkeletonTree.from_mjcf(XML)
         gen_amp(tree, make_clips())
         return
+    if sys.argv[1:] == ["state_init"]:
+        tree = SkeletonTree.from_mjcf(XML)
+        gen_state_init(tree, make_clips())
+        return
     gen_quat_prims()
     tree = gen_skeleton()
     clips, _ = gen_motion_lib(tree)
@@ -501,6 +615,7 @@ def main():
     gen_env(tree, clips)
     gen_pd()
     gen_amp(tree, clips)
+    gen_state_init(tree, clips)
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
