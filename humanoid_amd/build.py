@@ -75,15 +75,29 @@ def _compile(hipcc, cmd, src, o, force, hdr_time, verbose):
             print(" ".join(cmd))
         if os.path.basename(src) in MIN_OCCUPANCY:
             cmd = cmd + ["-Rpass-analysis=kernel-resource-usage"]
+        # a failed compile or occupancy check leaves neither the object nor the stamp behind, so the
+        # next build cannot mistake a rejected object for an up-to-date one
+        _discard(o, stamp)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
+            _discard(o, stamp)
             raise RuntimeError(f"hipcc failed for {os.path.basename(src)}:\n{r.stderr}")
-        _check_occupancy(src, r.stderr)
+        try:
+            _check_occupancy(src, r.stderr)
+        except RuntimeError:
+            _discard(o, stamp)
+            raise
         cmd = cmd[:-1] if cmd[-1] == "-Rpass-analysis=kernel-resource-usage" else cmd
         with open(stamp, "w") as f:
             f.write(" ".join(cmd))
         return True
     return False
+
+
+def _discard(*paths):
+    for p in paths:
+        if os.path.exists(p):
+            os.remove(p)
 
 
 def _link(hipcc, lib, objs, force):

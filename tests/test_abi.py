@@ -95,3 +95,35 @@ def test_mjcf_roundtrip_matches_baked_json(model):
     np.testing.assert_allclose(m.local_pos, model.local_pos)
     np.testing.assert_allclose(m.mass, model.mass)
     np.testing.assert_allclose(m.inertia, model.inertia)
+
+
+def test_occupancy_guard_removes_the_rejected_object(tmp_path, monkeypatch):
+    """build._compile must not leave an object (or its command stamp) behind when the occupancy check
+    rejects it: the next build would otherwise see an up-to-date object and skip the check."""
+    import subprocess
+    import types
+    from humanoid_amd import build
+    src = tmp_path / "he_physics.hip"
+    src.write_text("// fake")
+    o = str(tmp_path / "he_physics.hip.o")
+    stamp = o + ".cmd"
+    remark = ("remark: Function Name: physics_kernel\nremark:     VGPRs: 300\n"
+              "remark:     Occupancy [waves/SIMD]: 1\n")
+
+    def fake_run(cmd, capture_output=True, text=True):
+        out = cmd[cmd.index("-o") + 1]
+        with open(out, "w") as f:
+            f.write("object")
+        return types.SimpleNamespace(returncode=0, stderr=remark, stdout="")
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    cmd = ["hipcc", "-c", str(src), "-o", o]
+    with open(stamp, "w") as f:  # a stamp from an earlier build with the same command
+        f.write(" ".join(cmd))
+    with pytest.raises(RuntimeError, match="occupancy 1"):
+        build._compile("hipcc", cmd, str(src), o, True, 0.0, False)
+    assert not os.path.exists(o) and not os.path.exists(stamp)
+    # a passing report keeps the object and writes the stamp
+    remark = remark.replace("SIMD]: 1", "SIMD]: 2")
+    assert build._compile("hipcc", cmd, str(src), o, True, 0.0, False)
+    assert os.path.exists(o) and open(stamp).read() == " ".join(cmd)

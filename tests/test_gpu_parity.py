@@ -298,7 +298,9 @@ def test_state_init_default_and_hybrid_match_oracle(he_model, model, golden, sta
     he_reset_envs after 3 policy steps: Default writes the initial root state, zero dofs and targets,
     the zero pose's body rows and leaves the motion bookkeeping; Hybrid splits the envs by the draw
     u < hybrid_init_prob (reference init at phase u / p, else Default). Against the oracle's reset from
-    the engine's own pre-reset state; both kinds occur in the Hybrid case."""
+    the engine's own pre-reset state; both kinds occur in the Hybrid case.
+    Self-consistency (engine vs the builder's oracle); reference parity of these kinds is
+    test_state_init_matches_reference_golden."""
     n = 24
     eng, em, bk, mt, init = _state_init_case(he_model, model, golden, n)
     p = _abi.imitation_params(state_init=state_init, hybrid_init_prob=0.5)
@@ -324,7 +326,8 @@ def test_state_init_hybrid_device_reset_matches_oracle(he_model, model, golden):
     is the splitmix hash of (seed, step, env), resolved as in he_reset_envs. Envs are made to fail
     (bodies thrown off their reference), their reset rows checked against the oracle's reset with
     the same draws; AMP history rows of Default-reset envs equal their current row
-    (_init_amp_obs_default, humanoid_phc.py:801-803)."""
+    (_init_amp_obs_default, humanoid_phc.py:801-803).
+    Self-consistency: the reference raises for Default + AMP (humanoid_phc.py:794-795)."""
     n = 24
     eng, em, bk, mt, init = _state_init_case(he_model, model, golden, n)
     S = 4
