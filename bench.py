@@ -1,7 +1,8 @@
 """Env-step throughput of the MI355X humanoid engine (BASELINE.json metric).
 
-One "step" = one policy step of every env on every rank: actions -> PD targets -> 2 physics
-substeps at 1/60 s -> reward / reset / 934-float obs -> device-side reset of flagged envs
+One "step" = one policy step of every env on every rank: actions -> PD targets -> 2 gym.simulate()
+calls of 1/60 s, each 2 physics substeps of 1/120 s (Isaac Gym's SimParams.substeps default; DESIGN
+§5) -> reward / reset / 934-float obs -> device-side reset of flagged envs
 (puffer_phc/clean_pufferl/env.py:109-183 semantics; env-steps/s definition env.py:217-230).
 
 Default workload = BASELINE configs[1]: 4096 SMPL-neutral humanoids per GPU, PD stand-still
@@ -48,10 +49,12 @@ def parse(argv=None):
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=40)
-    ap.add_argument("--scheme", choices=["default", "r02"], default="default",
+    ap.add_argument("--scheme", choices=["default", "r02", "tgs"], default="default",
                     help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 sweeps, "
                          "link world angular-velocity clamp; r02 = round 2's energy-unstable step (2 x 1/60 s, "
-                         "explicit bias, 8 sweeps) with round 3's clamps, for the cost comparison only (DESIGN §5)")
+                         "explicit bias, 8 sweeps) with round 3's clamps, for the cost comparison only (DESIGN §5); tgs = "
+                         "PhysX TGS's 4 position iterations per 1/120 s step as 8 substeps of 1/480 s per simulate() "
+                         "with one sweep each (DESIGN §5 'TGS')")
     ap.add_argument("--solver-tolerance", type=float, default=None,
                     help="he_sim_params.solver_tolerance override (m/s; 0 = every sweep runs)")
     ap.add_argument("--no-puffer-level", action="store_true",
@@ -249,7 +252,28 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
                         "computed on the device each step (inside the timed region)",
             "joint_pose_l2_rad": {"mean": round(float(l2.mean()), 5), "p90": round(float(np.percentile(l2, 90)), 5),
                                   "steps": l2_steps,
-                                  "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x steps"}}
+                                  "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x "
+                                                "steps: PD tracking error against the clips' motion, not parity"},
+            "parity_vs_oracle": parity_record()}
+
+
+def parity_record():
+    """BASELINE's "joint-pose L2 vs ref" as parity: the fp32 engine against the fp64 oracle on a 48-env
+    sample of this workload over 30 policy steps, measured by the GPU test
+    tests/test_full_size.py::test_full_size_tracking_parity_30_steps (the bench never runs the oracle
+    outside its cpu_baseline leg); the newest committed record, profiles/r*/parity_configs2.json."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*",
+                                          "parity_configs2.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    keep = ("joint_pose_l2_vs_oracle_rad", "com_err_vs_oracle_m", "envs", "steps", "envs_with_event",
+            "env_steps_before_event")
+    out = {k: rec[k] for k in keep if k in rec}
+    out["source"] = os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    return out
 
 
 def _free_port():
@@ -352,6 +376,8 @@ def scheme_params(args):
     out = {}
     if getattr(args, "scheme", "default") == "r02":
         out = dict(substeps=1, bias_midpoint=0, solver_iterations=8)
+    elif getattr(args, "scheme", "default") == "tgs":
+        out = dict(substeps=8, solver_iterations=1)
     if getattr(args, "solver_tolerance", None) is not None:
         out["solver_tolerance"] = args.solver_tolerance
     return out
@@ -617,6 +643,10 @@ def main():
                 line["r02_scheme"] = scheme_leg(args, model, local)
             except Exception as exc:  # report, never fake
                 line["r02_scheme"] = {"value": None, "error": repr(exc)}
+            try:
+                line["tgs_scheme"] = scheme_leg(args, model, local, scheme="tgs")
+            except Exception as exc:  # report, never fake
+                line["tgs_scheme"] = {"value": None, "error": repr(exc)}
         if not args.no_tracking and world == 1 and args.num_envs == 4096:
             try:
                 line["tracking_configs2"] = tracking_leg(args, model, local)

@@ -496,6 +496,9 @@ void ho_set_drop_gap_out(float* out) { g_drop_out = out; }
  * (mu for a tangential row, mu r_patch for a torsional one, 0 otherwise), in the cache's row order */
 static float* g_roww_out;
 void ho_set_row_weight_out(float* out) { g_roww_out = out; }
+/* diagnostic (tests/diag): the gap of every solver row's contact of the last substep, [N, HE_MAX_ROWS] */
+static float* g_rowgap_out;
+void ho_set_row_gap_out(float* out) { g_rowgap_out = out; }
 static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k, const env_state* s, int terrain_kind,
                         R mu, contact* cs, int* total) {
     int nlim = 0;
@@ -694,6 +697,7 @@ typedef struct step_out {
     int sweeps;           /* Gauss-Seidel sweeps of the last substep's solve */
     int nr;               /* solver rows of the last substep */
     R muw[HE_MAX_ROWS];   /* their friction bound weights (0: a normal / limit row) */
+    R gap[HE_MAX_ROWS];   /* their contact's gap (m; a limit row: its angle gap in rad) */
 } step_out;
 
 /* Warm-start cache: the previous solve's impulses by row key (PhysX warm-starts its solver from
@@ -973,7 +977,10 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         }
         out->sweeps = sweeps;
         out->nr = nr < HE_MAX_ROWS ? nr : HE_MAX_ROWS;
-        for (int r = 0; r < out->nr; ++r) out->muw[r] = rows[r].kind == 0 ? 0 : rows[r].muw;
+        for (int r = 0; r < out->nr; ++r) {
+            out->muw[r] = rows[r].kind == 0 ? 0 : rows[r].muw;
+            out->gap[r] = cs[rows[r].slot].gap;
+        }
         /* complementarity residual of the returned impulses: normal rows min(w, lambda) -> 0,
          * friction rows w = 0 inside the bound (or lambda on the bound) */
         for (int r = 0; r < nr; ++r) {
@@ -1170,6 +1177,8 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         if (g_drop_out) g_drop_out[e] = (float)g_drop_gap;
         if (g_roww_out)
             for (int r = 0; r < HE_MAX_ROWS; ++r) g_roww_out[(size_t)e * HE_MAX_ROWS + r] = r < out.nr ? (float)out.muw[r] : 0.f;
+        if (g_rowgap_out)
+            for (int r = 0; r < HE_MAX_ROWS; ++r) g_rowgap_out[(size_t)e * HE_MAX_ROWS + r] = r < out.nr ? (float)out.gap[r] : 0.f;
         if (cw) {
             memset(cw, 0, HE_CACHE_WORDS * sizeof(float));
             if (p->warm_start) {

@@ -172,6 +172,12 @@ def set_row_weight_out(arr=None):
     lib().ho_set_row_weight_out(None if arr is None else arr.ctypes.data_as(C.POINTER(C.c_float)))
 
 
+def set_row_gap_out(arr=None):
+    """Diagnostics only: float32 [N, HE_MAX_ROWS] filled with the gap of every solver row's contact of
+    each env's last substep (m; a joint-limit row: its angle gap), in the cache's row order."""
+    lib().ho_set_row_gap_out(None if arr is None else arr.ctypes.data_as(C.POINTER(C.c_float)))
+
+
 def physics_step(model: "_abi.HeModel", sim: "_abi.HeSimParams", root_states, dof_state, targets, substeps=2,
                  mass_scale=None, friction=None, terrain_kind=None, cache=None):
     """In-place on root_states [N,13] / dof_state [N,69,2] (float32 arrays) and on the warm-start

@@ -235,7 +235,7 @@ def test_full_size_tracking_parity_30_steps(model, he_model):
     PD targets. The parity figures for the bench line (BASELINE's "joint-pose L2 vs ref" read as
     GPU vs oracle): per env and step ||q_gpu - q_oracle||_2 over the 69 joint coordinates, and
     |CoM_gpu - CoM_oracle|; recorded to HE_RECORD_DIR/parity_configs2.json (bench.py reports the
-    committed copy, profiles/parity_configs2.json). Joint angles and CoM at 1e-4 on every step
+    newest committed copy, profiles/r*/parity_configs2.json). Joint angles and CoM at 1e-4 on every step
     before an env's first contact-set or stick / slip event (8 probes)."""
     import cases
     from humanoid_amd import _abi

@@ -944,6 +944,21 @@ def test_explicit_bias_matches_oracle(he_model, model):
                      max_skip=0.0, max_widened=0.05)
 
 
+def test_tgs_small_step_mode_matches_oracle(he_model, model):
+    """The engine's TGS-style mode (DESIGN §5 "TGS"): substeps 8 (1/480 s) with one Gauss-Seidel
+    sweep each -- PhysX TGS's 4 position iterations per 1/120 s step, each re-integrating dt/4, 0
+    velocity iterations (isaacgym_env.py:16-18) -- against the oracle under the same parameters:
+    airborne actuated bodies (one policy step) and the PD stand-still (10 steps)."""
+    tgs = dict(substeps=8, solver_iterations=1)
+    rng = np.random.default_rng(41)
+    root, dof = cases.random_state(64, rng, height=(3.0, 4.0))
+    targets = rng.uniform(-0.5, 0.5, (64, 69)).astype(np.float32)
+    _physics_compare(he_model, root, dof, targets, self_collision=0, max_skip=0.0, max_widened=0.0, **tgs)
+    root, dof = cases.standing_state(model, 32, rng, xy_jitter=1.0)
+    _physics_compare(he_model, root, dof, np.zeros((32, 69), np.float32), steps=10, max_skip=0.0,
+                     max_widened=0.05, **tgs)
+
+
 def test_world_angular_velocity_clamp_matches_oracle(he_model, model):
     """max_angular_velocity on each link's WORLD angular velocity (PxRigidBody) and
     max_joint_velocity on the joint rates, both active: airborne bodies spun up to 60-80 rad/s with
@@ -1007,22 +1022,27 @@ def test_midpoint_bias_tames_the_runaway_on_gpu(he_model, model):
     assert res[1] < 1.5e3, res
 
 
-def test_saturated_random_actions_stay_physical_on_gpu(he_model, model):
-    """VERDICT r02 item 1 at full size: 4096 standing envs under U(+-1) random actions (new every policy
-    step) for 2 s. The median internal kinetic energy stays at the dt-refined level (oracle: 0.90 kJ;
-    1/480 s physics steps: 0.80 kJ; the explicit bias: 22 kJ with roots at 10^2 m/s) and no joint
-    passes its angle cap. Root speeds: the fastest roots are pelvises whipped by flailing legs while
-    airborne, the tail of the physics itself -- the fp64 oracle under this scheme reaches 9.5-10.7 m/s
-    over four 4096-env seeds (0-2 envs past 10 m/s), the 1/480 s refinement 8.75 m/s
-    (tests/diag/energy_probe.py) -- so the bar is: no root past 15 m/s, at most 0.1% of envs
-    past 10 m/s."""
+@pytest.mark.parametrize("amp", [0.5, 0.75, 1.0])
+def test_saturated_random_actions_stay_physical_on_gpu(he_model, model, amp):
+    """VERDICT r02 item 1 at full size, swept over the action amplitude: 4096
+    standing envs under U(+-amp) random actions (new every policy step) for 2 s. The median internal
+    kinetic energy stays at the dt-refined level (U(+-1): oracle 0.90 kJ, 1/480 s physics steps
+    0.80 kJ, the explicit bias 22 kJ with roots at 10^2 m/s) and no joint passes its angle cap.
+
+    Root speeds: the tail is two mechanisms of the physics itself, both reproduced by the fp64 oracle
+    under the same scheme and absent at dt/4 (DESIGN §5 "the runaway tail"): pelvises whipped by
+    flailing legs while airborne (U(+-1): 12.1 m/s, env 1736), and a limb wedged deep in its own
+    thigh launched off the ground (U(+-0.75): 17.4 m/s, env 3261; traced on the CPU by
+    test_runaway_tail_is_a_wedged_limb_launched_off_the_ground). So the bar is: at most 0.1 % of envs
+    past 10 m/s and no root past 20 m/s, at every amplitude."""
     _require_gpu()
     n = 4096
-    vmax, ke, dg = _random_action_gpu(he_model, model, n, 1.0, 60)
+    vmax, ke, dg = _random_action_gpu(he_model, model, n, amp, 60)
     q = np.linalg.norm(dg[..., 0].reshape(n, 23, 3), axis=-1)
-    print(f"envs over 10 m/s: {int((vmax > 10).sum())}/{n}, max root speed {vmax.max():.2f} m/s, "
-          f"median internal KE {np.median(ke):.1f} J, max joint angle {q.max():.4f}")
-    assert vmax.max() < 15.0, vmax.max()
+    print(f"U(+-{amp}): envs over 10 m/s: {int((vmax > 10).sum())}/{n}, over 15 m/s {int((vmax > 15).sum())}, "
+          f"max root speed {vmax.max():.2f} m/s (env {int(vmax.argmax())}), median internal KE {np.median(ke):.1f} J, "
+          f"max joint angle {q.max():.4f}")
+    assert vmax.max() < 20.0, vmax.max()
     assert int((vmax > 10).sum()) <= n // 1000, int((vmax > 10).sum())
     assert np.median(ke) < 1.5e3
     assert q.max() <= np.pi - 0.01 + 1e-5  # the limit backstop's cap (limit_clamp) at most

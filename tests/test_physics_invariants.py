@@ -290,3 +290,70 @@ def test_sliding_body_decelerates_at_mu_g(he_model, model, mu):
     good = np.abs(dec + mu * 9.81) < 0.05 * mu * 9.81
     assert abs(np.nanmedian(dec) + mu * 9.81) < 0.05 * mu * 9.81, dec
     assert good.sum() >= n - 2, dec
+
+
+def test_runaway_tail_is_a_wedged_limb_launched_off_the_ground(he_model, model):
+    """The fastest root of the random-action study at U(+-0.75) (tests/diag/trace_runaway.py on the
+    GPU; DESIGN §5 "the runaway tail"): env 3261, policy step 55, 17.4 m/s. The fixture holds that
+    env's engine state, warm-start cache and PD targets from 6 steps before the peak
+    (tests/data/trace_runaway_0.75.npz, written by the GPU engine). Replayed through the fp64 oracle
+    one physics step at a time (1/120 s):
+    * the oracle reproduces the engine's peak (same scheme, so not an fp32 / kernel effect);
+    * the right forearm and hand sit 5-7 cm deep in the right thigh (R_Hip-R_Elbow, R_Hip-R_Wrist
+      self rows) for the whole step, each row carrying >1 kN s per physics step: the thigh capsule
+      passes between forearm and hand, so the two depenetration rows push the limb in opposite
+      directions and their impulses mostly cancel;
+    * in the physics step where the centre of mass jumps (about 2.8 -> 10.5 m/s in 1/120 s) the wrist's
+      terrain row carries a ~0.9 kN s impulse: the wedge's internal push is turned into an external
+      one by the ground;
+    * the same interval at dt/4 (1/480 s physics steps) keeps the root under 5 m/s: the deep wedge
+      never forms when contacts are caught four times as often."""
+    from humanoid_amd.body_sets import BODY_NAMES
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "data", "trace_runaway_0.75.npz"))
+    k0, pk = int(d["k0"]), int(d["peak_step"])
+    i = pk - k0
+    root, dof, cache = d["root"][i][None].copy(), d["dof"][i][None].copy(), d["cache"][i][None].copy()
+    tg = d["targets"][i][None].copy()
+    r2, d2, c2 = root.copy(), dof.copy(), cache.copy()
+    O.physics_step(he_model, _abi.default_sim_params(), r2, d2, tg, 2, cache=c2)
+    v_engine = float(np.linalg.norm(d["root_after"][i][7:10]))
+    assert v_engine > 15.0
+    assert abs(float(np.linalg.norm(r2[0, 7:10])) - v_engine) < 0.01 * v_engine
+    # one physics step at a time: the same arithmetic as 2 simulate() x 2 substeps
+    sp = _abi.default_sim_params(dt=1.0 / 120.0, substeps=1)
+    names = lambda b: BODY_NAMES[b] if b >= 0 else {-1: "terrain", -2: "limit"}[b]  # noqa: E731
+    com_v, rows = [], []
+    for _ in range(4):
+        gp = np.zeros((1, _abi.MAX_ROWS), np.float32)
+        O.set_row_gap_out(gp)
+        try:
+            o = O.physics_step(he_model, sp, root, dof, tg, 1, cache=cache)
+        finally:
+            O.set_row_gap_out(None)
+        com_v.append(float(np.linalg.norm(cases.com_velocity(model, o["rb_state"])[0])))
+        n, keys, lam = _abi.cache_rows(cache)
+        step_rows = {}
+        for r in range(int(n[0])):
+            b0, b1, sub, kind = _abi.key_fields(keys[0, r])
+            if kind == 0:
+                step_rows[(names(b0), names(b1))] = (float(lam[0, r]), float(gp[0, r]))
+        rows.append(step_rows)
+    assert abs(float(np.linalg.norm(root[0, 7:10])) - float(np.linalg.norm(r2[0, 7:10]))) < 1e-3
+    jump = int(np.argmax(np.diff([0.0] + com_v)))
+    assert com_v[jump] > 10.0 and (jump == 0 or com_v[jump - 1] < 3.0), com_v
+    for s in range(jump + 1):
+        for pair in (("R_Hip", "R_Elbow"), ("R_Hip", "R_Wrist")):
+            lam, gap = rows[s][pair]
+            assert gap < -0.05 and lam > 800.0, (s, pair, lam, gap)
+    lam_w, gap_w = rows[jump][("R_Wrist", "terrain")]
+    assert lam_w > 500.0, rows[jump]
+    # dt/4 from 6 steps before the peak: no launch
+    sp4 = _abi.default_sim_params(substeps=8)
+    r4, d4 = d["root"][0][None].copy(), d["dof"][0][None].copy()
+    c4 = O.new_cache(1)
+    vmax4 = 0.0
+    for k in range(i + 3):
+        O.physics_step(he_model, sp4, r4, d4, d["targets"][k][None].copy(), 2, cache=c4)
+        vmax4 = max(vmax4, float(np.linalg.norm(r4[0, 7:10])))
+    assert vmax4 < 5.0, vmax4
