@@ -88,67 +88,10 @@ struct Lds {
     BodyTopo T;
 };
 
-// wave priority over the serial chains (PGS rows, the elimination, the L^-T sweep) against the
-// partner wave's throughput phases (diagnostic knobs, s_setprio 0..3)
-#ifndef HE_PRIO_PGS
-#define HE_PRIO_PGS 3
-#endif
-#ifndef HE_PRIO_FACTOR
-#define HE_PRIO_FACTOR 3
-#endif
-#ifndef HE_DELASSUS48
-#define HE_DELASSUS48 1
-#endif
-#ifndef HE_PGS_PACKED_BOUNDS  // a PGS row's two bound updates as one packed FMA (1) or two FMAs (0)
-#define HE_PGS_PACKED_BOUNDS 1
-#endif
-#ifndef HE_PGS_FORM  // packed PGS sweep form: 3 = branch-free up to the row-count class (32/48/63;
-// +0.65 % physics A/B, bit-identical), 0 = a row-count branch per row, 1 = rows in pairs, 2 = rows in
-// DPP quads (1 and 2: bit-identical, -0.3 % and -0.9 %; profiles/r03/ab_pgs_form.txt)
-#define HE_PGS_FORM 3
-#endif
-#ifndef HE_WCLAMP_BOUND  // skip the world angular-velocity prefix when a norm bound rules the clamp out
-#define HE_WCLAMP_BOUND 1  // -1.1 % standstill physics launch A/B, configs[2] neutral; bit-identical
-#endif
-#ifndef HE_PGS_STRIDE  // branch-free sweep: a row-count exit every HE_PGS_STRIDE rows (0: none)
-#define HE_PGS_STRIDE 4  // -0.7 % standstill, -1.4 % configs[2] physics launch A/B (8: neutral), bit-identical
-#endif
-#ifndef HE_PGS_CLASS_PREP  // scale the columns and form the packed bound weights for the row class only
-#define HE_PGS_CLASS_PREP 1  // -0.2..-0.4 % physics launch A/B on all three configs, bit-identical
-#endif
-#ifndef HE_PGS_MIN_CLASS  // smallest row-count class of the branch-free sweep (8, 16 or 32)
-#define HE_PGS_MIN_CLASS 16  // +1.3 % configs[2], +1.5 % configs[4] physics A/B (8: less); ab_pgs_form.txt
-#endif
-#ifndef HE_PGS_OPAQUE_MASK  // PGS bound weights formed per row (1) or hoisted by the compiler (0)
-#define HE_PGS_OPAQUE_MASK 0
-#endif
-#ifndef HE_PRED_LEVELS  // the midpoint bias's subtree sums by body levels (1) or per dof lane (0)
-#define HE_PRED_LEVELS 1
-#endif
-#ifndef HE_PRED_LT_GROUPS  // the midpoint bias's L^-T pass: in groups of independent pivots with the row loads
-#define HE_PRED_LT_GROUPS 2  // one group ahead (2), in groups (1), one pivot at a time (0): 2 is +4.3 % (r03 A/B)
-#endif
-#ifndef HE_PRED_JUMP  // the midpoint bias's velocities / accelerations by pointer jumping (1) or chain walks (0)
-#define HE_PRED_JUMP 1
-#endif
-#ifndef HE_BIAS_PREDICTOR  // 0: the midpoint bias compiled out (diagnostic A/B of its code's cost when off)
-#define HE_BIAS_PREDICTOR 1
-#endif
-#ifndef HE_FAC_PIPE
-#define HE_FAC_PIPE 1
-#endif
-#ifndef HE_JT_MFMA
-#define HE_JT_MFMA 1
-#endif
-#ifndef HE_CRBA_MFMA
-#define HE_CRBA_MFMA 1
-#endif
-#ifndef HE_PRIO_SOLVE
-#define HE_PRIO_SOLVE 0
-#endif
-#ifndef HE_PRIO_KIN
-#define HE_PRIO_KIN 0
-#endif
+// wave priority: s_setprio 3 over the serial chains (PGS rows, the elimination, the L^-T sweeps)
+// against the partner wave's throughput phases (+2.8 % A/B, r01), 0 elsewhere
+constexpr int kPrioSerial = 3;
+constexpr int kPrioDefault = 0;
 
 // wave-level ordering point: one wave per workgroup, LDS executes its instructions in order, so
 // only the compiler must not move memory operations across phase boundaries
@@ -389,8 +332,6 @@ HE_DEV const T* opaque(const T* p) {  // same address through an opaque offset: 
     asm volatile("" : "+v"(off));
     return reinterpret_cast<const T*>(reinterpret_cast<const char*>(p) + off);
 }
-HE_DEV void fmul_ordered(float& z, float a) { asm volatile("v_mul_f32 %0, %0, %1" : "+v"(z) : "v"(a)); }
-HE_DEV void ffma_ordered(float& acc, float a, float b) { asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "v"(a), "v"(b)); }
 
 // Delassus operator on the matrix cores: A = Zh Zh^T as four 32x32 tiles of
 // v_mfma_f32_32x32x2_f32 (exact f32, k-ordered fma chain), K = live dofs two at a time. Lane r
@@ -584,145 +525,20 @@ HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uin
     }
 }
 
-// one Gauss-Seidel sweep over the solver rows (patch friction, oracle build_rows), in delta form.
-// Lane r holds cd_r = -w_r / A[r][r] (the unconstrained impulse change of row r), its bounds on the
-// change [lo_r, hi_r] and the negated scaled Delassus column acolp[R] = -A[R][r] / A[r][r]: a normal
-// row [-lambda_r, +inf), a friction row the bound B_r = muw_r x (its patch's normal impulses) shifted
-// by its own impulse, [-B_r - lambda_r, B_r - lambda_r] (lambda as of the sweep's start). Row R's
-// change is its clamp, so the dependent chain per row is med3 -> v_readlane -> fma: the change d goes
-// to every lane's cd += acolp[R] d and into lane R of dvec; lambda += dvec once per sweep. When R is
-// a normal row of lane r's patch (bit R of the lane's patch mask), lane r's bounds widen by muw_r d
-// right away -- the patch's normal rows come before its friction rows, so a friction row sees this
-// sweep's normal impulses (Gauss-Seidel, as the oracle's bound from the current impulses).
-// Packed form (HE_PGS_PACKED_BOUNDS): lane r holds the pair (acolp[R], kk_R) per row -- kk_R = muw_r
-// where R is a normal row of its patch, else 0 -- and its (cd, hi) pair, so that a row's change goes
-// to cd and hi in one v_pk_fma_f32 (lo: one FMA with the pair's weight negated). Five VALU per row.
-template <int R>
-HE_DEV void pgs_sweep_pk(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
-    if constexpr (R < MAXR) {
-        if (R >= nr) return;
-        const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
-        ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
-        lo = fmaf(-ak[R].y, d, lo);
-        dvec = regla::wrlane<R>(d, dvec);
-        pgs_sweep_pk<R + 1>(ch, dvec, lo, ak, nr);
-    }
-}
-// Branch-free form (HE_PGS_FORM 3): every row up to a compile-time class bound N (32, 48, 63) by
-// the row count, with no per-row row-count branch; rows nr..N-1 are empty rows (zero columns and
+// One Gauss-Seidel sweep, branch-free: every row up to a compile-time class bound N (16, 32, 48,
+// 63) by the row count, with no per-row row-count branch (a row-count exit every 4 rows); rows nr..N-1 are empty rows (zero columns and
 // bound weights in every lane, zero cd and bounds in their own lanes: a +-0 change).
 template <int R, int N>
 HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
     if constexpr (R < N) {
-#if HE_PGS_STRIDE
-        if constexpr (R > 0 && R % HE_PGS_STRIDE == 0) {  // a row-count exit every HE_PGS_STRIDE rows
+        if constexpr (R > 0 && R % 4 == 0) {  // a row-count exit every 4 rows
             if (R >= nr) return;
         }
-#endif
         const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
         ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
         lo = fmaf(-ak[R].y, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
         pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr);
-    }
-}
-// Paired form (HE_PGS_FORM): rows R, R+1 (R even) per step. Lane R+1 takes row R's change from
-// its neighbour by DPP (row_shr:1 -- R+1 is odd, so never the first lane of a DPP row) and applies
-// it to its own (cd, hi) and lo exactly as the full-wave update would (the same FMAs on the same
-// operands), so its clamp is row R+1's Gauss-Seidel change bit for bit; the two v_readlane
-// broadcasts then update every lane in row order. One readlane -> FMA link per two rows leaves the
-// dependent chain: med3 -> dpp -> pk_fma -> med3 -> readlane -> pk_fma.
-template <int R>
-HE_DEV void pgs_sweep_pk2(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
-    if constexpr (R < MAXR) {
-        if (R >= nr) return;
-        if constexpr (R + 1 < MAXR) {
-            // row R + 1 == nr is an empty row (its column and bound weights are 0 in every lane, its
-            // own cd and bounds 0): its change is +-0 and leaves every lane's values as they were
-            const float x1 = __builtin_amdgcn_fmed3f(ch.x, lo, ch.y);
-            const float t = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x1), 0x111, 0xf, 0xf, true));
-            const regla::f2v c2 = __builtin_elementwise_fma(ak[R], regla::f2v{t, t}, ch);
-            const float lo2 = fmaf(-ak[R].y, t, lo);
-            const float d0 = regla::rdlane(x1, R);
-            const float d1 = regla::rdlane(__builtin_amdgcn_fmed3f(c2.x, lo2, c2.y), R + 1);
-            ch = __builtin_elementwise_fma(ak[R], regla::f2v{d0, d0}, ch);
-            lo = fmaf(-ak[R].y, d0, lo);
-            ch = __builtin_elementwise_fma(ak[R + 1], regla::f2v{d1, d1}, ch);
-            lo = fmaf(-ak[R + 1].y, d1, lo);
-            dvec = regla::wrlane<R>(d0, dvec);
-            dvec = regla::wrlane<R + 1>(d1, dvec);
-            asm volatile("" : "+v"(lo));  // the bound chain in this block, not sunk past the row-count branch
-            pgs_sweep_pk2<R + 2>(ch, dvec, lo, ak, nr);
-        } else {
-            const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
-            ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
-            lo = fmaf(-ak[R].y, d, lo);
-            dvec = regla::wrlane<R>(d, dvec);
-        }
-    }
-}
-// Quad form (HE_PGS_FORM 2): rows R..R+3 (R % 4 == 0) per step, Gauss-Seidel inside the DPP quad
-// of lanes R..R+3 (each change broadcast to the quad by quad_perm, applied to a local copy with the
-// full-wave FMAs' operands), then four readlane broadcasts update every lane in row order. Lanes
-// outside the quad compute garbage local copies that are discarded.
-template <int K>
-HE_DEV float quad_bcast(float x) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), K * 0x55, 0xf, 0xf, false));
-}
-template <int R>
-HE_DEV void pgs_sweep_pk4(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
-    if constexpr (R < MAXR) {
-        if (R >= nr) return;
-        if constexpr (R + 3 < MAXR) {
-            // rows R + k >= nr are empty rows (zero columns and bound weights, zero cd and bounds)
-            const float x0 = __builtin_amdgcn_fmed3f(ch.x, lo, ch.y);
-            const float t0 = quad_bcast<0>(x0);
-            const regla::f2v c1 = __builtin_elementwise_fma(ak[R], regla::f2v{t0, t0}, ch);
-            const float l1 = fmaf(-ak[R].y, t0, lo);
-            const float x1 = __builtin_amdgcn_fmed3f(c1.x, l1, c1.y);
-            const float t1 = quad_bcast<1>(x1);
-            const regla::f2v c2 = __builtin_elementwise_fma(ak[R + 1], regla::f2v{t1, t1}, c1);
-            const float l2 = fmaf(-ak[R + 1].y, t1, l1);
-            const float x2 = __builtin_amdgcn_fmed3f(c2.x, l2, c2.y);
-            const float t2 = quad_bcast<2>(x2);
-            const regla::f2v c3 = __builtin_elementwise_fma(ak[R + 2], regla::f2v{t2, t2}, c2);
-            const float l3 = fmaf(-ak[R + 2].y, t2, l2);
-            const float x3 = __builtin_amdgcn_fmed3f(c3.x, l3, c3.y);
-            const float d0 = regla::rdlane(x0, R), d1 = regla::rdlane(x1, R + 1);
-            const float d2 = regla::rdlane(x2, R + 2), d3 = regla::rdlane(x3, R + 3);
-            ch = __builtin_elementwise_fma(ak[R], regla::f2v{d0, d0}, ch);
-            lo = fmaf(-ak[R].y, d0, lo);
-            ch = __builtin_elementwise_fma(ak[R + 1], regla::f2v{d1, d1}, ch);
-            lo = fmaf(-ak[R + 1].y, d1, lo);
-            ch = __builtin_elementwise_fma(ak[R + 2], regla::f2v{d2, d2}, ch);
-            lo = fmaf(-ak[R + 2].y, d2, lo);
-            ch = __builtin_elementwise_fma(ak[R + 3], regla::f2v{d3, d3}, ch);
-            lo = fmaf(-ak[R + 3].y, d3, lo);
-            dvec = regla::wrlane<R>(d0, dvec);
-            dvec = regla::wrlane<R + 1>(d1, dvec);
-            dvec = regla::wrlane<R + 2>(d2, dvec);
-            dvec = regla::wrlane<R + 3>(d3, dvec);
-            asm volatile("" : "+v"(lo));  // the bound chain in this block, not sunk past the row-count branch
-            pgs_sweep_pk4<R + 4>(ch, dvec, lo, ak, nr);
-        } else {
-            pgs_sweep_pk2<R>(ch, dvec, lo, ak, nr);
-        }
-    }
-}
-template <int R>
-HE_DEV void pgs_sweep(float& cd, float& dvec, float& lo, float& hi, const float (&acolp)[MAXR], uint32_t mlo,
-                      uint32_t mhi, float muw, int nr) {
-    if constexpr (R < MAXR) {
-        if (R >= nr) return;
-        const float d = regla::rdlane(__builtin_amdgcn_fmed3f(cd, lo, hi), R);
-        cd = fmaf(acolp[R], d, cd);
-        dvec = regla::wrlane<R>(d, dvec);
-        // muw where bit R of the patch mask is set, else 0: a sign-extended bit field as an AND mask
-        const int sel = __builtin_amdgcn_sbfe((int)(R < 32 ? mlo : mhi), R & 31, 1);
-        const float kk = __int_as_float(sel & __float_as_int(muw));
-        hi = fmaf(kk, d, hi);
-        lo = fmaf(-kk, d, lo);
-        pgs_sweep<R + 1>(cd, dvec, lo, hi, acolp, mlo, mhi, muw, nr);
     }
 }
 
@@ -869,28 +685,6 @@ HE_DEV void crba_row(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[
     }
 }
 
-// CRBA straight into registers, four rows per group, software-pipelined: the LDS reads of group
-// G+1 are issued (behind an opaque base) before group G is computed from registers
-template <int G>
-HE_DEV void crba_groups(regla::RegMat& M, const float (&Sj)[6], const float (&Sj2)[6], float dadd, float dadd2,
-                        const Lds& L, const float (&cur)[4][6]) {
-    if constexpr (4 * G < NG) {
-        float nxt[4][6];
-        if constexpr (4 * (G + 1) < NG) {
-            const Lds& Lg = *opaque(&L);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (4 * (G + 1) + k < NG)
-                    for (int x = 0; x < 6; ++x) nxt[k][x] = Lg.IS[4 * (G + 1) + k < NG ? 4 * (G + 1) + k : 0][x];
-        }
-        crba_row<4 * G>(M, Sj, Sj2, dadd, dadd2, cur[0]);
-        if constexpr (4 * G + 1 < NG) crba_row<4 * G + 1>(M, Sj, Sj2, dadd, dadd2, cur[1]);
-        if constexpr (4 * G + 2 < NG) crba_row<4 * G + 2>(M, Sj, Sj2, dadd, dadd2, cur[2]);
-        if constexpr (4 * G + 3 < NG) crba_row<4 * G + 3>(M, Sj, Sj2, dadd, dadd2, cur[3]);
-        crba_groups<G + 1>(M, Sj, Sj2, dadd, dadd2, L, nxt);
-    }
-}
-
 // CRBA on the matrix cores: H = IS^T S as v_mfma_f32_32x32x2_f32 tiles (rows i, columns j, K = the
 // six spatial components in three steps), lower block triangle only: 6 tiles, 18 MFMAs. Operands
 // come straight from LDS (lane l: IS_{32R + l%32}[2s + l/32] and S_{32C + l%32}[2s + l/32]). One
@@ -907,31 +701,20 @@ HE_DEV void crba_tile_rows(regla::RegMat& M, const f32x16& ta, const f32x16& tb)
         if (r + 4 < NG) M.cp[(r + 4 < NG ? r + 4 : 0) >> 1][(r + 4) & 1] = b;
     }
 }
-// HE_CRBA_NOMASK: entries off the ancestor chains are left as the dense product. The elimination
+// Entries off the ancestor chains are left as the dense product. The elimination
 // reads only chain entries (an update of row I on lane j uses row K on lane j, and j in chain(I),
 // I in chain(K) gives j in chain(K)), stores only chain lanes, and the pivots are diagonal, so
 // those entries never reach L, D or the right-hand side; only the diagonal addends remain.
-#ifndef HE_CRBA_NOMASK
-#define HE_CRBA_NOMASK 1
-#endif
 template <int I>
 HE_DEV void crba_mask_rows(regla::RegMat& M, float dadd, float dadd2) {
     using namespace regla;
     if constexpr (I < NG) {
-#if HE_CRBA_NOMASK
         float h = mc<I>(M);
-#else
-        float h = lanes<smpl::kAncLo[I]>() ? mc<I>(M) : 0.f;
-#endif
         if constexpr (I < 64) h = lanes<1ull << I>() ? h + dadd : h;  // armature + implicit drive
         asm volatile("" : "+v"(h));
         mc_set<I>(M, h);
         if constexpr (I >= 64) {
-#if HE_CRBA_NOMASK
             float h2 = mc2<I - 64>(M);
-#else
-            float h2 = lanes<(uint64_t)smpl::kAncHi[I]>() ? mc2<I - 64>(M) : 0.f;
-#endif
             h2 = lanes<1ull << (I - 64)>() ? h2 + dadd2 : h2;
             asm volatile("" : "+v"(h2));
             mc2_set<I - 64>(M, h2);
@@ -990,28 +773,6 @@ HE_DEV void crba_mfma(regla::RegMat& M, const Lds& L, int lane, float dadd, floa
     crba_mask_rows<0>(M, dadd, dadd2);
 }
 
-// In-place subtree sums X[b] += sum over children of X[c], parents of the deepest level first: at
-// each level, lane (parent, component) pulls its (at most three) children's finished sums. The
-// levels are unrolled at compile time, so parents and children are immediates selected by lane
-// range. NC = 16 sums forces (6, stride 6) and inertias (10, stride 10) together; NC = 6 forces only.
-template <int NC, int J, int END>
-HE_DEV void subtree_parent(float* F, float* I, int lane, int j0) {
-    if constexpr (J < END) {
-        constexpr int p = smpl::kParentLevelBodies[J];
-        const int base = (J - j0) * NC;
-        if (lane >= base && lane < base + NC) {
-            const int x = lane - base;
-            float* X = x < 6 ? F : I;
-            const int st = x < 6 ? 6 : 10, xx = x < 6 ? x : x - 6;
-            float v = X[p * st + xx];
-            if constexpr (smpl::kChildren[p][0] >= 0) v += X[smpl::kChildren[p][0] * st + xx];
-            if constexpr (smpl::kChildren[p][1] >= 0) v += X[smpl::kChildren[p][1] * st + xx];
-            if constexpr (smpl::kChildren[p][2] >= 0) v += X[smpl::kChildren[p][2] * st + xx];
-            X[p * st + xx] = v;
-        }
-        subtree_parent<NC, J + 1, END>(F, I, lane, j0);
-    }
-}
 // one level with every parent at once: lane (group g = lane / NC, component x) takes its parent and
 // children from compile-time selects, reads them (a missing child reads the parent and adds 0:
 // the sum order of subtree_parent, bit-identical) and writes back; no exec-mask branch per parent
@@ -1045,19 +806,12 @@ HE_DEV void subtree_level_flat(float* F, float* I, int lane) {
         X[p * st + xx] = v;
     }
 }
-#ifndef HE_SUBTREE_FLAT
-#define HE_SUBTREE_FLAT 1
-#endif
 template <int NC, int D>
 HE_DEV void subtree_levels(float* F, float* I, int lane) {
     if constexpr (D >= 0) {
         constexpr int j0 = smpl::kParentLevelStart[D], j1 = smpl::kParentLevelStart[D + 1];
         if constexpr (j1 > j0) {
-#if HE_SUBTREE_FLAT
             subtree_level_flat<NC, D>(F, I, lane);
-#else
-            subtree_parent<NC, j0, j1>(F, I, lane, j0);
-#endif
             sync();
         }
         subtree_levels<NC, D - 1>(F, I, lane);
@@ -1066,31 +820,19 @@ HE_DEV void subtree_levels(float* F, float* I, int lane) {
 
 // ---------------------------------------------------------------------------------- kinematics
 // 2^k-th ancestor of every body (-1: none), for pointer jumping over the body tree
-#ifndef HE_DOF_FLAT  // bias / IS / drive terms for lane = dof without the dof loop and root branch
-#define HE_DOF_FLAT 1
-#endif
-#ifndef HE_KIN_AXES_FLAT  // joint axes S for lane = dof without the dof loop and root branch
-#define HE_KIN_AXES_FLAT 1
-#endif
-#ifndef HE_KIN_QCACHE  // later substeps start from the integrated local rotations instead of exp(log(.))
-#define HE_KIN_QCACHE 1
-#endif
-#ifndef HE_KIN_ROOTREL  // chains relative to the root: three jumping rounds, root frame applied last
-#define HE_KIN_ROOTREL 1
-#endif
 struct JumpTable {
     int j[4][NB];
     constexpr JumpTable() : j() {
         for (int b = 0; b < NB; ++b)
-            j[0][b] = HE_KIN_ROOTREL && smpl::kParentBody[b] == 0 ? -1 : smpl::kParentBody[b];
+            j[0][b] = smpl::kParentBody[b] == 0 ? -1 : smpl::kParentBody[b];  // stops below the root
         for (int k = 1; k < 4; ++k)
             for (int b = 0; b < NB; ++b) j[k][b] = j[k - 1][b] < 0 ? -1 : j[k - 1][j[k - 1][b]];
     }
 };
 constexpr JumpTable kJumpT{};
 static_assert(smpl::kNumBodyLevels <= 16, "four pointer-jumping rounds cover chains of 16 bodies");
-static_assert(!HE_KIN_ROOTREL || smpl::kNumBodyLevels - 1 <= 8, "three rounds cover the root's subtrees of depth 8");
-constexpr int kKinRounds = HE_KIN_ROOTREL ? 3 : 4;
+static_assert(smpl::kNumBodyLevels - 1 <= 8, "three rounds cover the root's subtrees of depth 8");
+constexpr int kKinRounds = 3;
 
 struct Jump4 {  // the four jump targets of each body packed as bytes (LDS table BodyTopo::jump4)
     uint32_t v[NB];
@@ -1108,7 +850,7 @@ HE_DEV int jump_of(uint32_t jp) {  // byte K of the lane's packed entry, sign-ex
 // World poses and spatial velocities, lane = body, by pointer jumping: X_b <- X_{J_k(b)} o X_b and
 // V_b <- V_b + V_{J_k(b)} with J_k the 2^k-th ancestor, four rounds for chains of up to 16 bodies
 // (log depth instead of a chain walk per body). X = (q, p): (qa, pa) o (qb, pb) = (qa qb, pa + Ra pb).
-// HE_KIN_ROOTREL: the table stops below the root, so three rounds compose each chain in the root's
+// The table stops below the root, so three rounds compose each chain in the root's
 // frame (SMPL subtrees are 8 deep) and the root's pose / velocity / base acceleration, uniform LDS
 // reads, are applied once at the end -- one dependent ds_bpermute round fewer per prefix.
 // Joint axes S (lane = dof) follow from the world poses.
@@ -1129,7 +871,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         u[0] = L.u0[0]; u[1] = L.u0[1]; u[2] = L.u0[2];
     } else {
         const int d = 3 * (b - 1);
-        if (HE_KIN_QCACHE && cached) {  // the previous substep's integrated rotation (pre-log)
+        if (cached) {  // the previous substep's integrated rotation (pre-log)
             q = f4{L.qloc[b][0], L.qloc[b][1], L.qloc[b][2], L.qloc[b][3]};
         } else {
             q = pqexp(f3{L.q[d], L.q[d + 1], L.q[d + 2]});
@@ -1153,7 +895,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     jump(std::integral_constant<int, 1>{});
     jump(std::integral_constant<int, 2>{});
     if constexpr (kKinRounds == 4) jump(std::integral_constant<int, 3>{});
-    if (HE_KIN_ROOTREL && b != 0) {  // root-frame pose of the chain -> world axes, origin about o
+    if (b != 0) {  // root-frame pose of the chain -> world axes, origin about o
         p = qapply(qr, p);
         q = qmul(qr, q);
     }
@@ -1184,7 +926,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     vjump(std::integral_constant<int, 1>{});
     vjump(std::integral_constant<int, 2>{});
     if constexpr (kKinRounds == 4) vjump(std::integral_constant<int, 3>{});
-    if (HE_KIN_ROOTREL && b != 0) {  // plus the root's own velocity
+    if (b != 0) {  // plus the root's own velocity
 #pragma unroll
         for (int x = 0; x < 6; ++x) V[x] += L.u0[x];
     }
@@ -1221,7 +963,7 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
         ajump(std::integral_constant<int, 1>{});
         ajump(std::integral_constant<int, 2>{});
         if constexpr (kKinRounds == 4) ajump(std::integral_constant<int, 3>{});
-        if (HE_KIN_ROOTREL && b != 0) {  // plus the base acceleration
+        if (b != 0) {  // plus the base acceleration
 #pragma unroll
             for (int x = 0; x < 6; ++x) A[x] += A0[x];
         }
@@ -1229,7 +971,6 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
             for (int x = 0; x < 6; ++x) L.Acc[b][x] = A[x];
     }
     sync();
-#if HE_KIN_AXES_FLAT
     // lane = dof: dofs 0..63 with the root's six unit axes selected in, then dofs 64..74 (ball
     // joints only); no loop and no root branch
     auto axis = [&](int i, bool may_root) {
@@ -1248,46 +989,14 @@ HE_DEV void kinematics(Lds& L, const he_model& m, int lane, const he_sim_params&
     axis(lane, true);
     static_assert(NG - W <= W && NG - W > 0, "a second set of lanes covers dofs 64..NG-1");
     if (lane < NG - W) axis(W + lane, false);
-#else
-    for (int i = lane; i < NG; i += W) {
-        float* S = L.S[i];
-        if (i < 6) {
-            for (int c = 0; c < 6; ++c) S[c] = (c == i) ? 1.f : 0.f;
-        } else {
-            int bb = dof_body(i), c = (i - 6) % 3;
-            f4 qb = f4{L.qw[bb][0], L.qw[bb][1], L.qw[bb][2], L.qw[bb][3]};
-            f3 e = c == 0 ? f3{1.f, 0.f, 0.f} : (c == 1 ? f3{0.f, 1.f, 0.f} : f3{0.f, 0.f, 1.f});
-            f3 ax = qapply(qb, e);
-            f3 l = cross3(f3{L.pw[bb][0], L.pw[bb][1], L.pw[bb][2]}, ax);
-            S[0] = ax.x; S[1] = ax.y; S[2] = ax.z; S[3] = l.x; S[4] = l.y; S[5] = l.z;
-        }
-    }
-#endif
     sync();
 }
 
-__device__ const regla::ChainBytes kChainBytesDev{};
-#ifndef HE_LSOLVE_GATHER  // ds_bpermute gathers per level: no gain over the readlane picks (A/B r01)
-#define HE_LSOLVE_GATHER 0
-#endif
 // y <- L^-1 y for the lane's rows (see regla::solve_L_rows / solve_L_gather)
 HE_DEV void solve_L(const float (&r1)[regla::kRowRegs], const float (&r2)[regla::kRowRegs], int lane, float& yl,
                     float& y2) {
-#if HE_LSOLVE_GATHER
-    uint32_t c1[8], c2[8];
-    const uint4* w1 = reinterpret_cast<const uint4*>(kChainBytesDev.w[lane]);
-    const uint4* w2 = reinterpret_cast<const uint4*>(kChainBytesDev.w[lane < regla::NH ? 64 + lane : 0]);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint4 a = w1[q], b = w2[q];
-        c1[4 * q] = a.x; c1[4 * q + 1] = a.y; c1[4 * q + 2] = a.z; c1[4 * q + 3] = a.w;
-        c2[4 * q] = b.x; c2[4 * q + 1] = b.y; c2[4 * q + 2] = b.z; c2[4 * q + 3] = b.w;
-    }
-    regla::solve_L_gather<0>(r1, r2, c1, c2, yl, y2);
-#else
     (void)lane;
     regla::solve_L_rows<0>(r1, r2, yl, y2);
-#endif
 }
 
 // lane i's packed row of L (dof i) and the row of dof 64 + i (lanes >= NH read row 64 and never
@@ -1312,31 +1021,17 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // with the factor in Lp and the first bias's subtree forces in F. Scratch: uf (holds um), V (the
 // final kinematics rewrites it), Acc (the contact phase's scratch after), Ib (own inertias, stored
 // by the force pass).
-#ifndef HE_PRED_NOINLINE  // diagnostic: the predictor as a called function (its own register allocation)
-#define HE_PRED_NOINLINE 0
-#endif
-#if HE_PRED_NOINLINE
-#define HE_PRED_FN __device__ __attribute__((noinline))
-#else
-#define HE_PRED_FN HE_DEV
-#endif
 // yh += D^-1/2 L^-T dc (lane = dof, then dofs 64..74 on lanes 0..10): the midpoint correction's
 // forward substitution replayed from the stored factor
 HE_DEV void mid_lt(Lds& L, const BodyTopo& T, int lane, float c1, float c2) {
     using regla::NH;
-#if HE_PRED_LT_GROUPS == 2
     regla::solve_LT_vec_pipelined(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
-#elif HE_PRED_LT_GROUPS
-    regla::solve_LT_vec_groups<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
-#else
-    regla::solve_LT_vec<0>(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
-#endif
     L.yh[lane] += c1 * L.sDinv[lane];
     if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
     sync();
 }
 
-HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, unsigned long long* stamps,
+HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, unsigned long long* stamps,
                                unsigned long long& t_prev) {
     (void)stamps; (void)t_prev;
     using namespace regla;
@@ -1354,7 +1049,6 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
     STAMP(25);
     const bool bl = lane < NB;
     const int b = bl ? lane : 0;
-#if HE_PRED_JUMP
     // velocities and bias accelerations at um by pointer jumping over the chain, as the kinematics
     // does at u0 (the jump table stops below the root; the root's velocity and base acceleration are
     // added once at the end): no LDS chain walks
@@ -1390,7 +1084,7 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
         };
         prefix6(V);
         const float um6[6] = {L.uf[0], L.uf[1], L.uf[2], L.uf[3], L.uf[4], L.uf[5]};
-        if (HE_KIN_ROOTREL && b != 0)
+        if (b != 0)
             for (int x = 0; x < 6; ++x) V[x] += um6[x];
         const f3 vxw = cross3(f3{um6[3], um6[4], um6[5]}, f3{um6[0], um6[1], um6[2]});
         const float A0[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
@@ -1401,7 +1095,7 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
             crm(V, vj, A);  // joint b's velocity-product term V_b x S_b um_b
         }
         prefix6(A);
-        if (HE_KIN_ROOTREL && b != 0)
+        if (b != 0)
             for (int x = 0; x < 6; ++x) A[x] += A0[x];
         float IA[6], IV[6], X[6];
         si_apply(L.Ib[b], A, IA);
@@ -1409,51 +1103,11 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
         crf(V, IV, X);
         for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
     }
-#else
-    if (bl) {  // joint velocities S_b uf_b (the root's S are the unit axes) -> Acc
-        float vj[6];
-        if (b == 0) {
-            for (int x = 0; x < 6; ++x) vj[x] = L.uf[x];
-        } else {
-            const int d0 = T.dof0[b];
-            for (int x = 0; x < 6; ++x)
-                vj[x] = L.S[d0][x] * L.uf[d0] + L.S[d0 + 1][x] * L.uf[d0 + 1] + L.S[d0 + 2][x] * L.uf[d0 + 2];
-        }
-        for (int x = 0; x < 6; ++x) L.Acc[b][x] = vj[x];
-    }
-    sync();
-    float V[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (bl) {  // body velocities: the chain's joint velocities summed, root first
-        for (int k = 0; k <= T.depth[b]; ++k) {
-            const int a = T.chain[b][k];
-            for (int x = 0; x < 6; ++x) V[x] += L.Acc[a][x];
-        }
-        for (int x = 0; x < 6; ++x) L.V[b][x] = V[x];
-    }
-    sync();
-    float Fb[6];
-    if (bl) {  // RNEA body force at um: a_b = a_0 + sum over the chain (root excluded) of V_a x S_a uf_a
-        const f3 vxw = cross3(f3{L.uf[3], L.uf[4], L.uf[5]}, f3{L.uf[0], L.uf[1], L.uf[2]});
-        float A[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
-        for (int k = 1; k <= T.depth[b]; ++k) {
-            const int a = T.chain[b][k];
-            float cr[6];
-            crm(L.V[a], L.Acc[a], cr);
-            for (int x = 0; x < 6; ++x) A[x] += cr[x];
-        }
-        float IA[6], IV[6], X[6];
-        si_apply(L.Ib[b], A, IA);
-        si_apply(L.Ib[b], V, IV);
-        crf(V, IV, X);
-        for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
-    }
-#endif
     sync();
     if (bl)
         for (int x = 0; x < 6; ++x) L.Acc[b][x] = Fb[x];
     sync();
     STAMP(26);
-#if HE_PRED_LEVELS
     // subtree sums of the new body forces, in place by body levels (as the first bias's): +4.8 %
     // against the per-dof-lane sums below (r03 A/B, profiles/r03/ab_pred_levels.txt, under the
     // two-wave bound that lets it fit)
@@ -1462,19 +1116,6 @@ HE_PRED_FN void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_
         const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
         return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], L.Acc[bi]));
     };
-#else
-    // lane = dof (then dofs 64..74 on lanes 0..10): dc_i = dt (S_i . F_b(u0) - S_i . F_b(um)) with the
-    // subtree sums of the new body forces, 24 masked body reads per lane
-    auto corr = [&](int i) {
-        const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
-        const uint32_t sm = T.sub_mask[bi];
-        float fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int d = 0; d < NB; ++d)
-            if ((sm >> d) & 1u)
-                for (int x = 0; x < 6; ++x) fs[x] += L.Acc[d][x];
-        return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], fs));
-    };
-#endif
     float c1 = corr(lane);
     float c2 = lane < NH ? corr(64 + lane) : 0.f;
     STAMP(27);
@@ -1534,9 +1175,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     const BodyTopo& T = L.T;
     const he_sim_params& p = a.p;
     const float dt = p.dt;
-    __builtin_amdgcn_s_setprio(HE_PRIO_KIN);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
     kinematics<true>(L, m, lane, a.p, !first);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
     STAMP(0);
     // ---- body spatial inertias about o + RNEA body forces (gravity as base acceleration)
     if (lane < NB) {
@@ -1564,7 +1205,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float* o10 = L.Ic[b];  // own inertia; the subtree sums accumulate in place
         o10[0] = mass; o10[1] = mass * s.x; o10[2] = mass * s.y; o10[3] = mass * s.z;
         o10[4] = I[0][0]; o10[5] = I[1][1]; o10[6] = I[2][2]; o10[7] = I[0][1]; o10[8] = I[0][2]; o10[9] = I[1][2];
-        if (HE_BIAS_PREDICTOR && p.bias_midpoint)  // the body's own inertia for the midpoint's second RNEA (Ib is free until
+        if (p.bias_midpoint)  // the body's own inertia for the midpoint's second RNEA (Ib is free until
             for (int x = 0; x < 10; ++x) L.Ib[b][x] = o10[x];  // the contact phase's segments)
         float IA[6], IV[6], X[6];
         si_apply(o10, L.Acc[b], IA);
@@ -1575,13 +1216,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     sync();
     STAMP(1);
     // ---- subtree sums: F_b (forces) and composite inertias, in place by body levels
-    __builtin_amdgcn_s_setprio(HE_PRIO_KIN);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
     subtree_levels<16, smpl::kNumBodyLevels - 2>(&L.F[0][0], &L.Ic[0][0], lane);
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
     STAMP(2);
     // ---- bias forces, IS_i = Ic S_i, drives
     const uint32_t limmask = p.joint_limits ? (uint32_t)__builtin_amdgcn_readfirstlane((int)L.limmask) : 0u;
-#if HE_DOF_FLAT
     // lane = dof (then dofs 64..74 on lanes 0..10), the root's six dofs selected out: no loop,
     // no root branch, saturation by selects
     auto dof_terms = [&](int i, bool may_root) {
@@ -1613,34 +1253,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     };
     dof_terms(lane, true);
     if (lane < NG - W) dof_terms(W + lane, false);
-#else
-    for (int i = lane; i < NG; i += W) {
-        int b = dof_body(i);
-        float bias = dot6(L.S[i], L.F[b]);
-        si_apply(L.Ic[b], L.S[i], L.IS[i]);
-        float rhs = -bias, cf = 0.f;
-        if (i >= 6) {
-            int d = i - 6;
-            float kp = m.stiffness[d] * p.kp_scale, kd = m.damping[d] * p.kd_scale;
-            float err = L.tgt[d] - L.q[d];
-            float u = L.u0[i];
-            float tau = kp * (err - dt * u) - kd * u;
-            float lim = m.effort[d];
-            const float c = dt * kp + kd;
-            const bool blocked = p.joint_limits && ((limmask >> b) & 1u);
-            const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) / (dot6(L.S[i], L.IS[i]) + m.armature[d] + dt * c);
-            if (fabsf(tau_i) > lim) {
-                const float sc = lim / fabsf(tau_i);
-                tau *= sc; kp *= sc; kd *= sc;
-            }
-            L.dforce[d] = tau;
-            rhs += tau;
-            cf = dt * kp + kd;
-        }
-        L.rhs[i] = dt * rhs;
-        L.coef[i] = cf;
-    }
-#endif
     sync();
     STAMP(3);
     // ---- CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i
@@ -1651,15 +1263,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // per-lane diagonal addend (dof = lane, and 64 + lane on lanes < 11), loaded once
         const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + dt * L.coef[lane] : 0.f;
         const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + dt * L.coef[64 + lane] : 0.f;
-#if HE_CRBA_MFMA
         (void)Sj; (void)Sj2;
         crba_mfma(M, L, lane, dadd, dadd2);
-#else
-        float first[4][6];
-        for (int k = 0; k < 4; ++k)
-            for (int x = 0; x < 6; ++x) first[k][x] = L.IS[k][x];
-        crba_groups<0>(M, Sj, Sj2, dadd, dadd2, L, first);
-#endif
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
@@ -1667,13 +1272,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     float yl = L.rhs[lane], y2 = lane < NH ? L.rhs[64 + lane] : 0.f;
     {
         float Dl = 1.f, D2 = 1.f;
-        __builtin_amdgcn_s_setprio(HE_PRIO_FACTOR);
-#if HE_FAC_PIPE
+        __builtin_amdgcn_s_setprio(kPrioSerial);
         factor_pipelined(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
-#else
-        factor_lds_groups<0>(M, Dl, D2, L.Lp, L.T.dof_depth[lane], lane < NH ? L.T.dof_depth[64 + lane] : 0, yl, y2);
-#endif
-        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(kPrioDefault);
         L.sDinv[lane] = 1.0f / sqrtf(Dl);
         if (lane < NH) L.sDinv[64 + lane] = 1.0f / sqrtf(D2);
         // the free velocity is not formed here: the contact bias takes z.u0 + zh.yh, and one L^-1
@@ -1683,7 +1284,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     sync();
     STAMP(5);
-    if (HE_BIAS_PREDICTOR && p.bias_midpoint) bias_midpoint(L, T, lane, p, stamps, t_prev);
+    if (p.bias_midpoint) bias_midpoint(L, T, lane, p, stamps, t_prev);
     // the contact phase's model reads (geometry of the lane's body, self-collision pair indices)
     // depend on nothing computed here: issued now, they land behind the free-velocity sweep
     constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
@@ -2190,9 +1791,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             STAMP(20);
-            __builtin_amdgcn_s_setprio(HE_PRIO_FACTOR);
+            __builtin_amdgcn_s_setprio(kPrioSerial);
             zbs<NG - 1>(L.Lp, z, lb);
-            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(kPrioDefault);
             STAMP(21);
             // z <- D^-1/2 z: the scale of dof i is broadcast from lane i's register (no LDS)
             const float sdl = L.sDinv[lane], sdl2 = lane < NH ? L.sDinv[64 + lane] : 0.f;
@@ -2218,9 +1819,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
             if (nr <= 32) delassus_mfma32(z, acol, live);  // wave-uniform
-#if HE_DELASSUS48
             else if (nr <= 48) delassus_mfma48(z, acol, live);
-#endif
             else delassus_mfma(z, acol, live);
         }
         STAMP(9);
@@ -2238,7 +1837,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     for (int r = 0; r < NRW; ++r) wa[r & 3] = fmaf(acol[r], regla::rdlane(lam0, r), wa[r & 3]);
                     w0 += (wa[0] + wa[1]) + (wa[2] + wa[3]);
                 };
-                if (HE_PGS_CLASS_PREP && nr <= 16) aw(std::integral_constant<int, 16>{});
+                if (nr <= 16) aw(std::integral_constant<int, 16>{});
                 else if (nr <= 32) aw(std::integral_constant<int, 32>{});
                 else if (nr <= 48) aw(std::integral_constant<int, 48>{});
                 else aw(std::integral_constant<int, MAXR>{});
@@ -2246,10 +1845,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             lamv = lam0;
             float cd = act ? -w0 * invd : 0.f;
             const float ninvd = -invd;
-#if !(HE_PGS_PACKED_BOUNDS && HE_PGS_FORM == 3 && HE_PGS_CLASS_PREP)
-#pragma unroll
-            for (int r = 0; r < MAXR; ++r) acol[r] *= ninvd;  // acolp: -A[r][lane] / A[lane][lane]
-#endif
             // the row's friction bound weight and its patch's normal rows n0 .. n0 + pc - 1 as a
             // 64-bit lane mask (friction rows only)
             const bool isn = kind == 0;
@@ -2274,9 +1869,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 }
                 bnd *= muw;
             }
-#if HE_PGS_PACKED_BOUNDS
             regla::f2v ak[MAXR];
-#if HE_PGS_FORM == 3 && HE_PGS_CLASS_PREP
             // the scaled columns acolp[r] = -A[r][lane] / A[lane][lane] and the packed bound weights of
             // the row-count class's rows only (the branch-free sweep reads no row past its class):
             // blocks of 16 rows, each behind a wave-uniform row-count test
@@ -2295,19 +1888,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 if (nrb > 32) prep(std::integral_constant<int, 32>{});
                 if (nrb > 48) prep(std::integral_constant<int, 48>{});
             }
-#else
-#pragma unroll
-            for (int r = 0; r < MAXR; ++r) {
-                const int sel = __builtin_amdgcn_sbfe((int)(r < 32 ? mlo : mhi), r & 31, 1);
-                ak[r] = regla::f2v{acol[r], __int_as_float(sel & __float_as_int(muw))};
-            }
-#endif
-#endif
             const float kInf = __builtin_inff();
             float lo = isn ? -lamv : -bnd - lamv;
             float hi = isn ? kInf : bnd - lamv;
             const int nru = __builtin_amdgcn_readfirstlane(nr);
-            __builtin_amdgcn_s_setprio(HE_PRIO_PGS);
+            __builtin_amdgcn_s_setprio(kPrioSerial);
             const float tol = p.solver_tolerance;
             for (int it = 0; it < p.solver_iterations; ++it) {
                 float dvec = 0.f;
@@ -2316,40 +1901,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 // lane-mask pairs (SGPR spills)
                 int nrs = nru;
                 asm volatile("" : "+s"(nrs));
-#if HE_PGS_PACKED_BOUNDS
                 regla::f2v ch = {cd, hi};
-#if HE_PGS_FORM == 3
-#if HE_PGS_MIN_CLASS <= 8
-                if (nrs <= 8) pgs_sweep_fix<0, 8>(ch, dvec, lo, ak, nrs);
-                else
-#endif
-#if HE_PGS_MIN_CLASS <= 16
                 if (nrs <= 16) pgs_sweep_fix<0, 16>(ch, dvec, lo, ak, nrs);
                 else
-#endif
                 if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak, nrs);
                 else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak, nrs);
                 else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak, nrs);
-#elif HE_PGS_FORM == 2
-                pgs_sweep_pk4<0>(ch, dvec, lo, ak, nrs);
-#elif HE_PGS_FORM
-                pgs_sweep_pk2<0>(ch, dvec, lo, ak, nrs);
-#else
-                pgs_sweep_pk<0>(ch, dvec, lo, ak, nrs);
-#endif
                 cd = ch.x;
                 hi = ch.y;
-#elif HE_PGS_OPAQUE_MASK
-                // the patch masks and weights through opaque copies per sweep: the per-row bound
-                // weights are formed in the sweep (2 VALU per row) instead of being hoisted out of
-                // the loop as 63 VGPRs
-                uint32_t mlo_ = mlo, mhi_ = mhi;
-                float muw_ = muw;
-                asm volatile("" : "+v"(mlo_), "+v"(mhi_), "+v"(muw_));
-                pgs_sweep<0>(cd, dvec, lo, hi, acol, mlo_, mhi_, muw_, nrs);
-#else
-                pgs_sweep<0>(cd, dvec, lo, hi, acol, mlo, mhi, muw, nrs);
-#endif
                 // the bound at the sweep's end: B = hi + lambda(start); then the bounds about the new impulse
                 const float bn = hi + lamv;
                 lamv += dvec;
@@ -2359,7 +1918,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 // the tolerance in this sweep, |d lambda_r| A_rr (oracle: the same test)
                 if (tol > 0.f && __ballot(act && fabsf(dvec) * diag > tol) == 0ull) break;
             }
-            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(kPrioDefault);
         }
         // the solve's impulses and row keys: the next solve's warm start and the reported forces
         L.lam[lane] = act ? lamv : 0.f;
@@ -2369,7 +1928,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // ---- du = M^-1 J^T lambda = L^-1 D^-1/2 (Zh^T lambda): lane r scales its row by lambda_r,
         // a wave reduce-scatter sums the 75 columns into lane = dof, then one L^-1 sweep
         {
-            __builtin_amdgcn_s_setprio(HE_PRIO_SOLVE);
+            __builtin_amdgcn_s_setprio(kPrioDefault);
             float v64[64], v16[16];
 #pragma unroll
             for (int i = 0; i < 64; ++i) v64[i] = ZV(z, i) * lamv;
@@ -2382,7 +1941,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
             load_rows(L, T, lane, r1, r2);
             solve_L(r1, r2, lane, yl, y2);
-            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(kPrioDefault);
             L.uf[lane] = L.u0[lane] + yl;
             if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
         }
@@ -2475,7 +2034,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         // the link's WORLD angular velocity (asset max_angular_velocity, PxRigidBody): w_b = w_parent +
         // R_b u_b summed along the chain (Acc is scratch here), clamped link by link; the joint rates
         // are then re-derived, u_b = R_b^T (w'_b - w'_parent) (oracle: the same pass)
-#if HE_WCLAMP_BOUND
         // no link can be over when |w_root| + (joints on the longest chain) x max_j |u_j| stays under
         // the cap (triangle inequality; a 1 % margin covers the prefix's rounding): the prefix and
         // the clamp are then skipped (wave-uniform), with the result they would give
@@ -2483,7 +2041,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const float wroot = regla::rdlane(un, 0);
         const bool may = bl && !root && un * (float)(smpl::kNumBodyLevels - 1) > 0.99f * p.max_angular_velocity - wroot;
         if (__ballot(may) != 0ull) {
-#endif
         const f4 qb = bl ? f4{L.qw[lane][0], L.qw[lane][1], L.qw[lane][2], L.qw[lane][3]} : f4{0.f, 0.f, 0.f, 1.f};
         const f3 wr = root ? f3{w[0], w[1], w[2]} : qapply(qb, f3{w[0], w[1], w[2]});
         // chain prefix by pointer jumping (the table stops below the root: its rate is added last)
@@ -2502,7 +2059,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             round(std::integral_constant<int, 2>{});
             if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
             const f3 w0 = f3{__shfl(wr.x, 0, W), __shfl(wr.y, 0, W), __shfl(wr.z, 0, W)};
-            if (HE_KIN_ROOTREL && bl && !root) wo = wo + w0;
+            if (bl && !root) wo = wo + w0;
         }
         const float wmax = p.max_angular_velocity;
         const float wn2 = dot3(wo, wo);
@@ -2517,9 +2074,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 w[0] = ub.x; w[1] = ub.y; w[2] = ub.z;
             }
         }
-#if HE_WCLAMP_BOUND
         }
-#endif
     }
     if (bl) {
         L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
@@ -2541,7 +2096,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 nql = pqexp(nv);
             }
             L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
-            if (HE_KIN_QCACHE) {
+            if (1) {
                 L.qloc[lane][0] = nql.x; L.qloc[lane][1] = nql.y; L.qloc[lane][2] = nql.z; L.qloc[lane][3] = nql.w;
             }
             lim_th = nv;

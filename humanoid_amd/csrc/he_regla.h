@@ -68,46 +68,11 @@ __device__ __forceinline__ bool lanes() {
     return __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
-    return v;
-}
-
-// ---------------------------------------------------------------- LTDL factorisation
-__device__ __forceinline__ float uniform(float v) {
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-
 // z -= a * b as an ordered instruction: the DAG linearisation would otherwise sink the whole
 // unrolled sweep's FMAs below its LDS reads and spill the loaded rows
 __device__ __forceinline__ void fnma(float& z, float a, float b) {
     asm volatile("v_fma_f32 %0, -%1, %2, %0" : "+v"(z) : "v"(a), "v"(b));
 }
-
-// the same without volatile: the scheduler may interleave them with independent work (data
-// dependences still order them)
-__device__ __forceinline__ void fnma_nv(float& z, float a, float b) {
-    asm("v_fma_f32 %0, -%1, %2, %0" : "+v"(z) : "v"(a), "v"(b));
-}
-template <int HALF>
-__device__ __forceinline__ void pk_fnma_nv(f2v& z, f2v a, f2v b) {
-    if constexpr (HALF == 0)
-        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "+v"(z) : "v"(a), "v"(b));
-    else
-        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
-            : "+v"(z) : "v"(a), "v"(b));
-}
-#ifndef HE_FAC_NV
-#define HE_FAC_NV 0
-#endif
-#if HE_FAC_NV
-#define FAC_FNMA fnma_nv
-#define FAC_PK_FNMA pk_fnma_nv
-#else
-#define FAC_FNMA fnma
-#define FAC_PK_FNMA pk_fnma
-#endif
 
 // z, z' -= a * b, a' * b as one v_pk_fma_f32, b taken from half HALF of its register pair
 template <int HALF>
@@ -120,6 +85,7 @@ __device__ __forceinline__ void pk_fnma(f2v& z, f2v a, f2v b) {
                      : "+v"(z) : "v"(a), "v"(b));
 }
 
+// ---------------------------------------------------------------- LTDL factorisation and solves
 // ---------------------------------------------------------------- per-lane z <- L^-T z (each lane its own rhs)
 // the packed row K (D entries) as registers: ceil(D/4) 16-byte LDS broadcasts
 template <int D>
@@ -186,24 +152,6 @@ __device__ __forceinline__ void undef_row(Row<D>& r) {
         asm volatile("" : "=v"(r.v[q]));
     }
 }
-template <int K>
-__device__ __forceinline__ void zbs_pipe(const float* Lp, ZVec& z, uint32_t lb, const typename RowOf<K>::T& rk) {
-    if constexpr (K >= 1) {
-        typename RowOf<K - 1>::T nx;
-        if constexpr (K - 1 >= 1) {
-            if (body_live<K - 1>(lb)) {  // prefetch row K-1 while row K is applied
-                int off = 0;
-                asm volatile("" : "+v"(off));
-                nx = load_row_if<K - 1>(Lp, off);
-            } else {
-                undef_row(nx);
-            }
-        }
-        if (body_live<K>(lb)) zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z);
-        __builtin_amdgcn_sched_barrier(0);
-        zbs_pipe<K - 1>(Lp, z, lb, nx);
-    }
-}
 // body-level variant: one liveness branch per body (its 3 rows, or the root's 5, applied in a
 // row-prefetch chain inside it) instead of two per dof
 template <int K>
@@ -250,20 +198,10 @@ __device__ __forceinline__ void zbs_bodies(const float* Lp, ZVec& z, uint32_t lb
         zbs_bodies<K0 - 1>(Lp, z, lb, nx);
     }
 }
-#ifndef HE_ZBS_BODY
-#define HE_ZBS_BODY 1
-#endif
 
 template <int K>
 __device__ __forceinline__ void zbs(const float* Lp, ZVec& z, uint32_t lb) {
-#if HE_ZBS_BODY
     zbs_bodies<K>(Lp, z, lb, row_if_live<K>(Lp, lb));
-    return;
-#endif
-    int off = 0;
-    asm volatile("" : "+v"(off));
-    const auto r0 = load_row_if<K>(Lp, off);
-    zbs_pipe<K>(Lp, z, lb, r0);
 }
 
 // ---------------------------------------------------------------- y <- L^-1 y, row-distributed
@@ -314,90 +252,15 @@ __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const 
     }
 }
 
-// ---------------------------------------------------------------- y <- L^-1 y by gathers
-// The same level sweep with the ancestor value gathered by ds_bpermute from a per-lane chain table
-// (byte D of chain word D/4 = the dof at depth D of the lane's chain, 0xFF past its end) instead
-// of one v_readlane + v_cndmask per dof of the level: two gathers (first / second register set)
-// and one masked FMA per level; the FMA and its operands are those of solve_L_rows (bit-identical).
-struct ChainBytes {
-    uint32_t w[NG][8];
-    constexpr ChainBytes() : w() {
-        for (int i = 0; i < NG; ++i)
-            for (int d = 0; d < 32; ++d) {
-                const uint32_t v = (d < kMaxChain && kChain[i][d] >= 0) ? (uint32_t)kChain[i][d] : 0xFFu;
-                w[i][d >> 2] |= v << (8 * (d & 3));
-            }
-    }
-};
-__device__ __forceinline__ float gather_lane(float v, int src) {  // v on lane src (0..63)
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
-}
-template <int D>
-constexpr bool level_reads_hi() {  // some dof at depth D is >= 64 (its y lives in the second set)
-    bool r = false;
-    for (int i = 0; i < NG; ++i)
-        if (kDofNanc[i] - 1 > D && kChain[i][D] >= 64) r = true;
-    return r;
-}
-template <int D>
-__device__ __forceinline__ void solve_L_gather(const float (&r1)[kRowRegs], const float (&r2)[kRowRegs],
-                                               const uint32_t (&c1)[8], const uint32_t (&c2)[8], float& yl,
-                                               float& y2) {
-    if constexpr (D < kNumLevels - 1) {
-        constexpr uint64_t ulo = level_desc_lo<D>();
-        constexpr uint64_t uhi = level_desc_hi<D>();
-        if constexpr (ulo != 0 || uhi != 0) {
-            const int s1 = (int)((c1[D >> 2] >> (8 * (D & 3))) & 0xFFu);
-            const int s2 = (int)((c2[D >> 2] >> (8 * (D & 3))) & 0xFFu);
-            float t1, t2 = 0.f;
-            if constexpr (level_reads_hi<D>()) {
-                const float a1 = gather_lane(yl, s1 & 63), b1 = gather_lane(y2, (s1 - 64) & 63);
-                t1 = s1 < 64 ? a1 : b1;
-                if constexpr (uhi != 0) {
-                    const float a2 = gather_lane(yl, s2 & 63), b2 = gather_lane(y2, (s2 - 64) & 63);
-                    t2 = s2 < 64 ? a2 : b2;
-                }
-            } else {
-                t1 = gather_lane(yl, s1 & 63);
-                if constexpr (uhi != 0) t2 = gather_lane(yl, s2 & 63);
-            }
-            if constexpr (ulo != 0) yl = lanes<ulo>() ? yl - r1[D] * t1 : yl;
-            if constexpr (uhi != 0) y2 = lanes<uhi>() ? y2 - r2[D] * t2 : y2;
-        }
-        solve_L_gather<D + 1>(r1, r2, c1, c2, yl, y2);
-    }
-}
-
 // ---------------------------------------------------------------- y <- L^-T y, one vector
 // Lane j holds y_j (and y_{64+j} in y2). The elimination's forward substitution replayed from the
 // stored factor: pivots in kElimOrder (deepest first, so every descendant of K is final before K
 // is read), each ancestor j of K taking y_j -= L[K][j] y_K with L[K][j] = Lp[kPackStart[K] + depth(j)].
-// Used by the bias predictor's correction, once per substep (not on the factor's latency chain).
-template <int J>
-__device__ __forceinline__ void solve_LT_vec(const float* Lp, int dj, int dj2, float& yl, float& y2) {
-    if constexpr (J < NG) {
-        constexpr int K = kElimOrder[J];
-        if constexpr (kDofNanc[K] - 1 > 0) {
-            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-            const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
-            // exec-masked: a branch-free form (every lane loads, selects) lets the compiler hoist
-            // all 75 row loads ahead of the chain, past the kernel's VGPR budget (measured: 1 wave
-            // per SIMD, -43% with the predictor off)
-            if (lanes<lo>()) yl = yl - Lp[kPackStart[K] + dj] * yk;
-            if constexpr (K > 64) {
-                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-                if (lanes<hi>()) y2 = y2 - Lp[kPackStart[K] + dj2] * yk;
-            }
-        }
-        solve_LT_vec<J + 1>(Lp, dj, dj2, yl, y2);
-    }
-}
-
-// solve_LT_vec in groups of mutually independent pivots (no pivot of a group is an ancestor of
+// Used by the midpoint bias's correction, once per substep (not on the factor's latency chain).
+// The pivots run in groups of mutually independent ones (no pivot of a group is an ancestor of
 // another, so every y_K of a group is final when the group starts; ElimGroups below): the group's
-// broadcasts are read first, then its updates, so the dependent chain is paid once per group (30
-// groups of the 75 pivots) instead of once per pivot. Each register's updates keep their order
-// within a group only up to the group's order, so the rounding differs from solve_LT_vec.
+// broadcasts are read first, then its updates, so the dependent chain is paid once per group
+// instead of once per pivot.
 template <int GMAX>
 struct ElimGroups;
 template <int S0, int Q, int N>
@@ -408,22 +271,6 @@ __device__ __forceinline__ void lt_group_read(float (&yk)[N], float yl, float y2
         lt_group_read<S0, Q + 1, N>(yk, yl, y2);
     }
 }
-template <int S0, int Q, int N>
-__device__ __forceinline__ void lt_group_update(const float* Lp, int dj, int dj2, const float (&yk)[N], float& yl,
-                                                float& y2) {
-    if constexpr (Q < N) {
-        constexpr int K = kElimOrder[S0 + Q];
-        if constexpr (kDofNanc[K] - 1 > 0) {
-            constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
-            if (lanes<lo>()) yl = yl - Lp[kPackStart[K] + dj] * yk[Q];
-            if constexpr (K > 64) {
-                constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-                if (lanes<hi>()) y2 = y2 - Lp[kPackStart[K] + dj2] * yk[Q];
-            }
-        }
-        lt_group_update<S0, Q + 1, N>(Lp, dj, dj2, yk, yl, y2);
-    }
-}
 
 // ---------------------------------------------------------------- grouped elimination
 // Consecutive steps of kElimOrder whose dofs are mutually independent (neither is an ancestor of
@@ -431,7 +278,7 @@ __device__ __forceinline__ void lt_group_update(const float* Lp, int dj, int dj2
 // step: all pivots and reciprocals, then all packed-row stores and right-hand-side updates, then
 // all row broadcasts (one LDS round trip), then the ancestor updates in the original order. Every
 // register sees its updates in the same order as in the one-at-a-time elimination, so the factor
-// is bit-identical to factor_lds_steps; the dependent latency chain is paid once per group.
+// is bit-identical to the one-at-a-time elimination; the dependent latency chain is paid once per group.
 constexpr bool dof_is_anc(int a, int b) {  // b in chain(a), a itself included
     return b < 64 ? ((kAncLo[a] >> b) & 1ull) != 0 : ((kAncHi[a] >> (b - 64)) & 1u) != 0;
 }
@@ -456,22 +303,14 @@ struct ElimGroups {
         start[count] = NG;
     }
 };
-#ifndef HE_ELIM_GMAX
-#define HE_ELIM_GMAX 2
-#endif
-constexpr int kElimGroupMax = HE_ELIM_GMAX;
+constexpr int kElimGroupMax = 2;
 constexpr ElimGroups<kElimGroupMax> kElimGroups{};
-constexpr ElimGroups<8> kLTGroups{};  // solve_LT_vec_groups: 30 groups
 
-// solve_LT_vec_groups with the packed-row loads one group ahead: group G+1's L entries are read
-// (every lane, its own ancestor offset, clamped into the factor) while group G's pivots are
-// broadcast and applied, so a group pays its readlanes and FMAs but not an LDS round trip. The
-// update stays exec-masked to the pivot's ancestor lanes; same operations in the same order as
-// solve_LT_vec_groups (bit-identical).
-#ifndef HE_LT_PIPE_GROUP
-#define HE_LT_PIPE_GROUP 4
-#endif
-constexpr ElimGroups<HE_LT_PIPE_GROUP> kLTPipeGroups{};
+// The packed-row loads run one group ahead: group G+1's L entries are read (every lane, its own
+// ancestor offset, clamped into the factor) while group G's pivots are broadcast and applied, so a
+// group (of at most 4 pivots) pays its readlanes and FMAs but not an LDS round trip. The update
+// stays exec-masked to the pivot's ancestor lanes.
+constexpr ElimGroups<4> kLTPipeGroups{};
 template <int G>
 struct LTGroup {
     static constexpr int S0 = G < kLTPipeGroups.count ? kLTPipeGroups.start[G] : 0;
@@ -534,21 +373,6 @@ __device__ __forceinline__ void solve_LT_vec_pipelined(const float* Lp, int dj, 
     solve_LT_vec_pipe<0>(Lp, dj, dj2, yl, y2, l1, l2);
 }
 
-template <int G>
-__device__ __forceinline__ void solve_LT_vec_groups(const float* Lp, int dj, int dj2, float& yl, float& y2) {
-    if constexpr (G < kLTGroups.count) {
-        constexpr int S0 = kLTGroups.start[G], N = kLTGroups.start[G + 1] - kLTGroups.start[G];
-        float yk[N];
-        lt_group_read<S0, 0, N>(yk, yl, y2);
-        lt_group_update<S0, 0, N>(Lp, dj, dj2, yk, yl, y2);
-        __builtin_amdgcn_sched_barrier(0);  // the next group's row loads stay behind (VGPR budget)
-        solve_LT_vec_groups<G + 1>(Lp, dj, dj2, yl, y2);
-    }
-}
-
-#ifndef HE_FAC_VINV  // +0.4% (A/B r01)
-#define HE_FAC_VINV 1
-#endif
 template <int K>
 struct PivotStep {
     float dk, l, l2;  // pivot, row K of L on this lane (scaled) and its second-set entry
@@ -559,40 +383,16 @@ struct PivotStep {
 template <int K>
 __device__ __forceinline__ void grp_pivot(const RegMat& M, PivotStep<K>& st) {
     st.dk = get<K, K>(M);
-#if HE_FAC_VINV  // the reciprocal stays a (wave-uniform) VGPR: no readfirstlane on the pivot chain
     const float inv = __builtin_amdgcn_rcpf(st.dk);
-#else
-    const float inv = uniform(__builtin_amdgcn_rcpf(st.dk));
-#endif
     st.l = mc<K>(M) * inv;
     if constexpr (K >= 64) st.l2 = mc2<K >= 64 ? K - 64 : 0>(M) * inv;
 }
 // B: packed-row store and the fused forward substitution of the right-hand side
-#ifndef HE_FAC_NOBRANCH  // sink-slot stores instead of exec-mask branches: no gain (A/B r01)
-#define HE_FAC_NOBRANCH 0
-#endif
 template <int K>
 __device__ __forceinline__ void grp_store(const PivotStep<K>& st, float* Lp, int dj, int dj2, float& yl, float& y2) {
     if constexpr (kDofNanc[K] - 1 > 0) {
         constexpr uint64_t lo = K < 64 ? (kAncLo[K] & ~(1ull << (K & 63))) : kAncLo[K];
         const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K >= 64 ? K - 64 : 0);
-#if HE_FAC_NOBRANCH
-        // no exec-mask branch: lanes off the chain store into the sink slot Lp[kNpack], and the
-        // right-hand side update is a select
-        {
-            const bool on = lanes<lo>();
-            Lp[on ? kPackStart[K] + dj : kNpack] = st.l;
-            const float yn = yl - st.l * yk;
-            yl = on ? yn : yl;
-        }
-        if constexpr (K > 64) {
-            constexpr uint64_t hi = kAncHi[K] & ~(1u << (K - 64));
-            const bool on2 = lanes<hi>();
-            Lp[on2 ? kPackStart[K] + dj2 : kNpack] = st.l2;
-            const float yn2 = y2 - st.l2 * yk;
-            y2 = on2 ? yn2 : y2;
-        }
-#else
         if (lanes<lo>()) {
             Lp[kPackStart[K] + dj] = st.l;
             yl = yl - st.l * yk;
@@ -604,7 +404,6 @@ __device__ __forceinline__ void grp_store(const PivotStep<K>& st, float* Lp, int
                 y2 = y2 - st.l2 * yk;
             }
         }
-#endif
     }
 }
 // C + D: row broadcast (in-order LDS: sees the stores of B), the ancestor updates, then row K of M
@@ -655,44 +454,11 @@ __device__ __forceinline__ float lrow(const PivotStep<K>& st) {  // L[K][I], wav
     if constexpr (I < 64) return rdlane(st.l, I);
     else return rdlane(st.l2, I >= 64 ? I - 64 : 0);
 }
-template <int K, int X, int D>
-__device__ __forceinline__ void fac_anc_rl(RegMat& M, const PivotStep<K>& st) {
-    if constexpr (X < D) {
-        constexpr int I = kChain[K][X];
-        constexpr bool PAIR = X + 1 < D && I % 2 == 0 && I + 1 < 64 && kChain[K][X + 1 < kMaxChain ? X + 1 : 0] == I + 1;
-        if constexpr (PAIR) {
-            f2v l;
-            l[0] = lrow<K, I>(st);
-            l[1] = lrow<K, I + 1>(st);
-            if constexpr ((K & 1) == 0) pk_fnma_s0(M.cp[I >> 1], l, M.cp[K >> 1]);
-            else pk_fnma_s1(M.cp[I >> 1], l, M.cp[K >> 1]);
-            fac_anc_rl<K, X + 2, D>(M, st);
-        } else {
-            const float l = lrow<K, I>(st);
-            float c = mc<I>(M);
-            c = fmaf(-l, mc<K>(M), c);
-            mc_set<I>(M, c);
-            if constexpr (I >= 64) {
-                float c2 = mc2<I - 64>(M);
-                c2 = fmaf(-l, mc2<K >= 64 ? K - 64 : 0>(M), c2);
-                mc2_set<I - 64>(M, c2);
-            }
-            fac_anc_rl<K, X + 1, D>(M, st);
-        }
-    }
-}
 // off: the elimination phase itself is ~8% shorter with it, but its ~1200 v_readlane per factor
 // take issue slots from the partner wave and the launch is 1.3% slower (A/B, r01)
-#ifndef HE_FAC_READLANE
-#define HE_FAC_READLANE 0
-#endif
 template <int K>
 __device__ __forceinline__ void grp_update(RegMat& M, float& Dl, float& D2, const PivotStep<K>& st) {
-#if HE_FAC_READLANE
-    if constexpr (kDofNanc[K] - 1 > 0) fac_anc_rl<K, 0, kDofNanc[K] - 1>(M, st);
-#else
     if constexpr (kDofNanc[K] - 1 > 0) fac_anc_pk<K, 0, kDofNanc[K] - 1>(M, st.row);
-#endif
     mc_set<K>(M, st.l);  // row K -> L[K][.] on lanes j < K
     if constexpr (K >= 64) mc2_set<K - 64>(M, st.l2);
     if constexpr (K < 64) Dl = wrlane<K>(st.dk, Dl);
@@ -700,9 +466,7 @@ __device__ __forceinline__ void grp_update(RegMat& M, float& Dl, float& D2, cons
 }
 template <int K>
 __device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st) {
-#if !HE_FAC_READLANE
     if constexpr (kDofNanc[K] - 1 > 0) st.row = load_row<K>(Lp, kPackStart[K]);
-#endif
 }
 // ---------------------------------------------------------------- software-pipelined groups
 // The next group's pivots only wait for the updates of their own rows. Those rows (I in chain(K)
@@ -724,11 +488,11 @@ __device__ __forceinline__ void fac_anc_fast(RegMat& M, const PivotStep<K>& st) 
         if constexpr (in_group<GN>(I)) {
             const float l = lrow<K, I>(st);
             float c = mc<I>(M);
-            FAC_FNMA(c, l, mc<K>(M));
+            fnma(c, l, mc<K>(M));
             mc_set<I>(M, c);
             if constexpr (I >= 64) {
                 float c2 = mc2<I - 64>(M);
-                FAC_FNMA(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
                 mc2_set<I - 64>(M, c2);
             }
         }
@@ -747,16 +511,16 @@ __device__ __forceinline__ void fac_anc_slow(RegMat& M, const Row<D>& row) {
             fac_anc_slow<K, X + 1, D, GN>(M, row);
         } else if constexpr (PAIR) {
             const f2v l = X % 4 == 0 ? __builtin_shufflevector(v, v, 0, 1) : __builtin_shufflevector(v, v, 2, 3);
-            FAC_PK_FNMA<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
+            pk_fnma<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
             fac_anc_slow<K, X + 2, D, GN>(M, row);
         } else {
             const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
             float c = mc<I>(M);
-            FAC_FNMA(c, l, mc<K>(M));
+            fnma(c, l, mc<K>(M));
             mc_set<I>(M, c);
             if constexpr (I >= 64) {
                 float c2 = mc2<I - 64>(M);
-                FAC_FNMA(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
+                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
                 mc2_set<I - 64>(M, c2);
             }
             fac_anc_slow<K, X + 1, D, GN>(M, row);
@@ -824,32 +588,4 @@ __device__ __forceinline__ void factor_pipelined(RegMat& M, float& Dl, float& D2
     factor_pipe<0>(M, Dl, D2, Lp, dj, dj2, yl, y2, g);
 }
 
-template <int GI>
-__device__ __forceinline__ void factor_lds_groups(RegMat& M, float& Dl, float& D2, float* Lp, int dj, int dj2,
-                                                  float& yl, float& y2) {
-    if constexpr (GI < kElimGroups.count) {
-        constexpr int S0 = kElimGroups.start[GI], n = kElimGroups.start[GI + 1] - S0;
-        static_assert(n >= 1 && n <= 3, "group size");
-        constexpr int K0 = kElimOrder[S0];
-        constexpr int K1 = kElimOrder[n > 1 ? S0 + 1 : S0];
-        constexpr int K2 = kElimOrder[n > 2 ? S0 + 2 : S0];
-        PivotStep<K0> a;
-        PivotStep<K1> b;
-        PivotStep<K2> c;
-        grp_pivot<K0>(M, a);
-        if constexpr (n > 1) grp_pivot<K1>(M, b);
-        if constexpr (n > 2) grp_pivot<K2>(M, c);
-        grp_store<K0>(a, Lp, dj, dj2, yl, y2);
-        if constexpr (n > 1) grp_store<K1>(b, Lp, dj, dj2, yl, y2);
-        if constexpr (n > 2) grp_store<K2>(c, Lp, dj, dj2, yl, y2);
-        grp_load<K0>(Lp, a);
-        if constexpr (n > 1) grp_load<K1>(Lp, b);
-        if constexpr (n > 2) grp_load<K2>(Lp, c);
-        grp_update<K0>(M, Dl, D2, a);
-        if constexpr (n > 1) grp_update<K1>(M, Dl, D2, b);
-        if constexpr (n > 2) grp_update<K2>(M, Dl, D2, c);
-        __builtin_amdgcn_sched_barrier(0);
-        factor_lds_groups<GI + 1>(M, Dl, D2, Lp, dj, dj2, yl, y2);
-    }
-}
 }  // namespace regla
