@@ -469,12 +469,19 @@ static int gen_limits(const he_model* m, const he_sim_params* p, const env_state
 
 /* Solver rows of a slot set (limits 1; a body's terrain patch of k points k normal rows + 2
  * tangential + 1 torsional from k = 2; a self pair 3) */
+/* diagnostic (tests/diag/anchor_study.py): PhysX-style two-anchor patch friction instead of the
+ * centroid pair + torsional row. A terrain patch of >= 2 points gets 2 tangential rows at each of two
+ * anchors -- its first point and the point farthest from it in the tangent plane -- each row bounded by
+ * mu / 2 x the patch's normal impulses (the anchors share the patch's load); 1-point patches and self
+ * pairs are unchanged. Off (0) in every test of the engine's physics. */
+static int g_two_anchor = 0;
+void ho_set_two_anchor(int on) { g_two_anchor = on; }
 static int rows_of(const contact* cs, int nc) {
     int nr = 0, pos = 0; /* pos: the point's index in its body's terrain patch */
     for (int i = 0; i < nc; ++i) {
         if (cs[i].b1 != -1) { nr += cs[i].b1 == -2 ? 1 : 3; continue; }
         pos = (i > 0 && cs[i - 1].b1 == -1 && cs[i - 1].b0 == cs[i].b0) ? pos + 1 : 0;
-        nr += pos == 0 ? 3 : (pos == 1 ? 2 : 1);
+        nr += pos == 0 ? 3 : (pos == 1 ? 2 + g_two_anchor : 1);
     }
     return nr;
 }
@@ -520,7 +527,7 @@ static int gen_contacts(const he_model* m, const he_sim_params* p, const kin* k,
     for (int q = 0; q < no; ++q) {
         const int i = order[q];
         const int terr = cs[i].b1 == -1;
-        const int cost = !terr ? 3 : (pc[cs[i].b0] == 0 ? 3 : (pc[cs[i].b0] == 1 ? 2 : 1));
+        const int cost = !terr ? 3 : (pc[cs[i].b0] == 0 ? 3 : (pc[cs[i].b0] == 1 ? 2 + g_two_anchor : 1));
         if (slots < maxc && rows + cost <= maxr) {
             kept[i] = 1;
             rows += cost;
@@ -570,6 +577,32 @@ static int build_rows(const contact* cs, int nc, const R* o, srow* rows) {
         }
         rp /= cnt;
         R xpo[3] = {xp[0] - o[0], xp[1] - o[1], xp[2] - o[2]};
+        if (g_two_anchor && terr && cnt >= 2) {
+            int far = first;
+            R best = -1;
+            for (int j = first + 1; j <= i; ++j) {
+                R d[3] = {cs[j].x[0] - cs[first].x[0], cs[j].x[1] - cs[first].x[1], cs[j].x[2] - cs[first].x[2]};
+                const R dn = dot3(d, np);
+                R tg[3] = {d[0] - dn * np[0], d[1] - dn * np[1], d[2] - dn * np[2]};
+                const R dd = dot3(tg, tg);
+                if (dd > best) { best = dd; far = j; }
+            }
+            const int anc[2] = {first, far};
+            for (int a = 0; a < 2; ++a) {
+                R xa[3] = {cs[anc[a]].x[0] - o[0], cs[anc[a]].x[1] - o[1], cs[anc[a]].x[2] - o[2]};
+                for (int kd = 1; kd <= 2; ++kd) {
+                    srow* f = &rows[nr++];
+                    memset(f, 0, sizeof(*f));
+                    f->slot = i; f->kind = kd; f->n0 = nr - 1 - (2 * a + kd - 1) - cnt;
+                    f->cnt = cnt; f->b0 = c->b0; f->b1 = c->b1;
+                    memcpy(f->dir, kd == 1 ? t1 : t2, sizeof(f->dir));
+                    cross3(xa, f->dir, f->rho);
+                    f->muw = 0.5 * c->mu;
+                    f->key = (c->b0 | (1 << 5) | ((HE_KEY_PATCH - a) << 10)) | (kd << 14);
+                }
+            }
+            continue;
+        }
         const int nf = cnt >= 2 ? 3 : 2;
         for (int kd = 1; kd <= nf; ++kd) {
             srow* f = &rows[nr++];

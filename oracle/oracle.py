@@ -172,6 +172,12 @@ def set_row_weight_out(arr=None):
     lib().ho_set_row_weight_out(None if arr is None else arr.ctypes.data_as(C.POINTER(C.c_float)))
 
 
+def set_two_anchor(on):
+    """Diagnostics only (tests/diag/anchor_study.py): PhysX-style two-anchor patch friction in the
+    oracle's solver rows instead of the engine's centroid pair + torsional row."""
+    lib().ho_set_two_anchor(int(bool(on)))
+
+
 def set_row_gap_out(arr=None):
     """Diagnostics only: float32 [N, HE_MAX_ROWS] filled with the gap of every solver row's contact of
     each env's last substep (m; a joint-limit row: its angle gap), in the cache's row order."""
