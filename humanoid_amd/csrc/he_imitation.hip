@@ -411,6 +411,27 @@ hipError_t launch_imitation(const ImitArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+namespace {
+__global__ void warm_tu_kernel() {}
+}  // namespace
+
+hipError_t warm_imitation_kernels(hipStream_t stream, int mode) {
+    if (mode == 1) {
+        warm_tu_kernel<<<1, 64, 0, stream>>>();
+        return hipGetLastError();
+    }
+    ImitArgs ia{};
+    imitation_kernel<false><<<1, HE_IMIT_THREADS, 0, stream>>>(ia);
+    imitation_kernel<true><<<1, HE_IMIT_THREADS, 0, stream>>>(ia);
+    MotionStateArgs ma{};
+    motion_state_kernel<<<1, 256, 0, stream>>>(ma);
+    AmpArgs aa{};
+    aa.amp.num_steps = 1;
+    amp_kernel<<<1, 256, 0, stream>>>(aa);
+    amp_function_kernel<<<1, 256, 0, stream>>>(aa);
+    return hipGetLastError();
+}
+
 hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream) {
     if (a.k <= 0) return hipSuccess;
     int threads = 256;

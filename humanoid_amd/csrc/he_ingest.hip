@@ -164,6 +164,21 @@ __global__ void __launch_bounds__(256) filter_kernel(IngestArgs a) {
 
 }  // namespace
 
+namespace {
+__global__ void warm_tu_kernel() {}
+}  // namespace
+
+hipError_t warm_ingest_kernels(hipStream_t stream, int mode) {
+    if (mode == 1) {
+        warm_tu_kernel<<<1, 64, 0, stream>>>();
+        return hipGetLastError();
+    }
+    IngestArgs ia{};
+    frame_kernel<<<1, 256, 0, stream>>>(ia);
+    filter_kernel<<<1, 256, 0, stream>>>(ia);
+    return hipGetLastError();
+}
+
 hipError_t launch_ingest(const float* pose, const float* trans, const int32_t* parents, const float* local_pos,
                          const int64_t* starts, const int64_t* nframes, const float* dt, int num_clips, int64_t F,
                          float* hot, float* cold, float* gav_raw, hipStream_t stream) {

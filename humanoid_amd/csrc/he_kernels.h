@@ -119,6 +119,14 @@ hipError_t launch_amp(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_amp_function(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream);
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);
+// First-dispatch warm-up (he_create_envs): every product kernel of the TU launched once with no work
+// (count 0, one block that exits at its guard), so the one-time first-dispatch cost of each kernel
+// (~0.4-0.8 ms on the MI355X, 16-30 ms under rocprofv3's kernel tracing) is paid at engine
+// creation, not by the setup's first reset or a timed step. mode 1: one trivial kernel per TU
+// (diagnostic: whether the cost is per code object or per kernel).
+hipError_t warm_imitation_kernels(hipStream_t stream, int mode);
+hipError_t warm_physics_kernels(hipStream_t stream, int mode);
+hipError_t warm_ingest_kernels(hipStream_t stream, int mode);
 bool physics_phase_stamps();  // built with HE_PHASE_STAMPS (diagnostic twin library)
 hipError_t launch_ingest(const float* pose, const float* trans, const int32_t* parents, const float* local_pos,
                          const int64_t* starts, const int64_t* nframes, const float* dt, int num_clips, int64_t F,
