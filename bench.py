@@ -176,6 +176,7 @@ class Rollout:
         phases = torch.as_tensor(rng.uniform(0, 1, n).astype(np.float32), device=dev)
         self.eng.reset_envs(self.p, self.em, ids, phases, self.obs, self.reset, self.term)
         self.eng.set_fused_step(self.fused)
+        torch.cuda.synchronize()  # the setup's launches end here, before any step is enqueued
 
     def tracking_actions(self):
         """a = clip(ref_dof_pos / scale, -1, 1) with the reference pose at

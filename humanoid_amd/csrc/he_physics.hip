@@ -93,10 +93,6 @@ struct Lds {
 constexpr int kPrioSerial = 3;
 constexpr int kPrioDefault = 0;
 
-#ifndef HE_PGS_DEFER
-#define HE_PGS_DEFER 0
-#endif
-
 // wave-level ordering point: one wave per workgroup, LDS executes its instructions in order, so
 // only the compiler must not move memory operations across phase boundaries
 HE_DEV void sync() {
@@ -533,33 +529,7 @@ HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uin
 // 63) by the row count, with no per-row row-count branch (a row-count exit every 4 rows); rows nr..N-1 are empty rows (zero columns and
 // bound weights in every lane, zero cd and bounds in their own lanes: a +-0 change).
 template <int R, int N>
-HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr, float dprev) {
-#if HE_PGS_DEFER
-    // row R-1's change is recorded on its lane in row R's block, after row R's clamp: the
-    // v_writelane sits between the v_med3 and its v_readlane instead of between the v_readlane and
-    // the FMAs that wait for its SGPR (microbenchmark tools/ubench/pgs_row.hip: 47.9 -> 43.7 cycles
-    // per row at two waves per SIMD); rows fenced by sched_barrier to keep that order
-    if constexpr (R < N) {
-        if constexpr (R > 0 && R % 4 == 0) {  // a row-count exit every 4 rows
-            if (R >= nr) {
-                dvec = regla::wrlane<R - 1>(dprev, dvec);
-                return;
-            }
-        }
-        const float m = __builtin_amdgcn_fmed3f(ch.x, lo, ch.y);
-        if constexpr (R > 0) dvec = regla::wrlane<R - 1>(dprev, dvec);
-        const float d = regla::rdlane(m, R);
-        ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
-        lo = fmaf(-ak[R].y, d, lo);
-#if !HE_PGS_DEFER_NOSB
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr, d);
-    } else {
-        dvec = regla::wrlane<N - 1>(dprev, dvec);
-    }
-#else
-    (void)dprev;
+HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
     if constexpr (R < N) {
         if constexpr (R > 0 && R % 4 == 0) {  // a row-count exit every 4 rows
             if (R >= nr) return;
@@ -568,9 +538,8 @@ HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f
         ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
         lo = fmaf(-ak[R].y, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
-        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr, 0.f);
+        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr);
     }
-#endif
 }
 
 // CRBA straight into registers: lane j owns column j, H[i][j] = S_j . IS_i for j in chain(i)
@@ -1933,11 +1902,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 int nrs = nru;
                 asm volatile("" : "+s"(nrs));
                 regla::f2v ch = {cd, hi};
-                if (nrs <= 16) pgs_sweep_fix<0, 16>(ch, dvec, lo, ak, nrs, 0.f);
+                if (nrs <= 16) pgs_sweep_fix<0, 16>(ch, dvec, lo, ak, nrs);
                 else
-                if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak, nrs, 0.f);
-                else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak, nrs, 0.f);
-                else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak, nrs, 0.f);
+                if (nrs <= 32) pgs_sweep_fix<0, 32>(ch, dvec, lo, ak, nrs);
+                else if (nrs <= 48) pgs_sweep_fix<0, 48>(ch, dvec, lo, ak, nrs);
+                else pgs_sweep_fix<0, MAXR>(ch, dvec, lo, ak, nrs);
                 cd = ch.x;
                 hi = ch.y;
                 // the bound at the sweep's end: B = hi + lambda(start); then the bounds about the new impulse
@@ -2127,9 +2096,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 nql = pqexp(nv);
             }
             L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
-            if (1) {
-                L.qloc[lane][0] = nql.x; L.qloc[lane][1] = nql.y; L.qloc[lane][2] = nql.z; L.qloc[lane][3] = nql.w;
-            }
+            // the next substep's kinematics starts from this rotation instead of exp(log(.))
+            L.qloc[lane][0] = nql.x; L.qloc[lane][1] = nql.y; L.qloc[lane][2] = nql.z; L.qloc[lane][3] = nql.w;
             lim_th = nv;
             lim_u = f3{w[0], w[1], w[2]};
         }

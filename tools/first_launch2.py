@@ -58,6 +58,8 @@ def main():
         out["pre_ms"] = timed(lambda: ro.eng.simulate(2))
     out["full_reset_ms"] = timed(lambda: ro.eng.reset_envs(p, em, ids, phases, obs, reset, term))
     out["full_reset_again_ms"] = timed(lambda: ro.eng.reset_envs(p, em, ids, phases, obs, reset, term))
+    out["first_step_ms"] = timed(ro.step)
+    out["second_step_ms"] = timed(ro.step)
     out["definition"] = "(event ms, host wall ms) per launch"
     print(json.dumps(out), flush=True)
 
