@@ -1023,9 +1023,17 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // by the force pass).
 // yh += D^-1/2 L^-T dc (lane = dof, then dofs 64..74 on lanes 0..10): the midpoint correction's
 // forward substitution replayed from the stored factor
+#ifndef HE_PRIO_DU  // A/B: s_setprio over the final du sweep
+#define HE_PRIO_DU 0
+#endif
+#ifndef HE_PRIO_MID  // A/B: s_setprio over the midpoint's serial sweeps (L^-1 for um, the L^-T of dc)
+#define HE_PRIO_MID 0
+#endif
 HE_DEV void mid_lt(Lds& L, const BodyTopo& T, int lane, float c1, float c2) {
     using regla::NH;
+    if constexpr (HE_PRIO_MID != 0) __builtin_amdgcn_s_setprio(HE_PRIO_MID);
     regla::solve_LT_vec_pipelined(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, c1, c2);
+    if constexpr (HE_PRIO_MID != 0) __builtin_amdgcn_s_setprio(kPrioDefault);
     L.yh[lane] += c1 * L.sDinv[lane];
     if (lane < NH) L.yh[64 + lane] += c2 * L.sDinv[64 + lane];
     sync();
@@ -1041,7 +1049,9 @@ HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_para
         load_rows(L, T, lane, r1, r2);
         float t1 = L.yh[lane] * L.sDinv[lane];
         float t2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
+        if constexpr (HE_PRIO_MID != 0) __builtin_amdgcn_s_setprio(HE_PRIO_MID);
         solve_L(r1, r2, lane, t1, t2);
+        if constexpr (HE_PRIO_MID != 0) __builtin_amdgcn_s_setprio(kPrioDefault);
         L.uf[lane] = L.u0[lane] + 0.5f * t1;
         if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + 0.5f * t2;
     }
@@ -1940,6 +1950,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             y2 = lane < NH ? (y2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
             load_rows(L, T, lane, r1, r2);
+            if constexpr (HE_PRIO_DU != 0) __builtin_amdgcn_s_setprio(HE_PRIO_DU);
             solve_L(r1, r2, lane, yl, y2);
             __builtin_amdgcn_s_setprio(kPrioDefault);
             L.uf[lane] = L.u0[lane] + yl;
