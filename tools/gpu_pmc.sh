@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-run}
 CONFIG=${CONFIG:-standstill}
-B="bench.py --config $CONFIG --steps 10 --warmup 3 --no-cpu-baseline --no-puffer-level --no-tracking"
+B="bench.py --config $CONFIG --steps 10 --warmup 3 --no-cpu-baseline --no-puffer-level --no-tracking --no-learner"
 rm -rf gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG
 [ -f profiles/pmc_traffic.json ] && [ ! -f gpurun_out/pmc_traffic.json ] && cp profiles/pmc_traffic.json gpurun_out/pmc_traffic.json
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run -- python3 $B > gpurun_out/pmc_fetch_$TAG.log 2>&1 &&

@@ -7,10 +7,10 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r03f}
-Q="bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-puffer-level --no-tracking"
+Q="bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-puffer-level --no-tracking --no-learner"
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_full_$TAG.log 2>&1 &&
-timeout -k 10 200 python -u bench.py --config imitation --no-cpu-baseline --no-puffer-level > gpurun_out/bench_imit_$TAG.log 2>&1 &&
-timeout -k 10 200 python -u bench.py --config dr --no-cpu-baseline --no-puffer-level --no-tracking > gpurun_out/bench_dr_$TAG.log 2>&1 &&
+timeout -k 10 200 python -u bench.py --config imitation --no-cpu-baseline --no-puffer-level --no-learner > gpurun_out/bench_imit_$TAG.log 2>&1 &&
+timeout -k 10 200 python -u bench.py --config dr --no-cpu-baseline --no-puffer-level --no-tracking --no-learner > gpurun_out/bench_dr_$TAG.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 $Q > gpurun_out/bench_prof_$TAG.log 2>&1 &&
 timeout -k 10 300 python tools/phase_profile.py > gpurun_out/phases_$TAG.json 2> gpurun_out/phases_$TAG.err &&
 timeout -k 10 300 python -u tools/action_regimes.py > gpurun_out/action_regimes_$TAG.json 2> gpurun_out/action_regimes_$TAG.err &&
