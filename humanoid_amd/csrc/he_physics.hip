@@ -1024,15 +1024,6 @@ HE_DEV void load_rows(const Lds& L, const BodyTopo& T, int lane, float (&r1)[reg
 // by the force pass).
 // yh += D^-1/2 L^-T dc (lane = dof, then dofs 64..74 on lanes 0..10): the midpoint correction's
 // forward substitution replayed from the stored factor
-#ifndef HE_PRIO_SUB  // A/B: s_setprio over the subtree sums by body levels (both RNEA passes)
-#define HE_PRIO_SUB 0
-#endif
-#ifndef HE_PRIO_DEL  // A/B: s_setprio over the matrix-core phases (CRBA, Delassus)
-#define HE_PRIO_DEL 0
-#endif
-#ifndef HE_PRIO_DU  // A/B: s_setprio over the final du sweep
-#define HE_PRIO_DU 0
-#endif
 HE_DEV void mid_lt(Lds& L, const BodyTopo& T, int lane, float c1, float c2) {
     using regla::NH;
     __builtin_amdgcn_s_setprio(kPrioSerial);  // a serial chain: -1.2 % physics launch by A/B (r04)
@@ -1125,9 +1116,7 @@ HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_para
     // subtree sums of the new body forces, in place by body levels (as the first bias's): +4.8 %
     // against the per-dof-lane sums below (r03 A/B, profiles/r03/ab_pred_levels.txt, under the
     // two-wave bound that lets it fit)
-    if constexpr (HE_PRIO_SUB != 0) __builtin_amdgcn_s_setprio(HE_PRIO_SUB);
     subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.Acc[0][0], nullptr, lane);
-    if constexpr (HE_PRIO_SUB != 0) __builtin_amdgcn_s_setprio(kPrioDefault);
     auto corr = [&](int i) {
         const int bi = i < 6 ? 0 : (i - 6) / 3 + 1;
         return dt * (dot6(L.S[i], L.F[bi]) - dot6(L.S[i], L.Acc[bi]));
@@ -1232,7 +1221,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     sync();
     STAMP(1);
     // ---- subtree sums: F_b (forces) and composite inertias, in place by body levels
-    __builtin_amdgcn_s_setprio(HE_PRIO_SUB != 0 ? HE_PRIO_SUB : kPrioDefault);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
     subtree_levels<16, smpl::kNumBodyLevels - 2>(&L.F[0][0], &L.Ic[0][0], lane);
     __builtin_amdgcn_s_setprio(kPrioDefault);
     STAMP(2);
@@ -1280,9 +1269,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + dt * L.coef[lane] : 0.f;
         const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + dt * L.coef[64 + lane] : 0.f;
         (void)Sj; (void)Sj2;
-        if constexpr (HE_PRIO_DEL != 0) __builtin_amdgcn_s_setprio(HE_PRIO_DEL);
         crba_mfma(M, L, lane, dadd, dadd2);
-        if constexpr (HE_PRIO_DEL != 0) __builtin_amdgcn_s_setprio(kPrioDefault);
     }
     STAMP(4);
     // ---- sparse LTDL in registers (RBDA 6.5, deepest dof first); L leaves through LDS, packed
@@ -1836,11 +1823,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 if (lb & kGroupBodies[g]) live |= 1u << g;
             STAMP(8);
             // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
-            if constexpr (HE_PRIO_DEL != 0) __builtin_amdgcn_s_setprio(HE_PRIO_DEL);
             if (nr <= 32) delassus_mfma32(z, acol, live);  // wave-uniform
             else if (nr <= 48) delassus_mfma48(z, acol, live);
             else delassus_mfma(z, acol, live);
-            if constexpr (HE_PRIO_DEL != 0) __builtin_amdgcn_s_setprio(kPrioDefault);
         }
         STAMP(9);
         // ---- projected Gauss-Seidel over the rows (pgs_sweep): lane r keeps its unconstrained change,
@@ -1960,7 +1945,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             y2 = lane < NH ? (y2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
             float r1[regla::kRowRegs], r2[regla::kRowRegs];
             load_rows(L, T, lane, r1, r2);
-            if constexpr (HE_PRIO_DU != 0) __builtin_amdgcn_s_setprio(HE_PRIO_DU);
             solve_L(r1, r2, lane, yl, y2);
             __builtin_amdgcn_s_setprio(kPrioDefault);
             L.uf[lane] = L.u0[lane] + yl;
