@@ -2126,10 +2126,6 @@ __global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
     Lds& L = *reinterpret_cast<Lds*>(smem);
     const int e = blockIdx.x;
     if (e >= a.num_envs) return;  // the first-dispatch warm-up (warm_physics_kernels): no env
-#ifdef HE_DESYNC  // A/B: odd workgroups start later, so co-resident waves sit in different phases
-    if (e & 1)
-        for (int k = 0; k < HE_DESYNC; ++k) __builtin_amdgcn_s_sleep(127);
-#endif
     const int lane = threadIdx.x;
     const he_model& m = *a.model;
     // ---- body-level tree tables into LDS

@@ -10,9 +10,8 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 &&
 bash tools/gpu_r03_final.sh $TAG
 rc=$?
-# keep the summaries (kernel_stats, pmc_*.json), drop the raw per-dispatch CSVs: gpurun copies back <= 64 MiB
-find gpurun_out -name "*counter_collection.csv" -delete
-find gpurun_out -name "*kernel_trace.csv" -size +1M -delete
+# keep the summaries and the engine kernels' rows of the per-dispatch CSVs: gpurun copies back <= 64 MiB
+python tools/trim_csv.py gpurun_out
 du -sh gpurun_out
 grep -E "passed|failed" gpurun_out/gpu_tests_$TAG.log | tail -2
 tail -2 gpurun_out/smoke_$TAG.log

@@ -14,10 +14,13 @@ import csv
 import glob
 import json
 import os
+import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N_SIMD = 256 * 4
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_traffic import full_grid_mean  # noqa: E402
 
 
 def main():
@@ -33,10 +36,10 @@ def main():
             for row in csv.DictReader(fh):
                 for k in ("physics_kernel", "imitation_kernel"):
                     if k in row["Kernel_Name"]:
-                        acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                        acc[k][row["Counter_Name"]].append((int(row["Grid_Size"]), float(row["Counter_Value"])))
     res = {}
     for k, d in acc.items():
-        m = {c: sum(v) / len(v) for c, v in d.items()}
+        m = {c: full_grid_mean(v) for c, v in d.items()}
         cyc = m.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
         wc = m.get("SQ_WAVE_CYCLES", 0.0)
         res[k] = {"counters": {c: round(v, 1) for c, v in sorted(m.items())},
