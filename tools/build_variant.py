@@ -1,6 +1,7 @@
 """Diagnostics: build the engine library with extra -D flags on the physics TU into
 humanoid_amd/_variants/<name>.so, for A/B timing on one GPU box (HE_ENGINE_LIB=<path>).
-Usage: python tools/build_variant.py NAME [--tu he_imitation.hip] [-DFOO=1 ...]"""
+Usage: python tools/build_variant.py NAME [--tu he_imitation.hip] [-DFOO=1 ...] [-mllvm -opt ...]
+(an -amdgpu-sched-strategy= given here replaces the product's max-ilp)"""
 import os
 import subprocess
 import sys
@@ -19,7 +20,10 @@ def main():
     out_dir = os.path.join(ROOT, "humanoid_amd", "_variants")
     os.makedirs(out_dir, exist_ok=True)
     hipcc = B._hipcc()
-    flags = dict(B.SOURCES)[tu]
+    flags = list(dict(B.SOURCES)[tu])
+    if any(d.startswith("-amdgpu-sched-strategy=") for d in defs) and "-amdgpu-sched-strategy=max-ilp" in flags:
+        i = flags.index("-amdgpu-sched-strategy=max-ilp")  # a variant's strategy replaces the product's
+        del flags[i - 1:i + 1]
     obj = os.path.join(out_dir, name + "." + tu + ".o")
     cmd = [hipcc, "--offload-arch=" + B.ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"] + flags + defs + \
           ["-c", os.path.join(B.CSRC, tu), "-o", obj]

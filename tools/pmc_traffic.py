@@ -28,7 +28,7 @@ def per_kernel(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 acc[row["Kernel_Name"]].append((int(row["Grid_Size"]), float(row["Counter_Value"])))
-    return {k: full_grid_mean(v) for k, v in acc.items()}
+    return {k: (full_grid_mean(v), len(v)) for k, v in acc.items()}
 
 
 def full_grid_mean(rows):
@@ -56,16 +56,20 @@ def main():
     a = ap.parse_args()
     fetch = per_kernel(a.fetch_dir, "FETCH_SIZE")
     write = per_kernel(a.write_dir, "WRITE_SIZE")
-    kernels = {}
+    kernels, launches = {}, {}
     for name in set(fetch) | set(write):
         k = short(name)
-        if k is None:
+        n = max(fetch.get(name, (0.0, 0))[1], write.get(name, (0.0, 0))[1])
+        # instantiations sharing a short name (imitation_kernel<false> / <true>): the one the workload
+        # launches most
+        if k is None or n <= launches.get(k, 0):
             continue
-        fb = 2.0 * fetch.get(name, 0.0) * 1024.0  # KB -> B, x2 gfx950 read correction
-        wb = write.get(name, 0.0) * 1024.0
+        launches[k] = n
+        fb = 2.0 * fetch.get(name, (0.0, 0))[0] * 1024.0  # KB -> B, x2 gfx950 read correction
+        wb = write.get(name, (0.0, 0))[0] * 1024.0
         kernels[k] = {"fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
                       "hbm_bytes_per_launch": round(fb + wb),
-                      "hbm_bytes_per_env": round((fb + wb) / a.num_envs, 1)}
+                      "hbm_bytes_per_env": round((fb + wb) / a.num_envs, 1), "launches": n}
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     key = f"{a.config}:{a.num_envs}"
     out[key] = {"kernels": kernels,
