@@ -410,7 +410,6 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
     const bool act = lane < NB;
     const int b = act ? lane : 0;
     const he_imitation_params& p = a.p;
-    const int64_t mid = x.mid;
     f3 off = x.off;
     float start = x.start, soff = x.soff;
     int prog = x.prog;
