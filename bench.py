@@ -15,6 +15,7 @@ its own 4096 envs (envs are independent: no data-path collective), barrier + syn
 timed region, max time over ranks, value = total env-steps of all ranks / that time.
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -500,7 +501,9 @@ def main():
         if shared:
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # a rank that fails mid-collective ends the job in minutes, not at the driver's limit
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=datetime.timedelta(seconds=300))
     torch.cuda.set_device(local)
     model = load_default_model()
     ro = Rollout(args, model, local, rank)
