@@ -190,6 +190,40 @@ def test_imitation_step_matches_golden_and_oracle(he_model, golden):
     np.testing.assert_array_equal(term.cpu().numpy(), g["terminate_eval"])
 
 
+@pytest.mark.parametrize("n", [65, 4097])
+def test_imitation_step_ragged_launch_equals_golden_run(he_model, golden, n):
+    """The imitation kernel packs two envs per wave and eight per 256-lane block: a launch of 65 or
+    4,097 envs ends in a partial block and a half-filled wave. Env i of such a launch gets the golden
+    fixture's env i mod n_g (state, motion, time, progress) and must produce exactly the golden run's
+    outputs for that env (obs, reward, raw terms, reset / terminate, progress), bit for bit."""
+    g = golden("env_step")
+    ng = g["rb_state"].shape[0]
+
+    def run(idx):
+        m = len(idx)
+        eng = make_engine(he_model, m)
+        eng.load_motions(tables_from_golden(g))
+        eng.rb_state.copy_(cu(g["rb_state"][idx].reshape(m * 24, 13)))
+        eng.dof_state.view(m, 69, 2)[..., 1] = cu(g["dof_vel"][idx])
+        eng.dof_force.copy_(cu(g["dof_force"][idx].reshape(-1)))
+        prog = cu(g["progress_in"][idx], torch.int16)
+        em = eng.env_motion(cu(g["motion_ids"][idx], torch.int64), cu(g["start_times"][idx]),
+                            cu(g["start_offsets"][idx]), cu(g["global_offset"][idx]), prog)
+        out = [torch.zeros(m, 934, device="cuda:0"), torch.zeros(m, device="cuda:0"), torch.zeros(m, 5, device="cuda:0"),
+               torch.zeros(m, dtype=torch.uint8, device="cuda:0"), torch.zeros(m, dtype=torch.uint8, device="cuda:0")]
+        eng.imitation_step(_abi.imitation_params(), em, *out)
+        torch.cuda.synchronize()
+        res = [o.cpu().numpy() for o in out] + [prog.cpu().numpy()]
+        del eng
+        return res
+
+    ref = run(np.arange(ng))
+    idx = np.arange(n) % ng
+    got = run(idx)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b[idx])
+
+
 def test_reset_envs_matches_golden(he_model, golden):
     g = golden("env_reset")
     s = golden("env_step")
@@ -635,6 +669,62 @@ def test_physics_standing_matches_oracle(he_model, model):
     root, dof = cases.standing_state(model, 64, rng, xy_jitter=1.0)
     targets = np.zeros((64, 69), np.float32)
     _physics_compare(he_model, root, dof, targets, steps=5, max_skip=0.0, max_widened=0.05)
+
+
+def test_env_results_independent_of_env_count_and_position(he_model, model):
+    """Envs never interact: an env's step is a function of its own state, targets and
+    warm-start cache only, whatever the launch's env count and wherever the env sits in it. Eight
+    distinct states (standing, lying, airborne actuated, contact-rich) are stepped 3 policy steps
+    alone (N = 1 each), inside a ragged launch of 65 envs (one past a wave multiple) and inside a
+    launch of 32,768 envs (configs[3]'s eight ranks' worth on one GPU, the largest size tested):
+    root, dof, rigid-body rows, contact forces, dof forces and the warm-start cache bit-identical."""
+    rng = np.random.default_rng(29)
+    r1, d1 = cases.standing_state(model, 2, rng, xy_jitter=1.0)
+    r2, d2 = cases.lying_state(2, rng)
+    r3, d3 = cases.random_state(2, rng, height=(6.0, 7.0), ang=0.4, vel=0.5)
+    r4, d4 = cases.random_state(2, rng, height=(0.85, 1.0), ang=0.8, vel=0.5)
+    root = np.concatenate([r1, r2, r3, r4])
+    dof = np.concatenate([d1, d2, d3, d4])
+    tg = rng.uniform(-0.5, 0.5, (8, 69)).astype(np.float32)
+    tg[:2] = 0.0
+
+    def run(n, slots):
+        fill_r, fill_d = cases.random_state(n, np.random.default_rng(n), height=(0.85, 1.2), ang=0.8, vel=0.5)
+        fill_t = np.random.default_rng(n + 1).uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
+        fill_r[slots], fill_d[slots], fill_t[slots] = root, dof, tg
+        eng = make_engine(he_model, n)
+        eng.root_states.copy_(cu(fill_r))
+        eng.dof_state.copy_(cu(fill_d.reshape(n * 69, 2)))
+        eng.dof_targets.copy_(cu(fill_t))
+        for _ in range(3):
+            eng.simulate(2)
+        torch.cuda.synchronize()
+        sl = torch.as_tensor(slots, device=eng.device)
+        out = {k: getattr(eng, k).reshape(n, -1)[sl].cpu().numpy().copy()
+               for k in ("root_states", "dof_state", "rb_state", "contact_forces", "dof_force", "contact_cache")}
+        del eng
+        return out
+
+    alone = {k: [] for k in ("root_states", "dof_state", "rb_state", "contact_forces", "dof_force", "contact_cache")}
+    for i in range(8):
+        fill_r, fill_d = root[i:i + 1], dof[i:i + 1]
+        eng = make_engine(he_model, 1)
+        eng.root_states.copy_(cu(fill_r))
+        eng.dof_state.copy_(cu(fill_d.reshape(69, 2)))
+        eng.dof_targets.copy_(cu(tg[i:i + 1]))
+        for _ in range(3):
+            eng.simulate(2)
+        torch.cuda.synchronize()
+        for k in alone:
+            alone[k].append(getattr(eng, k).reshape(1, -1).cpu().numpy().copy())
+        del eng
+    alone = {k: np.concatenate(v) for k, v in alone.items()}
+    ragged = run(65, np.array([0, 1, 31, 32, 33, 62, 63, 64]))
+    large = run(32768, np.array([0, 4095, 4096, 8191, 16384, 20000, 32766, 32767]))
+    assert np.isfinite(alone["root_states"]).all()
+    for k in alone:
+        assert np.array_equal(alone[k], ragged[k]), f"{k}: N = 65 differs from N = 1"
+        assert np.array_equal(alone[k], large[k]), f"{k}: N = 32768 differs from N = 1"
 
 
 def test_physics_trajectories_30_steps(he_model, model):
