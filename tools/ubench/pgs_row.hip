@@ -8,7 +8,7 @@
 //   5 the change kept by a v_cmp of the lane id + v_cndmask
 //   6 ILP 2 without the v_writelane
 //   7 the v_writelane of row R issued in row R+1's block (after its v_med3), rows fenced by sched_barrier
-// Waves per SIMD from the grid: 1024 workgroups = 1 per SIMD, 2048 = 2 (the kernel's occupancy).
+// Waves per SIMD from the grid: 1024 workgroups = 1 per SIMD, 2048 = 2 (the kernel's occupancy), 3072 = 3, 4096 = 4.
 // Output: median cycles per row update over the waves (s_memtime around S sweeps of N rows).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -115,7 +115,7 @@ double run(int blocks, const float* din, float* dout, unsigned long long* dcyc) 
 }
 
 int main() {
-    const int maxb = 2048;
+    const int maxb = 4096;
     std::vector<float> h(2 * N * 64 + 256);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f;
     float *din, *dout;
@@ -124,7 +124,7 @@ int main() {
     hipMalloc(&dout, maxb * 64 * 4);
     hipMalloc(&dcyc, maxb * 8);
     hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice);
-    for (int b : {1024, 2048}) {
+    for (int b : {1024, 2048, 3072, 4096}) {
         printf("{\"waves_per_simd\": %d, \"form0_shipped\": %.1f, \"form1_no_writelane\": %.1f, \"form2_plain_fma\": %.1f, "
                "\"form3_ilp2_per_row\": %.1f, \"form4_mask_select\": %.1f, \"form5_cmp_select\": %.1f, "
                "\"form6_ilp2_no_writelane\": %.1f, \"form7_deferred_writelane\": %.1f}\n", b / 1024, run<0>(b, din, dout, dcyc), run<1>(b, din, dout, dcyc),
