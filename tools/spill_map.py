@@ -39,6 +39,8 @@ def main():
     for i, ln in enumerate(lines):
         if "Function Name:" in ln and "physics_kernel" in ln:
             for ln2 in lines[i + 1:i + 14]:
+                if "Function Name:" in ln2:
+                    break
                 m = re.search(r"remark:\s+([^:]+):\s+(\S+)", ln2)
                 if m:
                     report[m.group(1).strip()] = m.group(2)
