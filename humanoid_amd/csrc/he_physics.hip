@@ -1897,6 +1897,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float lo = isn ? -lamv : -bnd - lamv;
             float hi = isn ? kInf : bnd - lamv;
             const int nru = __builtin_amdgcn_readfirstlane(nr);
+            STAMP(22);  // the solve's set-up (warm-start residual, bounds, scaled columns) apart from its sweeps
             __builtin_amdgcn_s_setprio(kPrioSerial);
             const float tol = p.solver_tolerance;
             for (int it = 0; it < p.solver_iterations; ++it) {
@@ -2278,7 +2279,10 @@ __global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
 }  // namespace
 
 static_assert(sizeof(Lds) <= 20480, "two workgroups per SIMD (8 per CU) need <= 20 KB of LDS each");
-size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16; }
+#ifndef HE_LDS_EXTRA  // diagnostics only: extra dynamic LDS per wave, to run fewer waves per CU
+#define HE_LDS_EXTRA 0   // (one wave alone on its CU: tools/gpu_r04_o.sh)
+#endif
+size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16 + HE_LDS_EXTRA; }
 
 bool physics_phase_stamps() { return HE_PHASE_STAMPS != 0; }
 

@@ -19,8 +19,8 @@ PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba"
           "contact gen", "Z rows + L^-T", "delassus A", "pgs", "du solve + forces", "integrate", "final fk+write",
           "contact: limit slots", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
           "terrain: geometry (to P0/P1)", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
-          "free: prefetch + row loads", "free: L^-1 levels", "fused imitation",
-          "mid: um sweep", "mid: velocities + rnea", "mid: subtree + dc", "mid: L^-T"]  # slots 25-28: the midpoint bias; slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22-23 out of "free solve"
+          "pgs: set-up", "(unused)", "fused imitation",
+          "mid: um sweep", "mid: velocities + rnea", "mid: subtree + dc", "mid: L^-T"]  # slots 25-28: the midpoint bias; slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22 out of "pgs" (its set-up before the sweeps)
 
 
 def main():

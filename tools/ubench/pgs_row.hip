@@ -8,6 +8,8 @@
 //   5 the change kept by a v_cmp of the lane id + v_cndmask
 //   6 ILP 2 without the v_writelane
 //   7 the v_writelane of row R issued in row R+1's block (after its v_med3), rows fenced by sched_barrier
+//   8 form 0 under s_setprio 3 (the kernel's PGS priority)
+//   9 form 0 with every row's change through one SGPR pair s[6:7], as the kernel's allocator does
 // Waves per SIMD from the grid: 1024 workgroups = 1 per SIMD, 2048 = 2 (the kernel's occupancy), 3072 = 3, 4096 = 4.
 // Output: median cycles per row update over the waves (s_memtime around S sweeps of N rows).
 #include <hip/hip_runtime.h>
@@ -59,8 +61,28 @@ __device__ __forceinline__ void row(f2v& ch, float& lo, float& dvec, const f2v (
             ch = __builtin_elementwise_fma(ak[R], f2v{d, d}, ch);
         }
         lo = fmaf(-ak[R].y, d, lo);
-        if constexpr (V == 0 || V == 2) dvec = wrlane<R>(d, dvec);
+        if constexpr (V == 0 || V == 2 || V == 8) dvec = wrlane<R>(d, dvec);
         row<V, R + 1>(ch, lo, dvec, ak);
+    }
+}
+// form 9: the shipped row with every row's change through the same SGPR pair s[6:7] (as the kernel's
+// allocator does), written as one asm block per row with the compiler's hazard nops
+template <int R>
+__device__ __forceinline__ void row9(f2v& ch, float& lo, float& dvec, const f2v (&ak)[N]) {
+    if constexpr (R < N) {
+        float m;
+        asm volatile(
+            "v_med3_f32 %[m], %[cx], %[lo], %[cy]\n"
+            "s_nop 0\n"
+            "v_readlane_b32 s6, %[m], %[r]\n"
+            "v_writelane_b32 %[dv], s6, %[r]\n"
+            "s_nop 1\n"
+            "v_pk_fma_f32 %[ch], %[ak], s[6:7], %[ch] op_sel_hi:[1,0,1]\n"
+            "v_fma_f32 %[lo], -%[aky], s6, %[lo]"
+            : [m] "=&v"(m), [ch] "+v"(ch), [lo] "+v"(lo), [dv] "+v"(dvec)
+            : [cx] "v"(ch.x), [cy] "v"(ch.y), [ak] "v"(ak[R]), [aky] "v"(ak[R].y), [r] "i"(R)
+            : "s6", "s7");
+        row9<R + 1>(ch, lo, dvec, ak);
     }
 }
 template <int R, bool WL>
@@ -90,9 +112,11 @@ __global__ void __launch_bounds__(64) k(const float* in, float* out, unsigned lo
     f2v ch = {in[l] * 0.1f, 1e30f}, ch2 = {in[64 + l] * 0.1f, 1e30f};
     float lo = -1.f, lo2 = -1.f, dv = 0.f, dv2 = 0.f;
     __builtin_amdgcn_s_waitcnt(0);
+    if constexpr (V == 8) __builtin_amdgcn_s_setprio(3);  // form 8: form 0 under the kernel's PGS priority
     const unsigned long long t0 = __builtin_readcyclecounter();
     for (int s = 0; s < S; ++s) {
-        if constexpr (V == 3) row2<0, true>(ch, lo, dv, ch2, lo2, dv2, ak);
+        if constexpr (V == 9) row9<0>(ch, lo, dv, ak);
+        else if constexpr (V == 3) row2<0, true>(ch, lo, dv, ch2, lo2, dv2, ak);
         else if constexpr (V == 6) row2<0, false>(ch, lo, dv, ch2, lo2, dv2, ak);
         else if constexpr (V == 7) row7<0>(ch, lo, dv, 0.f, ak);
         else row<V, 0>(ch, lo, dv, ak);
@@ -127,9 +151,11 @@ int main() {
     for (int b : {1024, 2048, 3072, 4096}) {
         printf("{\"waves_per_simd\": %d, \"form0_shipped\": %.1f, \"form1_no_writelane\": %.1f, \"form2_plain_fma\": %.1f, "
                "\"form3_ilp2_per_row\": %.1f, \"form4_mask_select\": %.1f, \"form5_cmp_select\": %.1f, "
-               "\"form6_ilp2_no_writelane\": %.1f, \"form7_deferred_writelane\": %.1f}\n", b / 1024, run<0>(b, din, dout, dcyc), run<1>(b, din, dout, dcyc),
+               "\"form6_ilp2_no_writelane\": %.1f, \"form7_deferred_writelane\": %.1f, \"form8_setprio3\": %.1f, "
+               "\"form9_one_sgpr_pair\": %.1f}\n", b / 1024, run<0>(b, din, dout, dcyc), run<1>(b, din, dout, dcyc),
                run<2>(b, din, dout, dcyc), run<3>(b, din, dout, dcyc) / 2.0, run<4>(b, din, dout, dcyc),
-               run<5>(b, din, dout, dcyc), run<6>(b, din, dout, dcyc) / 2.0, run<7>(b, din, dout, dcyc));
+               run<5>(b, din, dout, dcyc), run<6>(b, din, dout, dcyc) / 2.0, run<7>(b, din, dout, dcyc),
+               run<8>(b, din, dout, dcyc), run<9>(b, din, dout, dcyc));
     }
     return 0;
 }
