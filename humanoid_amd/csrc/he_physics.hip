@@ -106,6 +106,9 @@ HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
 // optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
 // s_memtime deltas per phase into stamps[block * HE_STAMP_SLOTS + phase] with a no-return vector
 // atomic add (a load-add-store would put one global round trip into every phase it opens)
+#ifndef HE_RL4  // A/B (round 4): dot-product broadcasts four lanes per block (regla::rdlane4)
+#define HE_RL4 0
+#endif
 #ifndef HE_PHASE_STAMPS
 #define HE_PHASE_STAMPS 0  // diagnostic twin library only (build.py PHASES_LIB)
 #endif
@@ -1811,9 +1814,21 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                // hoist into registers at the phase's register peak)
                 const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
                 float yacc[4] = {0.f, 0.f, 0.f, 0.f};
+#if HE_RL4
+                regla::static_for<0, NG, 4>([&](auto ic) {
+                    constexpr int i0 = decltype(ic)::value;
+                    float sv[4];
+                    if constexpr (i0 < 64) regla::rdlane4<i0>(yhl, sv);
+                    else regla::rdlane4<i0 - 64>(yh2, sv);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (i0 + q < NG) yacc[(i0 + q) & 3] = fmaf(ZV(z, i0 + q), sv[q], yacc[(i0 + q) & 3]);
+                });
+#else
 #pragma unroll
                 for (int i = 0; i < NG; ++i)
                     yacc[i & 3] = fmaf(ZV(z, i), regla::rdlane(i < 64 ? yhl : yh2, i & 63), yacc[i & 3]);
+#endif
                 brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
             }
             // dof groups of four touching a support body (wave-uniform, from lb)
@@ -1838,8 +1853,19 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 auto aw = [&](auto nrows) {  // four independent accumulation chains
                     constexpr int NRW = decltype(nrows)::value;
                     float wa[4] = {0.f, 0.f, 0.f, 0.f};
+#if HE_RL4
+                    regla::static_for<0, NRW, 4>([&](auto rc) {
+                        constexpr int r0 = decltype(rc)::value;
+                        float sv[4];
+                        regla::rdlane4<r0>(lam0, sv);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (r0 + q < NRW) wa[(r0 + q) & 3] = fmaf(acol[r0 + q], sv[q], wa[(r0 + q) & 3]);
+                    });
+#else
 #pragma unroll
                     for (int r = 0; r < NRW; ++r) wa[r & 3] = fmaf(acol[r], regla::rdlane(lam0, r), wa[r & 3]);
+#endif
                     w0 += (wa[0] + wa[1]) + (wa[2] + wa[3]);
                 };
                 if (nr <= 16) aw(std::integral_constant<int, 16>{});

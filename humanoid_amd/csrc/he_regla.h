@@ -41,6 +41,30 @@ __device__ __forceinline__ float rdlane(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+// lanes L .. L+3 of v into four SGPRs in one block: the allocator otherwise routes every broadcast of
+// a dot product through one SGPR, each behind its own hazard nop, and the products serialise
+template <int L>
+__device__ __forceinline__ void rdlane4(float v, float (&s)[4]) {
+    asm volatile(
+        "s_nop 0\n"
+        "v_readlane_b32 %0, %4, %5\n"
+        "v_readlane_b32 %1, %4, %6\n"
+        "v_readlane_b32 %2, %4, %7\n"
+        "v_readlane_b32 %3, %4, %8\n"
+        "s_nop 1"
+        : "=s"(s[0]), "=s"(s[1]), "=s"(s[2]), "=s"(s[3])
+        : "v"(v), "i"(L), "i"(L + 1), "i"(L + 2), "i"(L + 3));
+}
+
+// f(integral_constant<I>) for I = I0, I0 + STEP, ... < N (compile-time lane indices for rdlane4)
+template <int I0, int N, int STEP, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I0 < N) {
+        f(std::integral_constant<int, I0>{});
+        static_for<I0 + STEP, N, STEP>(f);
+    }
+}
+
 // v_writelane: `v` on lane `l` only
 template <int LANE>
 __device__ __forceinline__ float wrlane(float v, float old) {
