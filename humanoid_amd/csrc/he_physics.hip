@@ -106,9 +106,6 @@ HE_DEV int dof_body(int i) { return i < 6 ? 0 : (i - 6) / 3 + 1; }
 // optional per-phase cycle stamps (diagnostic: PhysArgs.stamps != null), lane 0 accumulates
 // s_memtime deltas per phase into stamps[block * HE_STAMP_SLOTS + phase] with a no-return vector
 // atomic add (a load-add-store would put one global round trip into every phase it opens)
-#ifndef HE_RL4  // A/B (round 4): dot-product broadcasts four lanes per block (regla::rdlane4)
-#define HE_RL4 0
-#endif
 #ifndef HE_PHASE_STAMPS
 #define HE_PHASE_STAMPS 0  // diagnostic twin library only (build.py PHASES_LIB)
 #endif
@@ -1811,10 +1808,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(ZV(z, i), ZV(z, i), dacc[i & 3]);
             diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
             {  // J_r (uf - u0) = zh_r . yh, yh_i broadcast from lane i (v_readlane: no LDS loads to
-               // hoist into registers at the phase's register peak)
+               // hoist into registers at the phase's register peak), four lanes per block into four
+               // SGPRs (one hazard nop per block; through one SGPR the 75 products serialised:
+               // this phase -10 %, the launch -0.5 % by A/B, bit-identical, round 4)
                 const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
                 float yacc[4] = {0.f, 0.f, 0.f, 0.f};
-#if HE_RL4
                 regla::static_for<0, NG, 4>([&](auto ic) {
                     constexpr int i0 = decltype(ic)::value;
                     float sv[4];
@@ -1824,11 +1822,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     for (int q = 0; q < 4; ++q)
                         if (i0 + q < NG) yacc[(i0 + q) & 3] = fmaf(ZV(z, i0 + q), sv[q], yacc[(i0 + q) & 3]);
                 });
-#else
-#pragma unroll
-                for (int i = 0; i < NG; ++i)
-                    yacc[i & 3] = fmaf(ZV(z, i), regla::rdlane(i < 64 ? yhl : yh2, i & 63), yacc[i & 3]);
-#endif
                 brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
             }
             // dof groups of four touching a support body (wave-uniform, from lb)
@@ -1850,10 +1843,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             // residual at the warm start: w = brow + A lambda0 (acol: lane c holds A[r][c] = A[c][r])
             float w0 = brow;
             if (__ballot(lam0 != 0.f)) {  // wave-uniform; rows >= nr hold no impulse
-                auto aw = [&](auto nrows) {  // four independent accumulation chains
+                auto aw = [&](auto nrows) {  // four independent accumulation chains, broadcasts in blocks of 4
                     constexpr int NRW = decltype(nrows)::value;
                     float wa[4] = {0.f, 0.f, 0.f, 0.f};
-#if HE_RL4
                     regla::static_for<0, NRW, 4>([&](auto rc) {
                         constexpr int r0 = decltype(rc)::value;
                         float sv[4];
@@ -1862,10 +1854,6 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                         for (int q = 0; q < 4; ++q)
                             if (r0 + q < NRW) wa[(r0 + q) & 3] = fmaf(acol[r0 + q], sv[q], wa[(r0 + q) & 3]);
                     });
-#else
-#pragma unroll
-                    for (int r = 0; r < NRW; ++r) wa[r & 3] = fmaf(acol[r], regla::rdlane(lam0, r), wa[r & 3]);
-#endif
                     w0 += (wa[0] + wa[1]) + (wa[2] + wa[3]);
                 };
                 if (nr <= 16) aw(std::integral_constant<int, 16>{});

@@ -334,10 +334,7 @@ constexpr ElimGroups<kElimGroupMax> kElimGroups{};
 // ancestor offset, clamped into the factor) while group G's pivots are broadcast and applied, so a
 // group (of at most 4 pivots) pays its readlanes and FMAs but not an LDS round trip. The update
 // stays exec-masked to the pivot's ancestor lanes.
-#ifndef HE_LT_GROUP
-#define HE_LT_GROUP 4
-#endif
-constexpr ElimGroups<HE_LT_GROUP> kLTPipeGroups{};
+constexpr ElimGroups<4> kLTPipeGroups{};
 template <int G>
 struct LTGroup {
     static constexpr int S0 = G < kLTPipeGroups.count ? kLTPipeGroups.start[G] : 0;
