@@ -549,12 +549,6 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
 #endif
 }
 
-template <bool EVAL>
-HE_DEV void imitation_group(const ImitArgs& a, int slot, int e, int lane, bool leader, int64_t mid, f3 off, float start,
-                            float soff, int prog, SimBody s, float pw) {
-    imitation_finish<EVAL>(a, slot, e, lane, leader, imitation_ref(a, lane, mid, off, start, soff, prog), s, pw);
-}
-
 // the power-reward term of joint `lane` (humanoid_phc.py:1297-1305): |tau . qdot| over its 3 dofs,
 // f = the joint's 3 dof forces, v = its 3 dof velocities (stride vs between them)
 HE_DEV float power_term(const float* f, const float* v, int vs) {

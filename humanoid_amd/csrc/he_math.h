@@ -14,7 +14,6 @@
 struct f3 { float x, y, z; };
 struct f4 { float x, y, z, w; };
 
-HE_DEV f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
 HE_DEV f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 HE_DEV f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 HE_DEV f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
@@ -141,20 +140,6 @@ HE_DEV f4 qnormalize(f4 q) {
     if (n2 < 1e-24f) return f4{0.f, 0.f, 0.f, 1.f};
     float r = rsqrtf(n2);
     return f4{q.x * r, q.y * r, q.z * r, q.w * r};
-}
-HE_DEV f4 qexp(f3 v) {
-    float th = norm3(v);
-    if (th < 1e-8f) return qnormalize(f4{0.5f * v.x, 0.5f * v.y, 0.5f * v.z, 1.f});
-    float s = sinf(0.5f * th) / th;
-    return f4{v.x * s, v.y * s, v.z * s, cosf(0.5f * th)};
-}
-HE_DEV f3 qlog(f4 q) {
-    if (q.w < 0.f) q = qneg(q);
-    float s = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
-    if (s < 1e-8f) return f3{2.f * q.x, 2.f * q.y, 2.f * q.z};
-    float th = 2.f * atan2f(s, q.w);
-    float k = th / s;
-    return f3{q.x * k, q.y * k, q.z * k};
 }
 // rotation matrix columns of q
 HE_DEV void qcols(f4 q, f3& c0, f3& c1, f3& c2) {

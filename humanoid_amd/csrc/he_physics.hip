@@ -494,38 +494,6 @@ HE_DEV void delassus_mfma(const regla::ZVec& z, float (&acol)[MAXR], uint32_t li
     }
 }
 
-// Delassus column entries A[RR][lane] for RR < nr, one row per step (constant register indices);
-// dof groups without a nonzero entry in any row are skipped
-template <int RR>
-HE_DEV void delassus_rows(const regla::ZVec& z, float (&acol)[MAXR], int nr, uint32_t live) {
-    // four rows at a time: four independent accumulation chains, and each v_readlane has three
-    // other instructions before its SGPR is consumed (no hazard s_nop)
-    if constexpr (RR < MAXR) {
-        if (RR >= nr) return;
-        constexpr int NQ = MAXR - RR < 4 ? MAXR - RR : 4;
-        float acc[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
-#pragma unroll
-        for (int g = 0; g < NGRP; ++g) {
-            if ((live >> g) & 1u) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int i = 4 * g + k < NG ? 4 * g + k : 0;
-                    if (4 * g + k < NG) {
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) acc[q] = fmaf(regla::rdlane(ZV(z, i), RR + q), ZV(z, i), acc[q]);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acol[RR + q] = acc[q];  // rows >= nr come out 0 (their lanes hold z = 0)
-        __builtin_amdgcn_sched_barrier(0);
-        delassus_rows<RR + NQ>(z, acol, nr, live);
-    }
-}
-
 // One Gauss-Seidel sweep, branch-free: every row up to a compile-time class bound N (16, 32, 48,
 // 63) by the row count, with no per-row row-count branch (a row-count exit every 4 rows); rows nr..N-1 are empty rows (zero columns and
 // bound weights in every lane, zero cd and bounds in their own lanes: a +-0 change).
@@ -1830,7 +1798,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             for (int g = 0; g < NGRP; ++g)
                 if (lb & kGroupBodies[g]) live |= 1u << g;
             STAMP(8);
-            // ---- Delassus columns by v_readlane: A[r][c] = sum_i zh_r[i] zh_c[i]
+            // ---- Delassus columns on the matrix cores: A[r][c] = sum_i zh_r[i] zh_c[i]
             if (nr <= 32) delassus_mfma32(z, acol, live);  // wave-uniform
             else if (nr <= 48) delassus_mfma48(z, acol, live);
             else delassus_mfma(z, acol, live);

@@ -403,7 +403,7 @@ struct PivotStep {
     Row<kDofNanc[K] - 1> row;
 };
 // A: pivot and reciprocal; the scaled entry L[K][j] goes to a fresh register, M keeps the unscaled
-// H[K][j] as the broadcast operand of the updates until grp_update
+// H[K][j] as the broadcast operand of the updates until grp_finish
 template <int K>
 __device__ __forceinline__ void grp_pivot(const RegMat& M, PivotStep<K>& st) {
     st.dk = get<K, K>(M);
@@ -430,67 +430,10 @@ __device__ __forceinline__ void grp_store(const PivotStep<K>& st, float* Lp, int
         }
     }
 }
-// C + D: row broadcast (in-order LDS: sees the stores of B), the ancestor updates, then row K of M
-// becomes L[K][.]
-template <int K>
-__device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st);
-// H[I][j] -= L[K][I] * H[K][j] over I in chain(K) (row entries from the LDS broadcast, H[K][j]
-// unscaled on lane j, read in place from M). Chain positions X, X+1 holding dofs I, I+1 with X and
-// I even share both a row register pair and a column register pair: one v_pk_fma_f32, with H[K][j]
-// taken from half (K & 1) of K's column pair for both products.
-template <int K, int X, int D>
-__device__ __forceinline__ void fac_anc_pk(RegMat& M, const Row<D>& row) {
-    if constexpr (X < D) {
-        constexpr int I = kChain[K][X];
-        constexpr bool PAIR = X % 2 == 0 && X + 1 < D && I % 2 == 0 && I + 1 < 64 &&
-                              kChain[K][X + 1 < kMaxChain ? X + 1 : 0] == I + 1;
-        const f4v v = row.v[X / 4];
-        if constexpr (PAIR) {
-            const f2v l = X % 4 == 0 ? __builtin_shufflevector(v, v, 0, 1) : __builtin_shufflevector(v, v, 2, 3);
-            pk_fnma<K & 1>(M.cp[I >> 1], l, M.cp[K >> 1]);
-            fac_anc_pk<K, X + 2, D>(M, row);
-        } else {
-            const float l = (X % 4 == 0) ? v.x : ((X % 4 == 1) ? v.y : ((X % 4 == 2) ? v.z : v.w));
-            float c = mc<I>(M);
-            fnma(c, l, mc<K>(M));  // ordered: keeps the row's registers short-lived
-            mc_set<I>(M, c);
-            if constexpr (I >= 64) {
-                float c2 = mc2<I - 64>(M);
-                fnma(c2, l, mc2<K >= 64 ? K - 64 : 0>(M));
-                mc2_set<I - 64>(M, c2);
-            }
-            fac_anc_pk<K, X + 1, D>(M, row);
-        }
-    }
-}
-// the same updates with L[K][I] read straight from lane I (v_readlane into SGPRs, a pair per
-// v_pk_fma_f32) instead of the LDS store -> broadcast round trip; the packed store of row K still
-// happens (the later sweeps read it) but nothing here waits for it
-__device__ __forceinline__ void pk_fnma_s0(f2v& z, f2v a, f2v b) {  // z -= a * b.x, a in SGPRs
-    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "+v"(z) : "s"(a), "v"(b));
-}
-__device__ __forceinline__ void pk_fnma_s1(f2v& z, f2v a, f2v b) {  // z -= a * b.y, a in SGPRs
-    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
-                 : "+v"(z) : "s"(a), "v"(b));
-}
 template <int K, int I>
 __device__ __forceinline__ float lrow(const PivotStep<K>& st) {  // L[K][I], wave-uniform
     if constexpr (I < 64) return rdlane(st.l, I);
     else return rdlane(st.l2, I >= 64 ? I - 64 : 0);
-}
-// off: the elimination phase itself is ~8% shorter with it, but its ~1200 v_readlane per factor
-// take issue slots from the partner wave and the launch is 1.3% slower (A/B, r01)
-template <int K>
-__device__ __forceinline__ void grp_update(RegMat& M, float& Dl, float& D2, const PivotStep<K>& st) {
-    if constexpr (kDofNanc[K] - 1 > 0) fac_anc_pk<K, 0, kDofNanc[K] - 1>(M, st.row);
-    mc_set<K>(M, st.l);  // row K -> L[K][.] on lanes j < K
-    if constexpr (K >= 64) mc2_set<K - 64>(M, st.l2);
-    if constexpr (K < 64) Dl = wrlane<K>(st.dk, Dl);
-    else D2 = wrlane<K - 64>(st.dk, D2);
-}
-template <int K>
-__device__ __forceinline__ void grp_load(const float* Lp, PivotStep<K>& st) {
-    if constexpr (kDofNanc[K] - 1 > 0) st.row = load_row<K>(Lp, kPackStart[K]);
 }
 // ---------------------------------------------------------------- software-pipelined groups
 // The next group's pivots only wait for the updates of their own rows. Those rows (I in chain(K)
