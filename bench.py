@@ -272,9 +272,18 @@ def parity_record():
     with open(files[-1]) as f:
         rec = json.load(f)
     keep = ("joint_pose_l2_vs_oracle_rad", "com_err_vs_oracle_m", "envs", "steps", "envs_with_event",
-            "env_steps_before_event")
+            "env_steps_before_event", "post_event")
     out = {k: rec[k] for k in keep if k in rec}
     out["source"] = os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    # the record belongs to this build only if it was measured with the same device code
+    from humanoid_amd import build as B
+    from humanoid_amd.engine import LIB_PATH
+    try:
+        here = B.device_code_id(os.environ.get("HE_ENGINE_LIB") or LIB_PATH)
+    except Exception:
+        here = None
+    out["device_code"] = {"record": rec.get("device_code"), "loaded": here,
+                          "status": "current" if rec.get("device_code") and rec.get("device_code") == here else "stale"}
     return out
 
 
@@ -549,6 +558,12 @@ def main():
         a1, a2, _ = kernel_pass(EV_STEPS // 2)
         split = (float(np.median(a1)), float(np.median(a2)))
         ro.set_fused(True)
+    # the headline's max-over-ranks time is settled before any optional leg runs a collective: a leg
+    # that fails on one rank cannot then pair its collectives with this reduction
+    if world > 1:
+        t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     # configs[3]'s learner slice on every rank (RCCL; a one-rank RCCL group at N = 1)
     learner = None
     if not args.no_learner and args.num_envs == 4096:
@@ -556,10 +571,14 @@ def main():
             learner = learner_leg(args, model, local)
         except Exception as exc:  # report, never fake
             learner = {"value": None, "error": repr(exc)}
-    if world > 1:
-        t = torch.tensor([elapsed], device="cpu" if shared else "cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        if world > 1:  # every rank learns whether any rank's leg failed; the report says so
+            try:
+                ok = torch.tensor([0 if "error" in learner else 1], device="cpu" if shared else "cuda")
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) == 0 and "error" not in learner:
+                    learner = {"value": None, "error": "the learner leg failed on another rank"}
+            except Exception as exc:
+                learner = {"value": None, "error": "rank agreement after the learner leg: " + repr(exc)}
     n = args.num_envs
     total_steps = n * args.steps * world
     value = total_steps / elapsed

@@ -125,5 +125,31 @@ def build(force=False, verbose=False):
     return LIB
 
 
+def device_code_id(lib=LIB):
+    """sha256[:16] of the library's embedded device code (the ELF `.hip_fatbin` section: every gfx950
+    code object linked in). Host-only changes leave it equal; any kernel change moves it. Measurement
+    records (tests/test_full_size.py) store it, and bench.py reports a record as stale when it does not
+    match the library it loaded."""
+    import hashlib
+    import struct
+    with open(lib, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise RuntimeError(f"{lib}: not an ELF64 file")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def sec(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise RuntimeError(f"{lib}: no .hip_fatbin section")
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -167,6 +168,8 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     if (num_envs <= 0) return fail("he_create_envs: num_envs must be positive");
     if (h->num_envs) return fail("he_create_envs: envs already created");
     HE_CHECK(hipSetDevice(h->device));
+    // before any allocation: a failed warm-up leaves nothing behind to leak or re-allocate
+    if (warm_kernels(h->device)) return 1;
     const int N = num_envs;
     HE_CHECK(dalloc(&h->root, (size_t)N * 13));
     HE_CHECK(dalloc(&h->dof_state, (size_t)N * HE_NUM_DOF * 2));
@@ -200,7 +203,6 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     HE_CHECK(hipMemset(h->cache, 0, (size_t)N * HE_CACHE_WORDS * sizeof(float)));
     HE_CHECK(dalloc(&h->meta_cache, (size_t)N * 8));
     HE_CHECK(hipMemset(h->meta_cache, 0xFF, (size_t)N * 8 * sizeof(int32_t)));  // motion -1: empty
-    if (warm_kernels(h->device)) return 1;
     h->num_envs = N;
     return 0;
 }
@@ -268,13 +270,20 @@ static int copy_rows(float* dst, const float* src, const int32_t* ids, int k, in
 }
 }  // namespace
 
-// Every kernel's one-time first-dispatch cost (~0.4-0.8 ms per kernel on the MI355X; 16-30 ms under
-// rocprofv3's kernel tracing) paid once per process and device at env creation, instead of by the
-// setup's first full reset or by a timed step (he_kernels.h: warm_*_kernels).
+// The env step's kernels (physics, imitation, motion ingestion, indexed row copies) each pay a
+// one-time first-dispatch cost (~0.4-0.8 ms per kernel on the MI355X; 16-30 ms under rocprofv3's
+// kernel tracing), paid here once per process and device at env creation, instead of by the setup's
+// first full reset or by a timed step (he_kernels.h: warm_*_kernels). The rollout handoff kernels
+// (he_rollout.hip, include/humanoid_rollout.h) are not on the env step and are not warmed: they pay
+// theirs at the first Experience store. Serialised by a mutex (engines may be created from several
+// threads); a failed warm-up is not recorded, so the next he_create_envs retries it.
 static int warm_kernels(int device) {
+    static std::mutex mu;
     static bool warmed[64] = {};
     const int wm = std::getenv("HE_WARM_MODE") ? std::atoi(std::getenv("HE_WARM_MODE")) : 2;
-    if (wm <= 0 || device < 0 || device >= 64 || warmed[device]) return 0;
+    if (wm <= 0 || device < 0 || device >= 64) return 0;
+    std::lock_guard<std::mutex> lock(mu);
+    if (warmed[device]) return 0;
     if (wm == 2) {
         copy_rows_kernel<<<1, 256>>>(nullptr, nullptr, nullptr, 0, 1, 0);
         HE_CHECK(hipGetLastError());

@@ -2262,7 +2262,7 @@ __global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
 
 static_assert(sizeof(Lds) <= 20480, "two workgroups per SIMD (8 per CU) need <= 20 KB of LDS each");
 #ifndef HE_LDS_EXTRA  // diagnostics only: extra dynamic LDS per wave, to run fewer waves per CU
-#define HE_LDS_EXTRA 0   // (one wave alone on its CU: tools/gpu_r04_o.sh)
+#define HE_LDS_EXTRA 0   // (one wave alone on its CU; round 4)
 #endif
 size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16 + HE_LDS_EXTRA; }
 

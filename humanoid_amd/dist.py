@@ -135,6 +135,7 @@ class GradBuckets:
                 self.buckets.append((flat, bucket))
         self._pending = [0] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
+        self._next = 0  # the next bucket to launch (index order)
         self.calls = 0
         self.overlap = bool(overlap) and self.active
         self._hooks = []
@@ -143,12 +144,22 @@ class GradBuckets:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._ready))
 
     def _ready(self, p):
+        """A parameter's gradient is final. Buckets are launched in index order only (as DDP does):
+        a complete bucket waits for every bucket before it, so all ranks issue their collectives in
+        the same order even when some parameter gets no gradient on some ranks (its bucket is then
+        launched by :meth:`finish`, after every earlier one). Contract: one ``backward()`` per
+        :meth:`finish` -- a second backward (gradient accumulation) would add into a buffer whose
+        all-reduce is in flight, and raises here instead."""
         import torch.distributed as dist
         b = self._bucket_of[p]
+        if self._handles[b] is not None or self._pending[b] >= len(self.buckets[b][1]):
+            raise RuntimeError("GradBuckets: a gradient arrived for a bucket already complete or in flight "
+                               "(one backward() per finish(); no gradient accumulation across backward calls)")
         self._pending[b] += 1
-        if self._pending[b] == len(self.buckets[b][1]):
-            self._handles[b] = dist.all_reduce(self.buckets[b][0], group=self.group, async_op=True)
+        while self._next < len(self.buckets) and self._pending[self._next] == len(self.buckets[self._next][1]):
+            self._handles[self._next] = dist.all_reduce(self.buckets[self._next][0], group=self.group, async_op=True)
             self.calls += 1
+            self._next += 1
 
     def check_views(self):
         for flat, ps in self.buckets:
@@ -179,6 +190,7 @@ class GradBuckets:
         self.calls = 0
         self._pending = [0] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
+        self._next = 0
         return n
 
     def remove(self):

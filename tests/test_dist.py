@@ -114,7 +114,40 @@ def _bucket_worker(rank, world, port, q):
                 ok = ok and torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-7)
             opt_r.step()
             opt_m.step()
-        q.put((rank, ok, calls, len(gb.buckets)))
+        # one backward() per finish(): a second backward before finish() raises instead of adding
+        # into buffers whose all-reduce is in flight
+        opt_m.zero_grad(set_to_none=False)
+        mine(xs[0]).square().mean().backward()
+        try:
+            mine(xs[1]).square().mean().backward()
+            refused = False
+        except RuntimeError as exc:
+            refused = "one backward() per finish()" in str(exc)
+        gb.finish()
+        # a parameter with no gradient on one rank (a branch rank 1 skips): the buckets still go out in
+        # index order on both ranks (no hang), and the average matches allreduce_gradients
+        torch.manual_seed(1)
+        trunk, branch = torch.nn.Linear(40, 64), torch.nn.Linear(64, 64)
+        head = torch.nn.Linear(64, 3)
+        net = torch.nn.ModuleList([trunk, branch, head])
+        ref2 = [p.detach().clone().requires_grad_(True) for p in net.parameters()]
+        gb2 = hd.GradBuckets(net.parameters(), bucket_bytes=2048, overlap=True)
+        h = trunk(xs[0])
+        if rank == 0:
+            h = branch(h)
+        head(h).square().mean().backward()
+        gb2.finish()
+        pr = dict(zip(["tw", "tb", "bw", "bb", "hw", "hb"], ref2))
+        h = xs[0] @ pr["tw"].T + pr["tb"]
+        if rank == 0:
+            h = h @ pr["bw"].T + pr["bb"]
+        (h @ pr["hw"].T + pr["hb"]).square().mean().backward()
+        for t in ref2:
+            if t.grad is None:
+                t.grad = torch.zeros_like(t)
+        hd.allreduce_gradients(ref2)
+        skip_ok = all(torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-7) for a, b in zip(ref2, net.parameters()))
+        q.put((rank, ok and refused and skip_ok, calls, len(gb.buckets)))
         dist.destroy_process_group()
     except Exception:
         import traceback

@@ -109,6 +109,11 @@ def _record(name, obj):
     d = os.environ.get("HE_RECORD_DIR")
     if d:
         import json
+        from humanoid_amd import build as B
+        from humanoid_amd.engine import LIB_PATH
+        # the device code the record was measured with (bench.py reports a record whose id differs
+        # from the library it loaded as stale)
+        obj = dict(obj, device_code=B.device_code_id(os.environ.get("HE_ENGINE_LIB") or LIB_PATH))
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, name + ".json"), "w") as f:
             json.dump(obj, f, indent=1)

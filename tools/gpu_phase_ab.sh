@@ -1,7 +1,7 @@
 #!/bin/bash
 # Phase profiles of stamp-build variants (tools/build_variant.py NAME -DHE_PHASE_STAMPS=1 ...),
 # interleaved, 2 passes: per-wave cycles by phase, so a change inside one phase is resolved
-# below the bench's box noise. Usage: bash tools/gpu_r04_p.sh NAME... (humanoid_amd/_variants/NAME.so)
+# below the bench's box noise. Usage: bash tools/gpu_phase_ab.sh NAME... (humanoid_amd/_variants/NAME.so)
 set -o pipefail
 mkdir -p gpurun_out
 for pass in 1 2; do

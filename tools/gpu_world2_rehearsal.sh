@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp HE_BENCH_SHARED_DEVICE=1
 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
-  bench.py --gpus 2 --steps 20 --warmup 5 > gpurun_out/bench_world2_r04.log 2>&1
+  bench.py --gpus 2 --steps 20 --warmup 5 > gpurun_out/bench_world2.log 2>&1
 rc=$?
-grep "^{" gpurun_out/bench_world2_r04.log | cut -c1-1500
+grep "^{" gpurun_out/bench_world2.log | cut -c1-1500
 exit $rc
