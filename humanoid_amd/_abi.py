@@ -63,6 +63,7 @@ class HeSimParams(C.Structure):
         ("terrain_slope", C.c_float), ("step_height", C.c_float), ("step_length", C.c_float),
         ("joint_limits", C.c_int32), ("limit_margin", C.c_float), ("warm_start", C.c_int32), ("solver_tolerance", C.c_float),
         ("bias_midpoint", C.c_int32), ("substeps", C.c_int32), ("max_joint_velocity", C.c_float),
+        ("solver_type", C.c_int32),
     ]
 
 
@@ -142,6 +143,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.bias_midpoint = 1  # explicit bias pumps energy under per-step random targets
     p.substeps = 2  # gymapi.SimParams.substeps default (not set by isaacgym_env.py:6-35)
     p.max_joint_velocity = 100.0  # PhysX articulation joint maxJointVelocity default
+    p.solver_type = 0  # 0 PGS (velocity level, solver_iterations sweeps), 1 TGS (isaacgym_env.py:16-18)
     for k, v in kw.items():
         setattr(p, k, v)
     return p

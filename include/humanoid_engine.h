@@ -96,6 +96,15 @@ typedef struct he_sim_params {
     float max_joint_velocity;        /* rad/s, per joint relative rate (PhysX articulation joint
                                         maxJointVelocity, default 100); max_angular_velocity above
                                         clamps each link's WORLD angular velocity (PxRigidBody) */
+    int32_t solver_type;             /* sim_params.physx.solver_type (isaacgym_env.py:16): 0 PGS --
+                                        `solver_iterations` velocity-level Gauss-Seidel sweeps per
+                                        physics step; 1 TGS -- `solver_iterations` position iterations
+                                        (num_position_iterations, :17) inside each physics step of dt:
+                                        the step's factor and contact set are kept, and iteration k is
+                                        one sweep at the sub-step h = dt / solver_iterations against the
+                                        separations advanced by h J u_j of the earlier iterations; the
+                                        positions advance by the sub-steps' mean velocity, the step ends
+                                        at the last iteration's (DESIGN.md §5 "TGS") */
 } he_sim_params;
 
 /* Per-env solver warm-start cache (f32 words; HE_BUF_CONTACT_CACHE), written at the end of every

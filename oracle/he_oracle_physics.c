@@ -742,6 +742,85 @@ typedef struct warm_cache {
     R lam[MAXROW];
 } warm_cache;
 
+/* The contact row's velocity bias at separation `gap` over a step of h: a speculative contact (gap >= 0)
+ * may close its gap within the step, a penetrating one is pushed out at baumgarte * gap / h, at most
+ * max_depenetration_velocity (isaacgym_env.py:22). TGS (solver_type 1) takes it per position iteration
+ * with h = dt / iterations, from the separation its earlier iterations left. */
+static R contact_bias(const he_sim_params* p, R gap, R h) {
+    return gap >= 0 ? gap / h : fmax(p->baumgarte * gap / h, -p->max_depenetration_velocity);
+}
+/* diagnostic (tests/diag/tgs_study.py): TGS with the positions integrated once per position iteration
+ * (h = dt / K, each with that iteration's velocity) instead of once with the iterations' mean velocity
+ * (the engine's form). Off (0) in every test of the engine's physics. */
+static int g_tgs_sequential = 0;
+void ho_set_tgs_sequential(int on) { g_tgs_sequential = on; }
+#define TGS_MAXIT 16
+
+/* damping and the angular-velocity clamps of a generalized velocity (the body rotations of k) */
+static void clamp_velocity(const he_model* m, const he_sim_params* p, const kin* k, R dt, R* unew) {
+    /* angular damping and max angular velocity (asset options, humanoid_phc.py:212-213) */
+    R damp = 1.0 / (1.0 + dt * p->angular_damping);
+    for (int c = 0; c < 3; ++c) unew[c] *= damp;
+    for (int d = 0; d < ND; ++d) unew[6 + d] *= damp;
+    /* PhysX articulation joint maxJointVelocity (default 100 rad/s): each joint's relative rate */
+    const R jmax = p->max_joint_velocity;
+    for (int b = 1; b < NB; ++b) {
+        R* w = &unew[6 + 3 * (b - 1)];
+        R nrm = sqrt(dot3(w, w));
+        if (nrm > jmax) { R sc = jmax / nrm; w[0] *= sc; w[1] *= sc; w[2] *= sc; }
+    }
+    /* max_angular_velocity (asset option, humanoid_phc.py:213; PxRigidBody maxAngularVelocity):
+     * each link's WORLD angular velocity w_b = w_parent + R_b u_b, clamped link by link; the
+     * joint rates are then re-derived from the clamped world rates, u_b = R_b^T (w'_b - w'_parent) */
+    const R wmax = p->max_angular_velocity;
+    R wo[NB][3], wc[NB][3];
+    int any = 0;
+    for (int c = 0; c < 3; ++c) wo[0][c] = unew[c];
+    for (int b = 1; b < NB; ++b) {
+        R r[3];
+        matvec((R(*)[3])k->Rw[b], &unew[6 + 3 * (b - 1)], r);
+        for (int c = 0; c < 3; ++c) wo[b][c] = wo[m->parents[b]][c] + r[c];
+    }
+    for (int b = 0; b < NB; ++b) {
+        R nrm = sqrt(dot3(wo[b], wo[b])), sc = 1;
+        if (nrm > wmax) { sc = wmax / nrm; any = 1; }
+        for (int c = 0; c < 3; ++c) wc[b][c] = wo[b][c] * sc;
+    }
+    if (any) {
+        for (int c = 0; c < 3; ++c) unew[c] = wc[0][c];
+        for (int b = 1; b < NB; ++b) {
+            const R* wp = wc[m->parents[b]];
+            R rel[3] = {wc[b][0] - wp[0], wc[b][1] - wp[1], wc[b][2] - wp[2]};
+            R* u = &unew[6 + 3 * (b - 1)];
+            for (int c = 0; c < 3; ++c) u[c] = k->Rw[b][0][c] * rel[0] + k->Rw[b][1][c] * rel[1] + k->Rw[b][2][c] * rel[2];
+        }
+    }
+}
+
+/* semi-implicit position update over h with the velocity up (root: exp(h w) (x) q; ball joint:
+ * log(exp(q) (x) exp(h u)) with the limit backstop, which also removes the outward rate from s->u) */
+static void integrate_positions(const he_sim_params* p, env_state* s, const R* up, R h) {
+    for (int c = 0; c < 3; ++c) s->root_pos[c] += h * up[3 + c];
+    {
+        R dw[3] = {h * up[0], h * up[1], h * up[2]}, dq[4], nq[4];
+        qexp(dw, dq);
+        qmul(dq, s->root_q, nq);
+        qnormalize(nq);
+        memcpy(s->root_q, nq, sizeof(nq));
+    }
+    for (int b = 1; b < NB; ++b) {
+        R* qv = &s->q[3 * (b - 1)];
+        const R* uj = &up[6 + 3 * (b - 1)];
+        R ql[4], dq[4], nq[4], dw[3] = {h * uj[0], h * uj[1], h * uj[2]};
+        qexp(qv, ql);
+        qexp(dw, dq);
+        qmul(ql, dq, nq);
+        qnormalize(nq);
+        qlog(nq, qv);
+        if (p->joint_limits) limit_clamp(nq, qv, &s->u[3 * (b - 1)]);
+    }
+}
+
 /* one substep; updates s in place */
 /* Velocity-dependent + gravity bias at the velocities of state sv (the midpoint bias,
  * he_sim_params.bias_midpoint): the same RNEA as the substep's, with sv's body velocities. */
@@ -784,17 +863,32 @@ static void bias_at(const he_model* m, const topo* t, const he_sim_params* p, co
     }
 }
 
-static void substep(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
-                    R mu, int terrain_kind, step_out* out, warm_cache* ws) {
-    static __thread kin k;
-    static __thread R H[NG][NG];
-    static __thread R Z[MAXROW][NG];
-    static __thread R A[MAXROW][MAXROW];
-    static __thread contact cs[MAXC];
-    const R dt = p->dt;
-    kinematics(m, t, s, &k);
-    sinertia I[NB], Ic[NB];
-    for (int b = 0; b < NB; ++b) body_inertia(m, &k, b, mass_scale ? mass_scale[b] : 1.0, &I[b]);
+/* J_r^T of solver row w (slot c) in generalized coordinates: a joint limit its row g over the joint's
+ * dofs; a contact row S_i . (rho, dir) on the first body's chain, minus on the second's */
+static void row_jacobian(const topo* t, const kin* k, const srow* w, const contact* c, R* z) {
+    if (w->b1 == -2) { /* joint limit: the row over the joint's dofs */
+        for (int i = 0; i < NG; ++i) z[i] = 0;
+        for (int x = 0; x < 3; ++x) z[t->body_dof0[w->b0] + x] = c->g[x];
+    } else {
+        for (int i = 0; i < NG; ++i) {
+            int bi = t->dof_body[i];
+            R sgn = 0;
+            if (t->is_anc[bi][w->b0]) sgn += 1;
+            if (w->b1 >= 0 && t->is_anc[bi][w->b1]) sgn -= 1;
+            const R* S = k->S[i];
+            z[i] = sgn == 0 ? 0 : sgn * (S[0] * w->rho[0] + S[1] * w->rho[1] + S[2] * w->rho[2] + S[3] * w->dir[0] + S[4] * w->dir[1] + S[5] * w->dir[2]);
+        }
+    }
+}
+
+/* The step's dynamics at state s: kinematics k, the bodies' own spatial inertias I about o, the bias
+ * forces (gravity + Coriolis / gyroscopic at s's velocities, RNEA with u_dot = 0) and the joint-space
+ * inertia H (CRBA; no armature or drive terms). */
+static void dynamics_terms(const he_model* m, const topo* t, const he_sim_params* p, const env_state* s,
+                           const R* mass_scale, kin* k, sinertia* I, R* bias, R H[NG][NG]) {
+    kinematics(m, t, s, k);
+    sinertia Ic[NB];
+    for (int b = 0; b < NB; ++b) body_inertia(m, k, b, mass_scale ? mass_scale[b] : 1.0, &I[b]);
     /* RNEA bias with u_dot = 0 and gravity (a_0 = -g) */
     R Aacc[NB][6], F[NB][6];
     Aacc[0][0] = Aacc[0][1] = Aacc[0][2] = 0;
@@ -808,7 +902,7 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         for (int i = 0; i < 6; ++i) Aacc[b][i] = Aacc[pb][i];
         for (int c = 0; c < 3; ++c) {
             R cr[6];
-            crm(k.V[b], k.S[t->body_dof0[b] + c], cr);
+            crm(k->V[b], k->S[t->body_dof0[b] + c], cr);
             R uu = s->u[3 * (b - 1) + c];
             for (int i = 0; i < 6; ++i) Aacc[b][i] += cr[i] * uu;
         }
@@ -816,8 +910,8 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     for (int b = 0; b < NB; ++b) {
         R IA[6], IV[6], x[6];
         si_apply(&I[b], Aacc[b], IA);
-        si_apply(&I[b], k.V[b], IV);
-        crf(k.V[b], IV, x);
+        si_apply(&I[b], k->V[b], IV);
+        crf(k->V[b], IV, x);
         for (int i = 0; i < 6; ++i) F[b][i] = IA[i] + x[i];
         Ic[b] = I[b];
     }
@@ -826,24 +920,36 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         for (int i = 0; i < 6; ++i) F[pb][i] += F[b][i];
         si_add(&Ic[pb], &Ic[b]);
     }
-    R bias[NG];
     for (int i = 0; i < NG; ++i) {
-        const R* S = k.S[i];
+        const R* S = k->S[i];
         const R* f = F[t->dof_body[i]];
         bias[i] = S[0] * f[0] + S[1] * f[1] + S[2] * f[2] + S[3] * f[3] + S[4] * f[4] + S[5] * f[5];
     }
     /* CRBA: H_ij = S_j . (Ic_{body(i)} S_i) for j ancestor-or-self of i */
-    memset(H, 0, sizeof(H));
+    memset(H, 0, sizeof(R) * NG * NG);
     for (int i = 0; i < NG; ++i) {
         R IS[6];
-        si_apply(&Ic[t->dof_body[i]], k.S[i], IS);
+        si_apply(&Ic[t->dof_body[i]], k->S[i], IS);
         for (int j = i; j != -1; j = t->dof_parent[j]) {
-            const R* S = k.S[j];
+            const R* S = k->S[j];
             R v = S[0] * IS[0] + S[1] * IS[1] + S[2] * IS[2] + S[3] * IS[3] + S[4] * IS[4] + S[5] * IS[5];
             H[i][j] = v;
             H[j][i] = v;
         }
     }
+}
+
+static void substep(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
+                    R mu, int terrain_kind, step_out* out, warm_cache* ws) {
+    static __thread kin k;
+    static __thread R H[NG][NG];
+    static __thread R Z[MAXROW][NG];
+    static __thread R A[MAXROW][MAXROW];
+    static __thread contact cs[MAXC];
+    const R dt = p->dt;
+    sinertia I[NB];
+    R bias[NG];
+    dynamics_terms(m, t, p, s, mass_scale, &k, I, bias, H);
     /* armature + implicit PD drives; a joint at its angle limit cannot give way to its drive, so
      * its effort check takes the drive torque at rest (no implicit relief) */
     R rhs[NG], coef[NG];
@@ -922,33 +1028,33 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
     memset(out->contact_force, 0, sizeof(out->contact_force));
     R unew[NG];
     memcpy(unew, uf, sizeof(unew));
+    R upos[NG];          /* TGS: the velocity the positions advance by (the iterations' mean) */
+    int have_upos = 0;
+    static __thread R useq[TGS_MAXIT][NG]; /* TGS sequential diagnostic: each iteration's velocity */
+    int nseq = 0;
     R lim_tau[ND];
     memset(lim_tau, 0, sizeof(lim_tau));
     if (nc > 0) {
         static __thread srow rows[MAXROW];
         const int nr = build_rows(cs, nc, k.o, rows);
-        R brow[MAXROW];
+        /* TGS (solver_type 1, isaacgym_env.py:16-18): K position iterations of h = dt / K, each one
+         * sweep; a normal / limit row's separation advances by h J_r u_k after iteration k (the step's
+         * rows, J linearised at its start) and its bias follows it. PGS: one step of dt. */
+        const int tgs = p->solver_type == 2; /* the fixed-drive TGS form (study only) */
+        const int K = tgs ? (p->solver_iterations > 0 ? (p->solver_iterations < TGS_MAXIT ? p->solver_iterations : TGS_MAXIT) : 1) : 1;
+        const R h = tgs ? dt / K : dt;
+        R brow[MAXROW], brow0[MAXROW], sep[MAXROW];
         for (int r = 0; r < nr; ++r) {
             const srow* w = &rows[r];
             const contact* c = &cs[w->slot];
             R* z = Z[r];
-            if (w->b1 == -2) { /* joint limit: the row over the joint's dofs */
-                for (int i = 0; i < NG; ++i) z[i] = 0;
-                for (int x = 0; x < 3; ++x) z[t->body_dof0[w->b0] + x] = c->g[x];
-            } else {
-                for (int i = 0; i < NG; ++i) {
-                    int bi = t->dof_body[i];
-                    R sgn = 0;
-                    if (t->is_anc[bi][w->b0]) sgn += 1;
-                    if (w->b1 >= 0 && t->is_anc[bi][w->b1]) sgn -= 1;
-                    const R* S = k.S[i];
-                    z[i] = sgn == 0 ? 0 : sgn * (S[0] * w->rho[0] + S[1] * w->rho[1] + S[2] * w->rho[2] + S[3] * w->dir[0] + S[4] * w->dir[1] + S[5] * w->dir[2]);
-                }
-            }
+            row_jacobian(t, &k, w, c, z);
             R ju = 0;
             for (int i = 0; i < NG; ++i) ju += z[i] * uf[i];
             R bb = 0;
-            if (w->kind == 0) bb = c->gap >= 0 ? c->gap / dt : fmax(p->baumgarte * c->gap / dt, -p->max_depenetration_velocity);
+            if (w->kind == 0) bb = contact_bias(p, c->gap, h);
+            brow0[r] = ju;
+            sep[r] = w->kind == 0 ? c->gap : 0;
             brow[r] = ju + bb;
             ltdl_solve_LT(H, t->dof_parent, z);
         }
@@ -965,7 +1071,9 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                     A[r][c2] *= 1.0 + g_probe_rel * probe_xi(r, c2);
                     A[c2][r] = A[r][c2];
                 }
-                brow[r] *= 1.0 + g_probe_rel * probe_xi(r, MAXROW);
+                const R f = 1.0 + g_probe_rel * probe_xi(r, MAXROW);
+                brow[r] *= f;
+                brow0[r] *= f;
             }
             ++g_probe_sub;
         }
@@ -982,7 +1090,10 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
 #define PATCH_BOUND_OF(L_, r) ({ R b_ = 0; for (int k_ = 0; k_ < rows[r].cnt; ++k_) b_ += L_[rows[r].n0 + k_]; rows[r].muw * b_; })
 #define PATCH_BOUND(r) PATCH_BOUND_OF(lam, r)
         int sweeps = 0;
-        for (int it = 0; it < p->solver_iterations; ++it) {
+        R lam_sum[MAXROW];
+        static __thread R lamk[TGS_MAXIT][MAXROW]; /* each iteration's impulses (the sequential diagnostic) */
+        memset(lam_sum, 0, sizeof(R) * nr);
+        for (int it = 0; it < (tgs ? K : p->solver_iterations); ++it) {
             R lam_prev[MAXROW];
             memcpy(lam_prev, lam, sizeof(R) * nr);
             ++sweeps;
@@ -996,6 +1107,18 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                     const R bound = g_lagged_bounds ? PATCH_BOUND_OF(lam_prev, r) : PATCH_BOUND(r);
                     lam[r] = l > bound ? bound : (l < -bound ? -bound : l);
                 }
+            }
+            if (tgs) { /* every iteration runs: they are sub-steps, not convergence sweeps */
+                for (int r = 0; r < nr; ++r) { lam_sum[r] += lam[r]; lamk[it][r] = lam[r]; }
+                if (it + 1 < K)
+                    for (int r = 0; r < nr; ++r) {
+                        if (rows[r].kind != 0) continue;
+                        R v = brow0[r]; /* J_r u_k = J_r uf + (A lambda)_r */
+                        for (int j = 0; j < nr; ++j) v += A[r][j] * lam[j];
+                        sep[r] += h * v;
+                        brow[r] = brow0[r] + contact_bias(p, sep[r], h);
+                    }
+                continue;
             }
             /* converged: no row's velocity moved by more than solver_tolerance in this sweep
              * (|d lambda_r| A_rr); 0 runs every sweep */
@@ -1042,6 +1165,28 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
         for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
         ltdl_solve_L(H, t->dof_parent, y);
         for (int i = 0; i < NG; ++i) unew[i] += y[i];
+        if (tgs) { /* the positions' velocity: uf + M^-1 J^T (mean of the iterations' impulses) */
+            memset(y, 0, sizeof(y));
+            for (int r = 0; r < nr; ++r) {
+                const R lb = lam_sum[r] / K;
+                if (lb != 0) for (int i = 0; i < NG; ++i) y[i] += Z[r][i] * lb;
+            }
+            for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
+            ltdl_solve_L(H, t->dof_parent, y);
+            for (int i = 0; i < NG; ++i) upos[i] = uf[i] + y[i];
+            have_upos = 1;
+            if (g_tgs_sequential) {
+                nseq = K;
+                for (int it = 0; it < K; ++it) {
+                    memset(y, 0, sizeof(y));
+                    for (int r = 0; r < nr; ++r)
+                        if (lamk[it][r] != 0) for (int i = 0; i < NG; ++i) y[i] += Z[r][i] * lamk[it][r];
+                    for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
+                    ltdl_solve_L(H, t->dof_parent, y);
+                    for (int i = 0; i < NG; ++i) useq[it][i] = uf[i] + y[i];
+                }
+            }
+        }
         for (int r = 0; r < nr; ++r) {
             const srow* w = &rows[r];
             if (w->b1 == -2) { /* a joint limit: a joint force (below), not a contact force */
@@ -1064,66 +1209,239 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
      * joint's dofs with its impulse lambda adds g lambda / dt */
     for (int d = 0; d < ND; ++d) out->dof_force[d] -= coef[6 + d] * (unew[6 + d] - u0[6 + d]);
     for (int d = 0; d < ND; ++d) out->dof_force[d] += lim_tau[d];
-    /* angular damping and max angular velocity (asset options, humanoid_phc.py:212-213) */
-    R damp = 1.0 / (1.0 + dt * p->angular_damping);
-    for (int c = 0; c < 3; ++c) unew[c] *= damp;
-    for (int d = 0; d < ND; ++d) unew[6 + d] *= damp;
-    /* PhysX articulation joint maxJointVelocity (default 100 rad/s): each joint's relative rate */
-    const R jmax = p->max_joint_velocity;
-    for (int b = 1; b < NB; ++b) {
-        R* w = &unew[6 + 3 * (b - 1)];
-        R nrm = sqrt(dot3(w, w));
-        if (nrm > jmax) { R sc = jmax / nrm; w[0] *= sc; w[1] *= sc; w[2] *= sc; }
-    }
-    /* max_angular_velocity (asset option, humanoid_phc.py:213; PxRigidBody maxAngularVelocity):
-     * each link's WORLD angular velocity w_b = w_parent + R_b u_b, clamped link by link; the
-     * joint rates are then re-derived from the clamped world rates, u_b = R_b^T (w'_b - w'_parent) */
-    {
-        const R wmax = p->max_angular_velocity;
-        R wo[NB][3], wc[NB][3];
-        int any = 0;
-        for (int c = 0; c < 3; ++c) wo[0][c] = unew[c];
-        for (int b = 1; b < NB; ++b) {
-            R r[3];
-            matvec(k.Rw[b], &unew[6 + 3 * (b - 1)], r);
-            for (int c = 0; c < 3; ++c) wo[b][c] = wo[m->parents[b]][c] + r[c];
-        }
-        for (int b = 0; b < NB; ++b) {
-            R nrm = sqrt(dot3(wo[b], wo[b])), sc = 1;
-            if (nrm > wmax) { sc = wmax / nrm; any = 1; }
-            for (int c = 0; c < 3; ++c) wc[b][c] = wo[b][c] * sc;
-        }
-        if (any) {
-            for (int c = 0; c < 3; ++c) unew[c] = wc[0][c];
-            for (int b = 1; b < NB; ++b) {
-                const R* wp = wc[m->parents[b]];
-                R rel[3] = {wc[b][0] - wp[0], wc[b][1] - wp[1], wc[b][2] - wp[2]};
-                R* u = &unew[6 + 3 * (b - 1)];
-                for (int c = 0; c < 3; ++c) u[c] = k.Rw[b][0][c] * rel[0] + k.Rw[b][1][c] * rel[1] + k.Rw[b][2][c] * rel[2];
-            }
-        }
-    }
-    /* write velocities + semi-implicit position update */
+    clamp_velocity(m, p, &k, dt, unew);
+    /* write velocities + semi-implicit position update (TGS: by the iterations' mean velocity, or per
+     * iteration in the sequential diagnostic) */
     for (int c = 0; c < 3; ++c) { s->root_w[c] = unew[c]; s->root_v[c] = unew[3 + c]; }
     for (int d = 0; d < ND; ++d) s->u[d] = unew[6 + d];
-    for (int c = 0; c < 3; ++c) s->root_pos[c] += dt * s->root_v[c];
-    {
-        R dw[3] = {dt * s->root_w[0], dt * s->root_w[1], dt * s->root_w[2]}, dq[4], nq[4];
-        qexp(dw, dq);
-        qmul(dq, s->root_q, nq);
-        qnormalize(nq);
-        memcpy(s->root_q, nq, sizeof(nq));
+    if (nseq > 0) {
+        for (int it = 0; it < nseq; ++it) {
+            clamp_velocity(m, p, &k, dt, useq[it]);
+            integrate_positions(p, s, useq[it], dt / nseq);
+        }
+    } else if (have_upos) {
+        clamp_velocity(m, p, &k, dt, upos);
+        integrate_positions(p, s, upos, dt);
+    } else {
+        integrate_positions(p, s, unew, dt);
     }
-    for (int b = 1; b < NB; ++b) {
-        R* qv = &s->q[3 * (b - 1)];
-        R ql[4], dq[4], nq[4], dw[3] = {dt * s->u[3 * (b - 1)], dt * s->u[3 * (b - 1) + 1], dt * s->u[3 * (b - 1) + 2]};
-        qexp(qv, ql);
-        qexp(dw, dq);
-        qmul(ql, dq, nq);
-        qnormalize(nq);
-        qlog(nq, qv);
-        if (p->joint_limits) limit_clamp(nq, qv, &s->u[3 * (b - 1)]);
+}
+
+/* TGS (solver_type 1): sim_params.physx.solver_type = 1 with num_position_iterations = K and
+ * num_velocity_iterations = 0 (isaacgym_env.py:16-18). One physics step of dt is K position iterations
+ * of h = dt / K on the step's kinematics, factor and contact set (TGS keeps the step's contacts and
+ * moves their separations; PhysX's TGS integrates the bodies once per position iteration):
+ *   - the drives are implicit over one iteration (M~ = H + armature + h kd + h^2 kp, factored once),
+ *     their error taken from the joint positions the earlier iterations reached;
+ *   - iteration k: free velocity u + M~^-1 h (tau(q_k, u_k) - bias), one Gauss-Seidel sweep of the
+ *     step's rows against it (bias from the row's separation, advanced by h J_r u_j of the earlier
+ *     iterations), the impulse change applied, damping and clamps over h, positions integrated by h;
+ *   - the rows' impulses accumulate over the iterations (the step's total: the bounds and the reported
+ *     forces); each iteration's sweep starts from the previous iteration's change (the first: the
+ *     previous step's last change, the warm-start cache), as a small-step solver warm-starts each
+ *     sub-step from the last; the drive force is the iterations' mean.
+ * The velocity-dependent bias is taken at u0 for the whole step (bias_midpoint 0) or re-evaluated at
+ * each iteration's start velocity with the step's kinematics (bias_midpoint 1). */
+static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
+                        R mu, int terrain_kind, step_out* out, warm_cache* ws) {
+    static __thread kin k;
+    static __thread R H[NG][NG];
+    static __thread R Z[MAXROW][NG], J[MAXROW][NG];
+    static __thread R A[MAXROW][MAXROW];
+    static __thread contact cs[MAXC];
+    static __thread srow rows[MAXROW];
+    const R dt = p->dt;
+    const int K = p->solver_iterations < 1 ? 1 : (p->solver_iterations > TGS_MAXIT ? TGS_MAXIT : p->solver_iterations);
+    const R h = dt / K;
+    sinertia I[NB];
+    R bias[NG];
+    dynamics_terms(m, t, p, s, mass_scale, &k, I, bias, H);
+    /* drives implicit over one iteration; the effort limit as in substep() with the iteration's h
+     * (PhysX clamps a drive's impulse per iteration to maxForce h) */
+    int blocked[NB] = {0};
+    if (p->joint_limits)
+        for (int b = 1; b < NB; ++b) {
+            R gap, dir[3];
+            blocked[b] = angle_row(p, s, b, &gap, dir);
+        }
+    R kp[ND], kd[ND];
+    for (int d = 0; d < ND; ++d) {
+        const int g = 6 + d;
+        H[g][g] += m->armature[d];
+        R kpv = m->stiffness[d] * p->kp_scale, kdv = m->damping[d] * p->kd_scale;
+        const R u = s->u[d];
+        const R tau = kpv * ((s->target[d] - s->q[d]) - h * u) - kdv * u;
+        const R c = h * kpv + kdv;
+        const R tau_i = blocked[d / 3 + 1] ? tau : tau - c * h * (tau - bias[g]) / (H[g][g] + h * c);
+        if (fabs(tau_i) > m->effort[d]) {
+            const R sc = m->effort[d] / fabs(tau_i);
+            kpv *= sc;
+            kdv *= sc;
+        }
+        H[g][g] += h * (kdv + h * kpv);
+        kp[d] = kpv;
+        kd[d] = kdv;
     }
+    ltdl_factor(H, t->dof_parent);
+    /* the step's contact set and rows (at the step's start) */
+    int total = 0;
+    const int nc = gen_contacts(m, p, &k, s, terrain_kind, mu, cs, &total);
+    out->num_contacts = nc;
+    out->dropped = total - nc;
+    out->residual = 0;
+    out->nr = 0;
+    memset(out->contact_force, 0, sizeof(out->contact_force));
+    const int nr = nc > 0 ? build_rows(cs, nc, k.o, rows) : 0;
+    R sep[MAXROW], lam[MAXROW], applied[MAXROW], guess[MAXROW], fprobe[MAXROW], wlast[MAXROW];
+    for (int r = 0; r < nr; ++r) {
+        row_jacobian(t, &k, &rows[r], &cs[rows[r].slot], J[r]);
+        memcpy(Z[r], J[r], sizeof(R) * NG);
+        ltdl_solve_LT(H, t->dof_parent, Z[r]);
+        sep[r] = rows[r].kind == 0 ? cs[rows[r].slot].gap : 0;
+        lam[r] = 0;
+        applied[r] = 0;
+        guess[r] = 0;
+        fprobe[r] = 1;
+    }
+    for (int r = 0; r < nr; ++r)
+        for (int c2 = 0; c2 <= r; ++c2) {
+            R acc = 0;
+            for (int i = 0; i < NG; ++i) acc += Z[r][i] * Z[c2][i] / H[i][i];
+            A[r][c2] = acc;
+            A[c2][r] = acc;
+        }
+    if (g_probe_rel > 0 && nr > 0) { /* sensitivity probe (see substep) */
+        for (int r = 0; r < nr; ++r) {
+            for (int c2 = 0; c2 <= r; ++c2) {
+                A[r][c2] *= 1.0 + g_probe_rel * probe_xi(r, c2);
+                A[c2][r] = A[r][c2];
+            }
+            fprobe[r] = 1.0 + g_probe_rel * probe_xi(r, MAXROW);
+        }
+        ++g_probe_sub;
+    }
+    /* warm start: each iteration's sweep starts from the accumulated impulses plus the previous
+     * iteration's change (the first iteration: the previous step's last change, by row key) */
+    if (ws && p->warm_start)
+        for (int r = 0; r < nr; ++r)
+            for (int j = 0; j < ws->n; ++j)
+                if (ws->key[j] == rows[r].key) {
+                    guess[r] = ws->lam[j];
+                    break;
+                }
+#define TGS_BOUND(r) ({ R b_ = 0; for (int k_ = 0; k_ < rows[r].cnt; ++k_) b_ += lam[rows[r].n0 + k_]; rows[r].muw * b_; })
+    R u[NG];
+    for (int c = 0; c < 3; ++c) { u[c] = s->root_w[c]; u[3 + c] = s->root_v[c]; }
+    for (int d = 0; d < ND; ++d) u[6 + d] = s->u[d];
+    env_state sw = *s; /* positions advance per iteration; s keeps the step's start */
+    R dfor[ND];
+    memset(dfor, 0, sizeof(dfor));
+    R bias_it[NG];
+    memcpy(bias_it, bias, sizeof(bias_it));
+    for (int it = 0; it < K; ++it) {
+        if (it > 0 && p->bias_midpoint) { /* the velocity-dependent bias at this iteration's velocity */
+            env_state sv = *s;
+            for (int c = 0; c < 3; ++c) { sv.root_w[c] = u[c]; sv.root_v[c] = u[3 + c]; }
+            for (int d = 0; d < ND; ++d) sv.u[d] = u[6 + d];
+            bias_at(m, t, p, &sv, &k, I, bias_it);
+        }
+        R y[NG];
+        for (int i = 0; i < NG; ++i) y[i] = -h * bias_it[i];
+        for (int d = 0; d < ND; ++d)
+            y[6 + d] += h * (kp[d] * ((s->target[d] - sw.q[d]) - h * u[6 + d]) - kd[d] * u[6 + d]);
+        ltdl_solve_LT(H, t->dof_parent, y);
+        for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
+        ltdl_solve_L(H, t->dof_parent, y);
+        R unew[NG];
+        for (int i = 0; i < NG; ++i) unew[i] = u[i] + y[i]; /* the iteration's free velocity */
+        if (nr > 0) {
+            R brow[MAXROW];
+            for (int r = 0; r < nr; ++r) {
+                R ju = 0;
+                for (int i = 0; i < NG; ++i) ju += J[r][i] * unew[i];
+                brow[r] = ju * fprobe[r] + (rows[r].kind == 0 ? contact_bias(p, sep[r], h) : 0);
+            }
+            for (int r = 0; r < nr; ++r) lam[r] = applied[r] + guess[r];
+            for (int r = 0; r < nr; ++r) { /* one Gauss-Seidel sweep on the accumulated impulses */
+                R w = brow[r];
+                for (int j = 0; j < nr; ++j) w += A[r][j] * (lam[j] - applied[j]);
+                const R l = lam[r] - w / (A[r][r] + 1e-12);
+                if (rows[r].kind == 0) {
+                    lam[r] = l > 0 ? l : 0;
+                } else {
+                    const R bound = TGS_BOUND(r);
+                    lam[r] = l > bound ? bound : (l < -bound ? -bound : l);
+                }
+            }
+            for (int r = 0; r < nr; ++r) { /* the rows' velocities after the sweep (the residual) */
+                R w = brow[r];
+                for (int j = 0; j < nr; ++j) w += A[r][j] * (lam[j] - applied[j]);
+                wlast[r] = w;
+            }
+            memset(y, 0, sizeof(y));
+            for (int r = 0; r < nr; ++r) {
+                const R dl = lam[r] - applied[r];
+                if (dl != 0) for (int i = 0; i < NG; ++i) y[i] += Z[r][i] * dl;
+                applied[r] = lam[r];
+                guess[r] = dl;
+            }
+            for (int i = 0; i < NG; ++i) y[i] /= H[i][i];
+            ltdl_solve_L(H, t->dof_parent, y);
+            for (int i = 0; i < NG; ++i) unew[i] += y[i];
+            for (int r = 0; r < nr; ++r) /* separations after this iteration's motion */
+                if (rows[r].kind == 0) {
+                    R ju = 0;
+                    for (int i = 0; i < NG; ++i) ju += J[r][i] * unew[i];
+                    sep[r] += h * ju;
+                }
+        }
+        /* the drive torque of the iteration, implicit at its end velocity */
+        for (int d = 0; d < ND; ++d)
+            dfor[d] += kp[d] * ((s->target[d] - sw.q[d]) - h * unew[6 + d]) - kd[d] * unew[6 + d];
+        clamp_velocity(m, p, &k, h, unew);
+        for (int c = 0; c < 3; ++c) { sw.root_w[c] = unew[c]; sw.root_v[c] = unew[3 + c]; }
+        for (int d = 0; d < ND; ++d) sw.u[d] = unew[6 + d];
+        integrate_positions(p, &sw, unew, h); /* the limit backstop removes outward rates from sw.u */
+        for (int c = 0; c < 3; ++c) { u[c] = sw.root_w[c]; u[3 + c] = sw.root_v[c]; }
+        for (int d = 0; d < ND; ++d) u[6 + d] = sw.u[d];
+    }
+    out->sweeps = K;
+    out->nr = nr < HE_MAX_ROWS ? nr : HE_MAX_ROWS;
+    R lim_tau[ND];
+    memset(lim_tau, 0, sizeof(lim_tau));
+    for (int r = 0; r < nr; ++r) {
+        if (r < HE_MAX_ROWS) {
+            out->muw[r] = rows[r].kind == 0 ? 0 : rows[r].muw;
+            out->gap[r] = cs[rows[r].slot].gap;
+        }
+        R res; /* complementarity residual of the last iteration */
+        if (rows[r].kind == 0) res = fmin(wlast[r], lam[r] * A[r][r]);
+        else {
+            const R bound = TGS_BOUND(r);
+            res = (lam[r] >= bound - 1e-12 && wlast[r] < 0) || (lam[r] <= -bound + 1e-12 && wlast[r] > 0) ? 0 : wlast[r];
+        }
+        if (fabs(res) > out->residual) out->residual = fabs(res);
+        const srow* w = &rows[r];
+        if (w->b1 == -2) {
+            for (int x = 0; x < 3; ++x) lim_tau[3 * (w->b0 - 1) + x] += cs[w->slot].g[x] * lam[r] / dt;
+            continue;
+        }
+        for (int x = 0; x < 3; ++x) {
+            const R f = lam[r] * w->dir[x] / dt;
+            out->contact_force[w->b0][x] += f;
+            if (w->b1 >= 0) out->contact_force[w->b1][x] -= f;
+        }
+    }
+#undef TGS_BOUND
+    if (ws) { /* the last iteration's changes: the next step's first guess */
+        ws->n = nr;
+        for (int r = 0; r < nr; ++r) {
+            ws->key[r] = rows[r].key;
+            ws->lam[r] = guess[r];
+        }
+    }
+    for (int d = 0; d < ND; ++d) out->dof_force[d] = dfor[d] / K + lim_tau[d];
+    *s = sw;
 }
 
 static void write_rb(const he_model* m, const topo* t, const env_state* s, float* rb) {
@@ -1192,7 +1510,8 @@ void ho_physics_step(const he_model* m, const he_sim_params* p, int n, float* ro
         memset(&out, 0, sizeof(out));
         g_probe_env = e;
         g_probe_sub = 0;
-        for (int it = 0; it < substeps; ++it) substep(m, &t, p, &s, mass_scale ? ms : NULL, mu, tk, &out, &ws);
+        for (int it = 0; it < substeps; ++it)
+            (p->solver_type == 1 ? substep_tgs : substep)(m, &t, p, &s, mass_scale ? ms : NULL, mu, tk, &out, &ws);
         for (int c = 0; c < 3; ++c) { rs[c] = (float)s.root_pos[c]; rs[7 + c] = (float)s.root_v[c]; rs[10 + c] = (float)s.root_w[c]; }
         for (int c = 0; c < 4; ++c) rs[3 + c] = (float)s.root_q[c];
         for (int d = 0; d < ND; ++d) {

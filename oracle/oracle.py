@@ -178,6 +178,12 @@ def set_two_anchor(on):
     lib().ho_set_two_anchor(int(bool(on)))
 
 
+def set_tgs_sequential(on):
+    """Diagnostic: TGS positions integrated once per position iteration (each with that iteration's
+    velocity) instead of once with the iterations' mean velocity (the engine's form)."""
+    lib().ho_set_tgs_sequential(int(bool(on)))
+
+
 def set_row_gap_out(arr=None):
     """Diagnostics only: float32 [N, HE_MAX_ROWS] filled with the gap of every solver row's contact of
     each env's last substep (m; a joint-limit row: its angle gap), in the cache's row order."""
