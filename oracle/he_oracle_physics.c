@@ -1235,7 +1235,9 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
  *     their error taken from the joint positions the earlier iterations reached;
  *   - iteration k: free velocity u + M~^-1 h (tau(q_k, u_k) - bias), one Gauss-Seidel sweep of the
  *     step's rows against it (bias from the row's separation, advanced by h J_r u_j of the earlier
- *     iterations), the impulse change applied, damping and clamps over h, positions integrated by h;
+ *     iterations), the impulse change applied, positions integrated by h with the damped and clamped
+ *     velocity (the solver's velocity itself is not clamped; the last iteration's clamped one is the
+ *     step's output);
  *   - the rows' impulses accumulate over the iterations (the step's total: the bounds and the reported
  *     forces); each iteration's sweep starts from the previous iteration's change (the first: the
  *     previous step's last change, the warm-start cache), as a small-step solver warm-starts each
@@ -1398,12 +1400,17 @@ static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p
         /* the drive torque of the iteration, implicit at its end velocity */
         for (int d = 0; d < ND; ++d)
             dfor[d] += kp[d] * ((s->target[d] - sw.q[d]) - h * unew[6 + d]) - kd[d] * unew[6 + d];
-        clamp_velocity(m, p, &k, h, unew);
-        for (int c = 0; c < 3; ++c) { sw.root_w[c] = unew[c]; sw.root_v[c] = unew[3 + c]; }
-        for (int d = 0; d < ND; ++d) sw.u[d] = unew[6 + d];
-        integrate_positions(p, &sw, unew, h); /* the limit backstop removes outward rates from sw.u */
-        for (int c = 0; c < 3; ++c) { u[c] = sw.root_w[c]; u[3 + c] = sw.root_v[c]; }
-        for (int d = 0; d < ND; ++d) u[6 + d] = sw.u[d];
+        /* the positions advance by the damped, clamped velocity (damping over the step's dt; the
+         * last iteration's is the step's output, with the limit backstop's outward rates removed);
+         * the solver's own velocity stays as the sweeps left it (the rows' velocities J u are the
+         * sweep's residuals, the kernel's delta form) */
+        R ucl[NG];
+        memcpy(ucl, unew, sizeof(ucl));
+        clamp_velocity(m, p, &k, dt, ucl);
+        for (int c = 0; c < 3; ++c) { sw.root_w[c] = ucl[c]; sw.root_v[c] = ucl[3 + c]; }
+        for (int d = 0; d < ND; ++d) sw.u[d] = ucl[6 + d];
+        integrate_positions(p, &sw, ucl, h); /* the limit backstop removes outward rates from sw.u */
+        memcpy(u, unew, sizeof(u));
     }
     out->sweeps = K;
     out->nr = nr < HE_MAX_ROWS ? nr : HE_MAX_ROWS;
