@@ -50,12 +50,13 @@ def parse(argv=None):
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=40)
-    ap.add_argument("--scheme", choices=["default", "r02", "tgs"], default="default",
-                    help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 sweeps, "
+    ap.add_argument("--scheme", choices=["default", "r02", "tgs", "tgs_small"], default="default",
+                    help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 PGS sweeps, "
                          "link world angular-velocity clamp; r02 = round 2's energy-unstable step (2 x 1/60 s, "
                          "explicit bias, 8 sweeps) with round 3's clamps, for the cost comparison only (DESIGN §5); tgs = "
-                         "PhysX TGS's 4 position iterations per 1/120 s step as 8 substeps of 1/480 s per simulate() "
-                         "with one sweep each (DESIGN §5 'TGS')")
+                         "PhysX TGS (solver_type 1, isaacgym_env.py:16-18): 4 position iterations inside each 1/120 s "
+                         "physics step on its factor and contact set (DESIGN §5 'TGS'); tgs_small = TGS's small-step "
+                         "form, 8 substeps of 1/480 s per simulate() with one sweep each")
     ap.add_argument("--solver-tolerance", type=float, default=None,
                     help="he_sim_params.solver_tolerance override (m/s; 0 = every sweep runs)")
     ap.add_argument("--no-puffer-level", action="store_true",
@@ -388,6 +389,8 @@ def scheme_params(args):
     if getattr(args, "scheme", "default") == "r02":
         out = dict(substeps=1, bias_midpoint=0, solver_iterations=8)
     elif getattr(args, "scheme", "default") == "tgs":
+        out = dict(solver_type=1, solver_iterations=4)
+    elif getattr(args, "scheme", "default") == "tgs_small":
         out = dict(substeps=8, solver_iterations=1)
     if getattr(args, "solver_tolerance", None) is not None:
         out["solver_tolerance"] = args.solver_tolerance
@@ -666,10 +669,11 @@ def main():
                 line["r02_scheme"] = scheme_leg(args, model, local)
             except Exception as exc:  # report, never fake
                 line["r02_scheme"] = {"value": None, "error": repr(exc)}
-            try:
-                line["tgs_scheme"] = scheme_leg(args, model, local, scheme="tgs")
-            except Exception as exc:  # report, never fake
-                line["tgs_scheme"] = {"value": None, "error": repr(exc)}
+            for sch in ("tgs", "tgs_small"):
+                try:
+                    line[f"{sch}_scheme"] = scheme_leg(args, model, local, scheme=sch)
+                except Exception as exc:  # report, never fake
+                    line[f"{sch}_scheme"] = {"value": None, "error": repr(exc)}
         if not args.no_tracking and world == 1 and args.num_envs == 4096:
             try:
                 line["tracking_configs2"] = tracking_leg(args, model, local)

@@ -50,21 +50,26 @@ MIN_OCCUPANCY = {"he_physics.hip": ("physics_kernel", 2)}
 
 
 def _check_occupancy(src, stderr):
+    """Every kernel of the TU whose name contains the watched name (the physics TU: physics_kernel and
+    physics_kernel_tgs) must reach the occupancy."""
     want = MIN_OCCUPANCY.get(os.path.basename(src))
     if not want:
         return
     name, waves = want
     lines = stderr.splitlines()
+    seen = 0
     for i, ln in enumerate(lines):
         if "Function Name:" in ln and name in ln:
             for ln2 in lines[i + 1:i + 16]:
                 m = re.search(r"Occupancy \[waves/SIMD\]: (\d+)", ln2)
                 if m:
                     if int(m.group(1)) < waves:
-                        raise RuntimeError(f"{name}: occupancy {m.group(1)} waves/SIMD < {waves} "
-                                           f"(register pressure; see the resource report)")
-                    return
-    raise RuntimeError(f"{name}: no occupancy in the compiler's resource report")
+                        raise RuntimeError(f"{ln.split('Function Name:')[1].split()[0]}: occupancy {m.group(1)} "
+                                           f"waves/SIMD < {waves} (register pressure; see the resource report)")
+                    seen += 1
+                    break
+    if not seen:
+        raise RuntimeError(f"{name}: no occupancy in the compiler's resource report")
 
 
 def _compile(hipcc, cmd, src, o, force, hdr_time, verbose):

@@ -113,6 +113,12 @@ int he_create(const he_sim_params* params, int device, he_engine** out) {
     if (params->substeps < 1 || params->substeps > 16) return fail("he_create: substeps must be in [1, 16]");
     if (!(params->max_joint_velocity > 0.f) || !(params->max_angular_velocity > 0.f))
         return fail("he_create: max_joint_velocity and max_angular_velocity must be positive");
+    // sim_params.physx.solver_type (isaacgym_env.py:16): 0 PGS, 1 TGS with solver_iterations position
+    // iterations (num_position_iterations, :17) per physics step
+    if (params->solver_type != 0 && params->solver_type != 1)
+        return fail("he_create: solver_type must be 0 (PGS) or 1 (TGS), got %d", params->solver_type);
+    if (params->solver_type == 1 && (params->solver_iterations < 1 || params->solver_iterations > 16))
+        return fail("he_create: TGS needs solver_iterations (position iterations) in [1, 16]");
     he_engine* h = new he_engine();
     h->device = device;
     h->params = *params;

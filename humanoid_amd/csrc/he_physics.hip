@@ -37,6 +37,7 @@ constexpr int MAXC = HE_MAX_CONTACTS;  // contact slots (points, joint limits)
 constexpr int MAXR = HE_MAX_ROWS;      // solver rows, one per lane (patch friction, oracle build_rows)
 constexpr int W = 64;
 static_assert(MAXR <= W - 1, "solver rows must fit one per lane");
+constexpr int kTgsMaxIt = 16;  // TGS position iterations per physics step (he_simulate checks; oracle TGS_MAXIT)
 static_assert(MAXC < W, "one slot per lane in the row-layout pass");
 static_assert(smpl::kNG == NG && smpl::kNB == NB, "generated topology mismatch");
 
@@ -508,6 +509,27 @@ HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f
         lo = fmaf(-ak[R].y, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
         pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr);
+    }
+}
+
+// TGS (solver_type 1): the same sweep with the friction bound weights rebuilt per row from the lane's
+// patch mask (2 VALU off the dependent chain) instead of a second register per row: the scaled
+// columns, the rows' Zh and the sweep state stay in registers through the position iterations'
+// triangular solves, bias passes and integrations
+template <int R, int N>
+HE_DEV void pgs_sweep_tgs(regla::f2v& ch, float& dvec, float& lo, const float (&ap)[MAXR], uint32_t mlo, uint32_t mhi,
+                          float muw, int nr) {
+    if constexpr (R < N) {
+        if constexpr (R > 0 && R % 4 == 0) {  // a row-count exit every 4 rows
+            if (R >= nr) return;
+        }
+        const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
+        const int sel = __builtin_amdgcn_sbfe((int)(R < 32 ? mlo : mhi), R & 31, 1);
+        const regla::f2v a = {ap[R], __int_as_float(sel & __float_as_int(muw))};
+        ch = __builtin_elementwise_fma(a, regla::f2v{d, d}, ch);
+        lo = fmaf(-a.y, d, lo);
+        dvec = regla::wrlane<R>(d, dvec);
+        pgs_sweep_tgs<R + 1, N>(ch, dvec, lo, ap, mlo, mhi, muw, nr);
     }
 }
 
@@ -1096,6 +1118,125 @@ HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_para
     STAMP(28);
 }
 
+// ---------------------------------------------------------------------------------- TGS iterations
+// he_sim_params.solver_type 1 (oracle/he_oracle_physics.c substep_tgs): the velocity-dependent bias of
+// the next position iteration at the working velocity `vel` (L.u0), with the step's kinematics (S, V
+// frames, own inertias Ib) -- bias_midpoint's second RNEA: the bodies' velocities and bias
+// accelerations by pointer jumping, their forces, the subtree sums by body levels (L.Acc scratch: the
+// contact phase's bounding spheres and patch radii are dead after the row set-up). Returns b_i = S_i . F
+// for dof lane and dof 64 + lane (lanes < NH).
+HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, const float* vel, float& c1,
+                        float& c2) {
+    const bool bl = lane < NB;
+    const int b = bl ? lane : 0;
+    float Fb[6];
+    {
+        const uint32_t jp = bl ? T.jump4[b] : 0xFFFFFFFFu;
+        float vj[6];
+        if (b == 0) {
+            for (int x = 0; x < 6; ++x) vj[x] = vel[x];
+        } else {
+            const int d0 = T.dof0[b];
+            const float u0_ = vel[d0], u1_ = vel[d0 + 1], u2_ = vel[d0 + 2];
+            for (int x = 0; x < 6; ++x) vj[x] = L.S[d0][x] * u0_ + L.S[d0 + 1][x] * u1_ + L.S[d0 + 2][x] * u2_;
+        }
+        float V[6];
+        for (int x = 0; x < 6; ++x) V[x] = vj[x];
+        auto prefix6 = [&](float (&y)[6]) {
+            auto round = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                const int j = jump_of<K>(jp);
+                const int src = j < 0 ? lane : j;
+                float ya[6];
+#pragma unroll
+                for (int x = 0; x < 6; ++x) ya[x] = __shfl(y[x], src, W);
+                if (j >= 0)
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) y[x] += ya[x];
+            };
+            round(std::integral_constant<int, 0>{});
+            round(std::integral_constant<int, 1>{});
+            round(std::integral_constant<int, 2>{});
+            if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
+        };
+        prefix6(V);
+        const float v6[6] = {vel[0], vel[1], vel[2], vel[3], vel[4], vel[5]};
+        if (b != 0)
+            for (int x = 0; x < 6; ++x) V[x] += v6[x];
+        const f3 vxw = cross3(f3{v6[3], v6[4], v6[5]}, f3{v6[0], v6[1], v6[2]});
+        const float A0[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
+        float A[6];
+        if (b == 0) {
+            for (int x = 0; x < 6; ++x) A[x] = A0[x];
+        } else {
+            crm(V, vj, A);
+        }
+        prefix6(A);
+        if (b != 0)
+            for (int x = 0; x < 6; ++x) A[x] += A0[x];
+        float IA[6], IV[6], X[6];
+        si_apply(L.Ib[b], A, IA);
+        si_apply(L.Ib[b], V, IV);
+        crf(V, IV, X);
+        for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
+    }
+    sync();
+    if (bl)
+        for (int x = 0; x < 6; ++x) L.Acc[b][x] = Fb[x];
+    sync();
+    subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.Acc[0][0], nullptr, lane);
+    c1 = dot6(L.S[lane], L.Acc[dof_body(lane)]);
+    c2 = lane < regla::NH ? dot6(L.S[64 + lane], L.Acc[(64 + lane - 6) / 3 + 1]) : 0.f;
+}
+
+// the next position iteration's free motion: yh = D^-1/2 L^-T hs (kp (tgt - q) - c u - b) per dof (lane,
+// then 64 + lane), forward substituted from the stored factor (kp parked in L.dforce during the step,
+// c = hs kp + kd in L.coef, u the working velocity L.u0, b from tgs_bias_at)
+HE_DEV void tgs_rhs(Lds& L, const BodyTopo& T, int lane, float hs, float c1, float c2) {
+    using regla::NH;
+    auto rhs = [&](int i, float b) {
+        const bool jd = i >= 6;
+        const int d = jd ? i - 6 : 0;
+        const float drive = jd ? L.dforce[d] * (L.tgt[d] - L.q[d]) - L.coef[i] * L.u0[i] : 0.f;
+        return hs * (drive - b);
+    };
+    float y1 = rhs(lane, c1);
+    float y2 = lane < NH ? rhs(64 + lane, c2) : 0.f;
+    __builtin_amdgcn_s_setprio(kPrioSerial);
+    regla::solve_LT_vec_pipelined(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, y1, y2);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
+    L.yh[lane] = y1 * L.sDinv[lane];
+    if (lane < NH) L.yh[64 + lane] = y2 * L.sDinv[64 + lane];
+    sync();
+}
+
+// the working velocity's update by one iteration: u += L^-1 D^-1/2 (yh + extra), extra = Zh^T (the
+// iteration's impulse change) reduced into lane = dof (0 without contact rows)
+HE_DEV void tgs_velocity(Lds& L, const BodyTopo& T, int lane, float e1, float e2) {
+    using regla::NH;
+    float yl = (e1 + L.yh[lane]) * L.sDinv[lane];
+    float y2 = lane < NH ? (e2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
+    float r1[regla::kRowRegs], r2[regla::kRowRegs];
+    load_rows(L, T, lane, r1, r2);
+    __builtin_amdgcn_s_setprio(kPrioSerial);
+    solve_L(r1, r2, lane, yl, y2);
+    __builtin_amdgcn_s_setprio(kPrioDefault);
+    L.u0[lane] += yl;
+    if (lane < NH) L.u0[64 + lane] += y2;
+    sync();
+}
+
+// the iteration's implicit drive torque kp (tgt - q) - c u at its end velocity, accumulated per dof
+// (lane, then 64 + lane): the reported drive force is the iterations' mean
+HE_DEV void tgs_drive_acc(const Lds& L, int lane, float& f1, float& f2) {
+    auto tq = [&](int i) {
+        const int d = i - 6;
+        return L.dforce[d] * (L.tgt[d] - L.q[d]) - L.coef[i] * L.u0[i];
+    };
+    if (lane >= 6) f1 += tq(lane >= 6 ? lane : 6);
+    if (lane < regla::NH) f2 += tq(64 + lane);
+}
+
 // ---------------------------------------------------------------------------------- fused imitation
 // he_env_step's imitation step (reward / reset / observations + the device reset of flagged envs)
 // as the physics kernel's epilogue, from the post-step state in LDS: the same code as the stand-alone
@@ -1120,7 +1261,106 @@ HE_DEV SimBody body_row(const Lds& L, int b) {
     return s;
 }
 
+// ---------------------------------------------------------------------------------- integration
+// Damping, the angular-velocity clamps and the semi-implicit position update over hs in one pass per
+// body (lane = body). src: the solved generalized velocity (PGS: L.uf; TGS: the working velocity
+// L.u0). write_out: the damped, clamped velocity becomes the state's (PGS always; TGS the last
+// position iteration only: the solver's own velocity is not clamped, oracle substep_tgs). detect: the
+// next substep's limit rows from the new state.
+HE_DEV void integrate_bodies(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, float hs, float damp,
+                             const float* src, bool write_out, bool detect) {
+    // damping, the angular-velocity clamps and the semi-implicit position update in one pass per
+    // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
+    // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
+    f3 lim_th = f3{0.f, 0.f, 0.f}, lim_u = f3{0.f, 0.f, 0.f};  // the joint's new q and u
+    const bool bl = lane < NB;
+    const bool root = lane == 0;
+    const int d0 = root ? 0 : 6 + 3 * ((bl ? lane : 1) - 1);
+    float w[3] = {src[d0] * damp, src[d0 + 1] * damp, src[d0 + 2] * damp};
+    {
+        // the joint's relative rate: PhysX articulation joint maxJointVelocity
+        const float nrm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        if (!root && nrm > p.max_joint_velocity) {
+            const float s = p.max_joint_velocity / nrm;
+            w[0] *= s; w[1] *= s; w[2] *= s;
+        }
+        // the link's WORLD angular velocity (asset max_angular_velocity, PxRigidBody): w_b = w_parent +
+        // R_b u_b summed along the chain (Acc is scratch here), clamped link by link; the joint rates
+        // are then re-derived, u_b = R_b^T (w'_b - w'_parent) (oracle: the same pass)
+        // no link can be over when |w_root| + (joints on the longest chain) x max_j |u_j| stays under
+        // the cap (triangle inequality; a 1 % margin covers the prefix's rounding): the prefix and
+        // the clamp are then skipped (wave-uniform), with the result they would give
+        const float un = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        const float wroot = regla::rdlane(un, 0);
+        const bool may = bl && !root && un * (float)(smpl::kNumBodyLevels - 1) > 0.99f * p.max_angular_velocity - wroot;
+        if (__ballot(may) != 0ull) {
+        const f4 qb = bl ? f4{L.qw[lane][0], L.qw[lane][1], L.qw[lane][2], L.qw[lane][3]} : f4{0.f, 0.f, 0.f, 1.f};
+        const f3 wr = root ? f3{w[0], w[1], w[2]} : qapply(qb, f3{w[0], w[1], w[2]});
+        // chain prefix by pointer jumping (the table stops below the root: its rate is added last)
+        f3 wo = bl ? wr : f3{0.f, 0.f, 0.f};
+        {
+            const uint32_t jp = bl ? T.jump4[lane] : 0xFFFFFFFFu;
+            auto round = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                const int j = jump_of<K>(jp);
+                const int src = j < 0 ? lane : j;
+                const f3 wa = f3{__shfl(wo.x, src, W), __shfl(wo.y, src, W), __shfl(wo.z, src, W)};
+                if (j >= 0) wo = wo + wa;
+            };
+            round(std::integral_constant<int, 0>{});
+            round(std::integral_constant<int, 1>{});
+            round(std::integral_constant<int, 2>{});
+            if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
+            const f3 w0 = f3{__shfl(wr.x, 0, W), __shfl(wr.y, 0, W), __shfl(wr.z, 0, W)};
+            if (bl && !root) wo = wo + w0;
+        }
+        const float wmax = p.max_angular_velocity;
+        const float wn2 = dot3(wo, wo);
+        const bool over = bl && wn2 > wmax * wmax;
+        if (__ballot(over) != 0ull) {  // rare (wave-uniform branch)
+            const f3 wc = over ? wo * (wmax * __builtin_amdgcn_rsqf(wn2)) : wo;
+            const int pb = bl && !root ? T.chain[lane][T.depth[lane] - 1] : 0;
+            const f3 wp = f3{__shfl(wc.x, pb, W), __shfl(wc.y, pb, W), __shfl(wc.z, pb, W)};
+            if (bl) {
+                const f3 rel = root ? wc : wc - wp;
+                const f3 ub = root ? rel : qapply(qconj(qb), rel);
+                w[0] = ub.x; w[1] = ub.y; w[2] = ub.z;
+            }
+        }
+        }
+    }
+    if (bl) {
+        if (write_out) { L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2]; }
+        const int d = root ? 0 : 3 * (lane - 1);
+        const f3 dtw = f3{hs * w[0], hs * w[1], hs * w[2]};
+        const f4 ed = pqexp(dtw);  // exp(q_b) itself: the kinematics' qloc (L.q is unchanged since)
+        const f4 e1 = root ? ed : f4{L.qloc[lane][0], L.qloc[lane][1], L.qloc[lane][2], L.qloc[lane][3]};
+        const f4 e2 = root ? f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]} : ed;
+        const f4 nq = qnormalize(qmul(e1, e2));
+        if (root) {
+            if (write_out) { L.u0[3] = src[3]; L.u0[4] = src[4]; L.u0[5] = src[5]; }
+            for (int c = 0; c < 3; ++c) L.root_pos[c] += hs * src[3 + c];
+            L.root_q[0] = nq.x; L.root_q[1] = nq.y; L.root_q[2] = nq.z; L.root_q[3] = nq.w;
+        } else {
+            f3 nv = pqlog(nq);
+            f4 nql = nq;
+            if (p.joint_limits && limit_clamp(nq, nv, w)) {  // rare: the limit rows lost
+                if (write_out) { L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2]; }
+                nql = pqexp(nv);
+            }
+            L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
+            // the next substep's kinematics starts from this rotation instead of exp(log(.))
+            L.qloc[lane][0] = nql.x; L.qloc[lane][1] = nql.y; L.qloc[lane][2] = nql.z; L.qloc[lane][3] = nql.w;
+            lim_th = nv;
+            lim_u = f3{w[0], w[1], w[2]};
+        }
+    }
+    if (p.joint_limits && detect) limit_detect(L, lane, lane >= 1 && lane < NB, lim_th, lim_u, p);
+    sync();
+}
+
 // ---------------------------------------------------------------------------------- one substep
+template <bool TGS>
 HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float* mass_scale, float mu, int tkind, unsigned long long* stamps,
                     unsigned long long& t_prev, bool first, bool last) {
@@ -1148,6 +1388,10 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     const BodyTopo& T = L.T;
     const he_sim_params& p = a.p;
     const float dt = p.dt;
+    // TGS (solver_type 1, oracle substep_tgs): K position iterations of hs = dt / K on this step's
+    // factor and contact set; PGS: one step of hs = dt
+    const int K = TGS ? (p.solver_iterations < 1 ? 1 : (p.solver_iterations > kTgsMaxIt ? kTgsMaxIt : p.solver_iterations)) : 1;
+    const float hs = TGS ? dt / (float)K : dt;
     __builtin_amdgcn_s_setprio(kPrioDefault);
     kinematics<true>(L, m, lane, a.p, !first);
     __builtin_amdgcn_s_setprio(kPrioDefault);
@@ -1206,23 +1450,24 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float kp = m.stiffness[d] * p.kp_scale, kd = m.damping[d] * p.kd_scale;
         const float err = L.tgt[d] - L.q[d];
         const float u = L.u0[i];
-        float tau = kp * (err - dt * u) - kd * u;
+        float tau = kp * (err - hs * u) - kd * u;
         const float lim = m.effort[d];
         // effort limit: the implicit step's drive torque, estimated with the dof's own joint-space
         // inertia H_ii = S_i . IS_i (+ armature) as tau - c dt (tau - bias) / (H_ii + dt c), scales
         // the whole drive down to the limit (oracle/he_oracle_physics.c, the drive block)
         // A joint held at its angle limit cannot give way: its check takes the torque at rest.
-        const float c = dt * kp + kd;
+        const float c = hs * kp + kd;
         const float hii = dot6(L.S[i], L.IS[i]) + m.armature[d];
         const bool blocked = p.joint_limits && jd && ((limmask >> b) & 1u);
-        const float tau_i = blocked ? tau : tau - c * dt * (tau - bias) * __builtin_amdgcn_rcpf(hii + dt * c);
+        const float tau_i = blocked ? tau : tau - c * hs * (tau - bias) * __builtin_amdgcn_rcpf(hii + hs * c);
         const float sc = fabsf(tau_i) > lim ? lim / fabsf(tau_i) : 1.f;
         tau *= sc;
         kp *= sc;
         kd *= sc;
-        if (jd) L.dforce[d] = tau;
-        L.rhs[i] = dt * (jd ? tau - bias : -bias);
-        L.coef[i] = jd ? dt * kp + kd : 0.f;
+        if (jd) L.dforce[d] = TGS ? kp : tau;  // TGS: the scaled stiffness, for the iterations' drives
+        if constexpr (TGS) L.uf[i] = bias;       // TGS: the bias at u0 (bias_midpoint 0 keeps it)
+        L.rhs[i] = hs * (jd ? tau - bias : -bias);
+        L.coef[i] = jd ? hs * kp + kd : 0.f;
     };
     dof_terms(lane, true);
     if (lane < NG - W) dof_terms(W + lane, false);
@@ -1234,8 +1479,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float Sj[6], Sj2[6];
         for (int x = 0; x < 6; ++x) { Sj[x] = L.S[lane][x]; Sj2[x] = lane < NH ? L.S[64 + lane][x] : 0.f; }
         // per-lane diagonal addend (dof = lane, and 64 + lane on lanes < 11), loaded once
-        const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + dt * L.coef[lane] : 0.f;
-        const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + dt * L.coef[64 + lane] : 0.f;
+        const float dadd = lane >= 6 ? m.armature[lane >= 6 ? lane - 6 : 0] + hs * L.coef[lane] : 0.f;
+        const float dadd2 = lane < NH ? m.armature[lane < NH ? 58 + lane : 0] + hs * L.coef[64 + lane] : 0.f;
         (void)Sj; (void)Sj2;
         crba_mfma(M, L, lane, dadd, dadd2);
     }
@@ -1257,7 +1502,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     }
     sync();
     STAMP(5);
-    if (p.bias_midpoint) bias_midpoint(L, T, lane, p, stamps, t_prev);
+    if (!TGS && p.bias_midpoint) bias_midpoint(L, T, lane, p, stamps, t_prev);
     // the contact phase's model reads (geometry of the lane's body, self-collision pair indices)
     // depend on nothing computed here: issued now, they land behind the free-velocity sweep
     constexpr int ROUNDS = (HE_MAX_PAIRS + W - 1) / W;
@@ -1364,7 +1609,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         if (self_col && lane < NB) {
             // world segments (the Ib scratch is dead after the subtree sums), and the bounding
             // sphere about the segment midpoint for the pair cull as one 16-byte record
-            float* sg = L.Ib[lane];
+            float* sg = TGS ? L.Ic[lane] : L.Ib[lane];  // TGS: Ib (own inertias) serves the iterations' bias
             sg[0] = P0.x; sg[1] = P0.y; sg[2] = P0.z; sg[3] = P1.x; sg[4] = P1.y; sg[5] = P1.z; sg[6] = rs;
             const f3 mid = (P0 + P1) * 0.5f;
             bsph(L)[lane] = make_float4(mid.x, mid.y, mid.z, 0.5f * norm3(P1 - P0) + rs);
@@ -1495,8 +1740,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 const int e = list[lane];
                 i = (e >> 16) & 0xFF;
                 j = (e >> 24) & 0xFF;
-                const float* si = L.Ib[i];
-                const float* sj = L.Ib[j];
+                const float* si = TGS ? L.Ic[i] : L.Ib[i];
+                const float* sj = TGS ? L.Ic[j] : L.Ib[j];
                 const float ri = si[6], rj = sj[6];
                 f3 ci, cj;
                 seg_seg(f3{si[0], si[1], si[2]}, f3{si[3], si[4], si[5]}, f3{sj[0], sj[1], sj[2]}, f3{sj[3], sj[4], sj[5]}, ci, cj);
@@ -1729,6 +1974,31 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         }
     }
     static_assert(2 * kCand + 3 * W <= NG * 6, "per-row force directions fit IS");
+    const float damp = 1.0f / (1.0f + dt * p.angular_damping);
+    float tf1 = 0.f, tf2 = 0.f;  // TGS: the iterations' drive torques, summed per dof (lane, 64 + lane)
+    // TGS: what follows a position iteration's velocity update: its drive torques, the positions by hs
+    // (the last iteration: the step's output velocity), then (not the last) the next iteration's bias
+    // and free motion
+    auto tgs_advance = [&](bool lastit) {
+        tgs_drive_acc(L, lane, tf1, tf2);
+        integrate_bodies(L, T, lane, p, hs, damp, L.u0, lastit, lastit && !last);
+        if (!lastit) {
+            float c1, c2;
+            if (p.bias_midpoint) {
+                tgs_bias_at(L, T, lane, p, L.u0, c1, c2);
+            } else {
+                c1 = L.uf[lane];
+                c2 = lane < NH ? L.uf[64 + lane] : 0.f;
+            }
+            tgs_rhs(L, T, lane, hs, c1, c2);
+        }
+    };
+    // TGS: the reported drive force, the iterations' mean (the joint-limit force is added by the caller)
+    auto tgs_drive_out = [&]() {
+        if (lane >= 6) L.dforce[lane >= 6 ? lane - 6 : 0] = tf1 / (float)K;
+        if (lane < NH) L.dforce[58 + lane] = tf2 / (float)K;
+        sync();
+    };
     if (nr > 0) {
         // ---- contact rows, one per lane: z = J_r^T, brow = J_r uf + bias, then z <- D^-1/2 L^-T z
         // (dofs outside every row's support stay zero and are skipped wave-uniformly), so that the
@@ -1761,7 +2031,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
             if (act && kind == 0) {
                 const float g = L.cgap[rs_];
-                brow += g >= 0.f ? g / dt : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
+                brow += g >= 0.f ? g / hs : fmaxf(p.baumgarte * g / hs, -p.max_depenetration_velocity);
             }
             STAMP(20);
             __builtin_amdgcn_s_setprio(kPrioSerial);
@@ -1804,6 +2074,152 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             else delassus_mfma(z, acol, live);
         }
         STAMP(9);
+        if constexpr (TGS) {
+            // ---- TGS position iterations (oracle substep_tgs): each one Gauss-Seidel sweep on the
+            // accumulated impulses, started from them plus the previous iteration's change (the first:
+            // the cached change of the previous step), against J u of the iteration's free velocity and
+            // the bias of the row's separation, advanced by hs J_r u after each iteration
+            const float invd = 1.0f / (act ? diag + 1e-12f : 1.f);
+            const float ninvd = -invd;
+            const int nrb = __builtin_amdgcn_readfirstlane(nr);
+            float ap[MAXR];  // -A[r][lane] / A[lane][lane], the row-count class's rows
+            {
+                auto prep = [&](auto r0c) {
+                    constexpr int R0 = decltype(r0c)::value;
+#pragma unroll
+                    for (int r = R0; r < (R0 + 16 < MAXR ? R0 + 16 : MAXR); ++r) ap[r] = acol[r] * ninvd;
+                };
+                prep(std::integral_constant<int, 0>{});
+                if (nrb > 16) prep(std::integral_constant<int, 16>{});
+                if (nrb > 32) prep(std::integral_constant<int, 32>{});
+                if (nrb > 48) prep(std::integral_constant<int, 48>{});
+            }
+            // sum_R ap[R] x_R (x_R from lane R, four lanes per block of SGPRs)
+            auto aprod = [&](float x) {
+                float acc = 0.f;
+                if (__ballot(x != 0.f)) {  // wave-uniform; rows >= nr hold nothing
+                    auto aw = [&](auto nrows) {
+                        constexpr int NRW = decltype(nrows)::value;
+                        float wa[4] = {0.f, 0.f, 0.f, 0.f};
+                        regla::static_for<0, NRW, 4>([&](auto rc) {
+                            constexpr int r0 = decltype(rc)::value;
+                            float sv[4];
+                            regla::rdlane4<r0>(x, sv);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                if (r0 + q < NRW) wa[(r0 + q) & 3] = fmaf(ap[r0 + q < NRW ? r0 + q : 0], sv[q], wa[(r0 + q) & 3]);
+                        });
+                        acc = (wa[0] + wa[1]) + (wa[2] + wa[3]);
+                    };
+                    if (nrb <= 16) aw(std::integral_constant<int, 16>{});
+                    else if (nrb <= 32) aw(std::integral_constant<int, 32>{});
+                    else if (nrb <= 48) aw(std::integral_constant<int, 48>{});
+                    else aw(std::integral_constant<int, MAXR>{});
+                }
+                return acc;
+            };
+            const bool isn = kind == 0;
+            const float muw = L.lam[lane];  // the friction bound weight parked by the row set-up
+            uint32_t mlo = 0u, mhi = 0u;
+            if (act && !isn) {
+                const int pc = rb1 == -1 ? L.tcnt[rb0] : 1;
+                const uint64_t pm = ((1ull << pc) - 1ull) << (lane - (kind - 1) - pc);
+                mlo = (uint32_t)pm;
+                mhi = (uint32_t)(pm >> 32);
+            }
+            const int n0 = act && !isn ? (int)__builtin_ctzll(((uint64_t)mhi << 32) | mlo) : 0;
+            auto patch_bound = [&](float lv) {  // muw x the patch's normal impulses (<= 4 rows)
+                float bnd = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = __shfl(lv, (n0 + j) & (W - 1), W);
+                    const int bit = n0 + j;
+                    const bool in = bit < 32 ? ((mlo >> (bit & 31)) & 1u) : ((mhi >> (bit & 31)) & 1u);
+                    bnd += in ? v : 0.f;
+                }
+                return bnd * muw;
+            };
+            auto gbias = [&](float g) {
+                return g >= 0.f ? g / hs : fmaxf(p.baumgarte * g / hs, -p.max_depenetration_velocity);
+            };
+            const float kInf = __builtin_inff();
+            float sep = act && isn ? L.cgap[rs_] : 0.f;  // the row's separation (a limit row: its angle gap)
+            float bb = act && isn ? gbias(sep) : 0.f;   // its bias (brow holds it)
+            float applied = 0.f;                         // the impulse already in the working velocity
+            lamv = lam0;
+            float cd = act ? -brow * invd + aprod(lam0) : 0.f;
+            float bnd = patch_bound(lamv);
+            float lo = isn ? -lamv : -bnd - lamv;
+            float hi = isn ? kInf : bnd - lamv;
+            float dl = 0.f;
+            const int nru = __builtin_amdgcn_readfirstlane(nr);
+            for (int it = 0; it < K; ++it) {
+                float dvec = 0.f;
+                int nrs = nru;
+                asm volatile("" : "+s"(nrs));
+                regla::f2v ch = {cd, hi};
+                __builtin_amdgcn_s_setprio(kPrioSerial);
+                if (nrs <= 16) pgs_sweep_tgs<0, 16>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                else if (nrs <= 32) pgs_sweep_tgs<0, 32>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                else if (nrs <= 48) pgs_sweep_tgs<0, 48>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                else pgs_sweep_tgs<0, MAXR>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                __builtin_amdgcn_s_setprio(kPrioDefault);
+                cd = ch.x;
+                lamv += dvec;
+                dl = act ? lamv - applied : 0.f;  // this iteration's impulse change
+                applied = lamv;
+                const float v = act ? -cd * (diag + 1e-12f) - bb : 0.f;  // J_r u after the sweep
+                {  // the working velocity: u += L^-1 D^-1/2 (yh + Zh^T dl)
+                    float v64[64], v16[16];
+#pragma unroll
+                    for (int i = 0; i < 64; ++i) v64[i] = ZV(z, i) * dl;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? ZV(z, 64 + i < NG ? 64 + i : 0) * dl : 0.f;
+                    const float e1 = reduce_scatter<64>(v64);
+                    const float e2 = __shfl(reduce_scatter<16>(v16), 4 * (lane & 15), W);
+                    tgs_velocity(L, T, lane, e1, lane < NH ? e2 : 0.f);
+                }
+                if (isn) sep += hs * v;
+                const bool lastit = it + 1 == K;
+                tgs_advance(lastit);
+                if (!lastit) {
+                    // the next sweep's start: w = J u + zh . yh + bias(sep) + A dl about lambda = applied + dl
+                    const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
+                    float yacc[4] = {0.f, 0.f, 0.f, 0.f};
+                    regla::static_for<0, NG, 4>([&](auto ic) {
+                        constexpr int i0 = decltype(ic)::value;
+                        float sv[4];
+                        if constexpr (i0 < 64) regla::rdlane4<i0>(yhl, sv);
+                        else regla::rdlane4<i0 - 64>(yh2, sv);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (i0 + q < NG) yacc[(i0 + q) & 3] = fmaf(ZV(z, i0 + q < NG ? i0 + q : 0), sv[q], yacc[(i0 + q) & 3]);
+                    });
+                    const float zy = (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
+                    bb = act && isn ? gbias(sep) : 0.f;
+                    lamv = applied + dl;
+                    cd = act ? -(v + zy + bb) * invd + aprod(dl) : 0.f;
+                    bnd = patch_bound(lamv);
+                    lo = isn ? -lamv : -bnd - lamv;
+                    hi = isn ? kInf : bnd - lamv;
+                }
+            }
+            // the cache keeps the last iteration's change (the next step's first start); the reported
+            // forces take the accumulated impulses
+            L.lam[lane] = act ? dl : 0.f;
+            if (lane == 0) L.nwc = p.warm_start ? nr : 0;
+            tgs_drive_out();
+            // the joint-limit force (dof_force = drive and limit together): limit row c = slot c
+            const int nl = __builtin_amdgcn_readfirstlane(L.nlim);
+            if (lane < nl) {
+                const int d0 = 3 * ((L.cbb[lane < MAXC ? lane : 0] & 0xFF) - 1);
+                const float lf = lamv / dt;
+                L.dforce[d0] += L.cx[lane < MAXC ? lane : 0][0] * lf;
+                L.dforce[d0 + 1] += L.cx[lane < MAXC ? lane : 0][1] * lf;
+                L.dforce[d0 + 2] += L.cx[lane < MAXC ? lane : 0][2] * lf;
+            }
+            sync();
+        } else {
         // ---- projected Gauss-Seidel over the rows (pgs_sweep): lane r keeps its unconstrained change,
         // its impulse and its bounds
         {
@@ -1933,6 +2349,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             L.uf[lane] = L.u0[lane] + yl;
             if (lane < NH) L.uf[64 + lane] = L.u0[64 + lane] + y2;
         }
+        }  // PGS
         // ---- reported contact forces (net linear contact impulse per body / dt): the output is the
         // last substep's, so the earlier substeps skip them (their cf rows stay zero, as set above)
         if (last) {
@@ -1974,7 +2391,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         L.lam[lane] = 0.f;
         if (lane == 0) L.nwc = 0;
     }
-    if (nr == 0) {  // no contact: uf = u0 + L^-1 D^-1/2 yh
+    if (TGS && nr == 0) {  // TGS without contact rows: the iterations' drives and bias only
+        for (int it = 0; it < K; ++it) {
+            tgs_velocity(L, T, lane, 0.f, 0.f);
+            tgs_advance(it + 1 == K);
+        }
+        tgs_drive_out();
+    }
+    if (!TGS && nr == 0) {  // no contact: uf = u0 + L^-1 D^-1/2 yh
         float yl = L.yh[lane] * L.sDinv[lane];
         float y2 = lane < NH ? L.yh[64 + lane] * L.sDinv[64 + lane] : 0.f;
         float r1[regla::kRowRegs], r2[regla::kRowRegs];
@@ -1985,8 +2409,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         sync();
     }
     STAMP(11);
+    if constexpr (TGS) {  // TGS: the iterations integrated the positions and set the drive force
+        STAMP(12);
+        return;
+    }
     // ---- drive force actually applied, damping, clamps, write velocities
-    const float damp = 1.0f / (1.0f + dt * p.angular_damping);
     if (last) {  // the reported drive force is the last substep's
         for (int i = lane; i < NG; i += W)
             if (i >= 6) L.dforce[i - 6] -= L.coef[i] * (L.uf[i] - L.u0[i]);
@@ -2004,94 +2431,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         }
         sync();
     }
-    // damping, the angular-velocity clamps and the semi-implicit position update in one pass per
-    // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
-    // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
-    f3 lim_th = f3{0.f, 0.f, 0.f}, lim_u = f3{0.f, 0.f, 0.f};  // the joint's new q and u
-    const bool bl = lane < NB;
-    const bool root = lane == 0;
-    const int d0 = root ? 0 : 6 + 3 * ((bl ? lane : 1) - 1);
-    float w[3] = {L.uf[d0] * damp, L.uf[d0 + 1] * damp, L.uf[d0 + 2] * damp};
-    {
-        // the joint's relative rate: PhysX articulation joint maxJointVelocity
-        const float nrm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        if (!root && nrm > p.max_joint_velocity) {
-            const float s = p.max_joint_velocity / nrm;
-            w[0] *= s; w[1] *= s; w[2] *= s;
-        }
-        // the link's WORLD angular velocity (asset max_angular_velocity, PxRigidBody): w_b = w_parent +
-        // R_b u_b summed along the chain (Acc is scratch here), clamped link by link; the joint rates
-        // are then re-derived, u_b = R_b^T (w'_b - w'_parent) (oracle: the same pass)
-        // no link can be over when |w_root| + (joints on the longest chain) x max_j |u_j| stays under
-        // the cap (triangle inequality; a 1 % margin covers the prefix's rounding): the prefix and
-        // the clamp are then skipped (wave-uniform), with the result they would give
-        const float un = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        const float wroot = regla::rdlane(un, 0);
-        const bool may = bl && !root && un * (float)(smpl::kNumBodyLevels - 1) > 0.99f * p.max_angular_velocity - wroot;
-        if (__ballot(may) != 0ull) {
-        const f4 qb = bl ? f4{L.qw[lane][0], L.qw[lane][1], L.qw[lane][2], L.qw[lane][3]} : f4{0.f, 0.f, 0.f, 1.f};
-        const f3 wr = root ? f3{w[0], w[1], w[2]} : qapply(qb, f3{w[0], w[1], w[2]});
-        // chain prefix by pointer jumping (the table stops below the root: its rate is added last)
-        f3 wo = bl ? wr : f3{0.f, 0.f, 0.f};
-        {
-            const uint32_t jp = bl ? T.jump4[lane] : 0xFFFFFFFFu;
-            auto round = [&](auto kc) {
-                constexpr int K = decltype(kc)::value;
-                const int j = jump_of<K>(jp);
-                const int src = j < 0 ? lane : j;
-                const f3 wa = f3{__shfl(wo.x, src, W), __shfl(wo.y, src, W), __shfl(wo.z, src, W)};
-                if (j >= 0) wo = wo + wa;
-            };
-            round(std::integral_constant<int, 0>{});
-            round(std::integral_constant<int, 1>{});
-            round(std::integral_constant<int, 2>{});
-            if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
-            const f3 w0 = f3{__shfl(wr.x, 0, W), __shfl(wr.y, 0, W), __shfl(wr.z, 0, W)};
-            if (bl && !root) wo = wo + w0;
-        }
-        const float wmax = p.max_angular_velocity;
-        const float wn2 = dot3(wo, wo);
-        const bool over = bl && wn2 > wmax * wmax;
-        if (__ballot(over) != 0ull) {  // rare (wave-uniform branch)
-            const f3 wc = over ? wo * (wmax * __builtin_amdgcn_rsqf(wn2)) : wo;
-            const int pb = bl && !root ? T.chain[lane][T.depth[lane] - 1] : 0;
-            const f3 wp = f3{__shfl(wc.x, pb, W), __shfl(wc.y, pb, W), __shfl(wc.z, pb, W)};
-            if (bl) {
-                const f3 rel = root ? wc : wc - wp;
-                const f3 ub = root ? rel : qapply(qconj(qb), rel);
-                w[0] = ub.x; w[1] = ub.y; w[2] = ub.z;
-            }
-        }
-        }
-    }
-    if (bl) {
-        L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
-        const int d = root ? 0 : 3 * (lane - 1);
-        const f3 dtw = f3{dt * w[0], dt * w[1], dt * w[2]};
-        const f4 ed = pqexp(dtw);  // exp(q_b) itself: the kinematics' qloc (L.q is unchanged since)
-        const f4 e1 = root ? ed : f4{L.qloc[lane][0], L.qloc[lane][1], L.qloc[lane][2], L.qloc[lane][3]};
-        const f4 e2 = root ? f4{L.root_q[0], L.root_q[1], L.root_q[2], L.root_q[3]} : ed;
-        const f4 nq = qnormalize(qmul(e1, e2));
-        if (root) {
-            L.u0[3] = L.uf[3]; L.u0[4] = L.uf[4]; L.u0[5] = L.uf[5];
-            for (int c = 0; c < 3; ++c) L.root_pos[c] += dt * L.uf[3 + c];
-            L.root_q[0] = nq.x; L.root_q[1] = nq.y; L.root_q[2] = nq.z; L.root_q[3] = nq.w;
-        } else {
-            f3 nv = pqlog(nq);
-            f4 nql = nq;
-            if (p.joint_limits && limit_clamp(nq, nv, w)) {  // rare: the limit rows lost
-                L.u0[d0] = w[0]; L.u0[d0 + 1] = w[1]; L.u0[d0 + 2] = w[2];
-                nql = pqexp(nv);
-            }
-            L.q[d] = nv.x; L.q[d + 1] = nv.y; L.q[d + 2] = nv.z;
-            // the next substep's kinematics starts from this rotation instead of exp(log(.))
-            L.qloc[lane][0] = nql.x; L.qloc[lane][1] = nql.y; L.qloc[lane][2] = nql.z; L.qloc[lane][3] = nql.w;
-            lim_th = nv;
-            lim_u = f3{w[0], w[1], w[2]};
-        }
-    }
-    if (p.joint_limits && !last) limit_detect(L, lane, lane >= 1 && lane < NB, lim_th, lim_u, p);
-    sync();
+    integrate_bodies(L, T, lane, p, dt, damp, L.uf, true, !last);
     STAMP(12);
 }
 
@@ -2104,7 +2444,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
 #ifndef HE_MIN_WAVES
 #define HE_MIN_WAVES 2
 #endif
-__global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
+template <bool TGS>
+HE_DEV void physics_body(const PhysArgs& a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
     const int e = blockIdx.x;
@@ -2191,7 +2532,8 @@ __global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
     int tk = (a.p.terrain && a.terrain_kind) ? a.terrain_kind[e] : 0;
     unsigned long long* stamps = a.stamps ? a.stamps + (size_t)e * HE_STAMP_SLOTS : nullptr;
     unsigned long long t_prev = __builtin_readcyclecounter();
-    for (int s = 0; s < a.substeps; ++s) substep(L, a, a.model, lane, ms, mu, tk, stamps, t_prev, s == 0, s == a.substeps - 1);
+    for (int s = 0; s < a.substeps; ++s)
+        substep<TGS>(L, a, a.model, lane, ms, mu, tk, stamps, t_prev, s == 0, s == a.substeps - 1);
     // ---- fused imitation (he_env_step): the reference samples depend only on the env's motion
     // bookkeeping (read into LDS at the kernel's start), so their loads are issued here and land
     // behind the final kinematics and stores
@@ -2258,6 +2600,11 @@ __global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) {
     }
 }
 
+// he_sim_params.solver_type 0 (PGS) and 1 (TGS): one instantiation each, so that the TGS iterations'
+// register plan does not touch the PGS kernel's
+__global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel(PhysArgs a) { physics_body<false>(a); }
+__global__ void __launch_bounds__(64, HE_MIN_WAVES) physics_kernel_tgs(PhysArgs a) { physics_body<true>(a); }
+
 }  // namespace
 
 static_assert(sizeof(Lds) <= 20480, "two workgroups per SIMD (8 per CU) need <= 20 KB of LDS each");
@@ -2272,6 +2619,11 @@ namespace {
 __global__ void warm_tu_kernel() {}
 }  // namespace
 
+#define HE_RETURN_IF(x)                      \
+    do {                                     \
+        const hipError_t e_ = (x);           \
+        if (e_ != hipSuccess) return e_;     \
+    } while (0)
 hipError_t warm_physics_kernels(hipStream_t stream, int mode) {
     if (mode == 1) {
         warm_tu_kernel<<<1, 64, 0, stream>>>();
@@ -2279,12 +2631,15 @@ hipError_t warm_physics_kernels(hipStream_t stream, int mode) {
     }
     PhysArgs pa{};
     physics_kernel<<<1, W, physics_lds_bytes(), stream>>>(pa);
+    HE_RETURN_IF(hipGetLastError());
+    physics_kernel_tgs<<<1, W, physics_lds_bytes(), stream>>>(pa);
     return hipGetLastError();
 }
 
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream) {
     if (a.num_envs <= 0) return hipSuccess;
     const size_t lds = physics_lds_bytes();
-    physics_kernel<<<a.num_envs, W, lds, stream>>>(a);
+    if (a.p.solver_type == 1) physics_kernel_tgs<<<a.num_envs, W, lds, stream>>>(a);
+    else physics_kernel<<<a.num_envs, W, lds, stream>>>(a);
     return hipGetLastError();
 }
