@@ -2031,7 +2031,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
             if (act && kind == 0) {
                 const float g = L.cgap[rs_];
-                brow += g >= 0.f ? g / hs : fmaxf(p.baumgarte * g / hs, -p.max_depenetration_velocity);
+                // speculative: close within the solve's step; penetrating: recover at baumgarte per physics
+                // step (TGS too: oracle contact_bias)
+                brow += g >= 0.f ? g / hs : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             }
             STAMP(20);
             __builtin_amdgcn_s_setprio(kPrioSerial);
@@ -2140,7 +2142,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 return bnd * muw;
             };
             auto gbias = [&](float g) {
-                return g >= 0.f ? g / hs : fmaxf(p.baumgarte * g / hs, -p.max_depenetration_velocity);
+                return g >= 0.f ? g / hs : fmaxf(p.baumgarte * g / dt, -p.max_depenetration_velocity);
             };
             const float kInf = __builtin_inff();
             float sep = act && isn ? L.cgap[rs_] : 0.f;  // the row's separation (a limit row: its angle gap)

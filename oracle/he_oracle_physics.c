@@ -742,12 +742,16 @@ typedef struct warm_cache {
     R lam[MAXROW];
 } warm_cache;
 
-/* The contact row's velocity bias at separation `gap` over a step of h: a speculative contact (gap >= 0)
- * may close its gap within the step, a penetrating one is pushed out at baumgarte * gap / h, at most
- * max_depenetration_velocity (isaacgym_env.py:22). TGS (solver_type 1) takes it per position iteration
- * with h = dt / iterations, from the separation its earlier iterations left. */
-static R contact_bias(const he_sim_params* p, R gap, R h) {
-    return gap >= 0 ? gap / h : fmax(p->baumgarte * gap / h, -p->max_depenetration_velocity);
+/* The contact row's velocity bias at separation `gap`: a speculative contact (gap >= 0) may close its gap
+ * within the solve's step h, a penetrating one is pushed out at baumgarte * gap / dt, at most
+ * max_depenetration_velocity (isaacgym_env.py:22), dt the physics step. TGS (solver_type 1) takes it
+ * per position iteration (h = dt / iterations) from the separation its earlier iterations left; the
+ * recovery rate of a penetration stays per physics step, whatever the iteration count (per iteration,
+ * baumgarte * gap / h would push a 5 cm self-penetration out at 4x the PGS step's rate: under
+ * saturated random actions that wedged limbs and launched 3 of 4096 standing bodies past 15 m/s,
+ * tests/diag/tgs_study.py). */
+static R contact_bias(const he_sim_params* p, R gap, R h, R dt) {
+    return gap >= 0 ? gap / h : fmax(p->baumgarte * gap / dt, -p->max_depenetration_velocity);
 }
 /* diagnostic (tests/diag/tgs_study.py): TGS with the positions integrated once per position iteration
  * (h = dt / K, each with that iteration's velocity) instead of once with the iterations' mean velocity
@@ -1052,7 +1056,7 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
             R ju = 0;
             for (int i = 0; i < NG; ++i) ju += z[i] * uf[i];
             R bb = 0;
-            if (w->kind == 0) bb = contact_bias(p, c->gap, h);
+            if (w->kind == 0) bb = contact_bias(p, c->gap, h, dt);
             brow0[r] = ju;
             sep[r] = w->kind == 0 ? c->gap : 0;
             brow[r] = ju + bb;
@@ -1116,7 +1120,7 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
                         R v = brow0[r]; /* J_r u_k = J_r uf + (A lambda)_r */
                         for (int j = 0; j < nr; ++j) v += A[r][j] * lam[j];
                         sep[r] += h * v;
-                        brow[r] = brow0[r] + contact_bias(p, sep[r], h);
+                        brow[r] = brow0[r] + contact_bias(p, sep[r], h, dt);
                     }
                 continue;
             }
@@ -1361,7 +1365,7 @@ static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p
             for (int r = 0; r < nr; ++r) {
                 R ju = 0;
                 for (int i = 0; i < NG; ++i) ju += J[r][i] * unew[i];
-                brow[r] = ju * fprobe[r] + (rows[r].kind == 0 ? contact_bias(p, sep[r], h) : 0);
+                brow[r] = ju * fprobe[r] + (rows[r].kind == 0 ? contact_bias(p, sep[r], h, dt) : 0);
             }
             for (int r = 0; r < nr; ++r) lam[r] = applied[r] + guess[r];
             for (int r = 0; r < nr; ++r) { /* one Gauss-Seidel sweep on the accumulated impulses */
