@@ -2,7 +2,8 @@
 
 One "step" = one policy step of every env on every rank: actions -> PD targets -> 2 gym.simulate()
 calls of 1/60 s, each 2 physics substeps of 1/120 s (Isaac Gym's SimParams.substeps default; DESIGN
-§5) -> reward / reset / 934-float obs -> device-side reset of flagged envs
+§5) solved by PhysX TGS's 4 position iterations (isaacgym_env.py:16-18) -> reward / reset /
+934-float obs -> device-side reset of flagged envs
 (puffer_phc/clean_pufferl/env.py:109-183 semantics; env-steps/s definition env.py:217-230).
 
 Default workload = BASELINE configs[1]: 4096 SMPL-neutral humanoids per GPU, PD stand-still
@@ -50,13 +51,14 @@ def parse(argv=None):
     ap.add_argument("--cpu-envs", type=int, default=2048)
     ap.add_argument("--cpu-steps", type=int, default=300)
     ap.add_argument("--max-contacts", type=int, default=40)
-    ap.add_argument("--scheme", choices=["default", "r02", "tgs", "tgs_small"], default="default",
-                    help="physics scheme: default = 2 simulate() x 2 substeps of 1/120 s, midpoint bias, 8 PGS sweeps, "
-                         "link world angular-velocity clamp; r02 = round 2's energy-unstable step (2 x 1/60 s, "
-                         "explicit bias, 8 sweeps) with round 3's clamps, for the cost comparison only (DESIGN §5); tgs = "
-                         "PhysX TGS (solver_type 1, isaacgym_env.py:16-18): 4 position iterations inside each 1/120 s "
-                         "physics step on its factor and contact set (DESIGN §5 'TGS'); tgs_small = TGS's small-step "
-                         "form, 8 substeps of 1/480 s per simulate() with one sweep each")
+    ap.add_argument("--scheme", choices=["default", "pgs", "r02", "tgs_small"], default="default",
+                    help="physics scheme: default = the reference's PhysX TGS (solver_type 1, isaacgym_env.py:16-18): "
+                         "2 simulate() x 2 substeps of 1/120 s, each 4 position iterations on its factor and contact "
+                         "set (DESIGN §5 'TGS'); pgs = the engine's velocity-level PGS step (rounds 1-4's default: 8 "
+                         "warm-started sweeps per 1/120 s step, midpoint bias); r02 = round 2's energy-unstable step "
+                         "(2 x 1/60 s, explicit bias, 8 PGS sweeps) with round 3's clamps, for the cost comparison "
+                         "only (DESIGN §5); tgs_small = TGS's small-step form, 8 PGS substeps of 1/480 s per simulate() "
+                         "with one sweep each")
     ap.add_argument("--solver-tolerance", type=float, default=None,
                     help="he_sim_params.solver_tolerance override (m/s; 0 = every sweep runs)")
     ap.add_argument("--no-puffer-level", action="store_true",
@@ -387,19 +389,20 @@ def scheme_params(args):
     """he_sim_params overrides of the --scheme and --solver-tolerance."""
     out = {}
     if getattr(args, "scheme", "default") == "r02":
-        out = dict(substeps=1, bias_midpoint=0, solver_iterations=8)
-    elif getattr(args, "scheme", "default") == "tgs":
-        out = dict(solver_type=1, solver_iterations=4)
+        out = dict(substeps=1, bias_midpoint=0, solver_type=0, solver_iterations=8)
+    elif getattr(args, "scheme", "default") == "pgs":
+        out = dict(solver_type=0, solver_iterations=8)
     elif getattr(args, "scheme", "default") == "tgs_small":
-        out = dict(substeps=8, solver_iterations=1)
+        out = dict(substeps=8, solver_type=0, solver_iterations=1)
     if getattr(args, "solver_tolerance", None) is not None:
         out["solver_tolerance"] = args.solver_tolerance
     return out
 
 
 def scheme_leg(args, model, device_index, scheme="r02", steps=50, warmup=10):
-    """The bench workload under another physics scheme, timed the same way: the cost of the
-    energy-stable default against round 2's scheme (2 x 1/60 s, explicit bias, 8 sweeps)."""
+    """The bench workload under another physics scheme (--scheme), timed the same way: the default
+    TGS step against the engine's PGS step, round 2's scheme (2 x 1/60 s, explicit bias, 8 sweeps) and
+    TGS's small-step form."""
     import torch
     a = argparse.Namespace(**vars(args))
     a.scheme = scheme
@@ -618,7 +621,8 @@ def main():
         # measured matrix-core busy share (rocprofv3 SQ counters)
         phys_roof = {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                     "kernel": f"physics_kernel (fp32 VALU + MFMA; SURVEY §8d canonical 0.6546 MFLOP per physics step "
+                     "kernel": f"{'physics_kernel_tgs' if scheme_params(args).get('solver_type', 1) == 1 else 'physics_kernel'} "
+                               f"(fp32 VALU + MFMA; SURVEY §8d canonical 0.6546 MFLOP per physics step "
                                f"x {2 * sim_substeps(args)} physics steps per env-step)",
                      "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma}
         if split is not None:  # the fused launch (physics + the imitation epilogue) is the dominant kernel
@@ -669,7 +673,7 @@ def main():
                 line["r02_scheme"] = scheme_leg(args, model, local)
             except Exception as exc:  # report, never fake
                 line["r02_scheme"] = {"value": None, "error": repr(exc)}
-            for sch in ("tgs", "tgs_small"):
+            for sch in ("pgs", "tgs_small"):
                 try:
                     line[f"{sch}_scheme"] = scheme_leg(args, model, local, scheme=sch)
                 except Exception as exc:  # report, never fake

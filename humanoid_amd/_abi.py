@@ -127,7 +127,7 @@ def default_sim_params(**kw) -> HeSimParams:
     p.max_depenetration_velocity = 10.0
     p.angular_damping = 0.01
     p.max_angular_velocity = 100.0
-    p.solver_iterations = 8  # PGS sweeps per physics step (4 leave 100x the one-step deviation)
+    p.solver_iterations = 4  # TGS position iterations per physics step (num_position_iterations, isaacgym_env.py:17)
     p.self_collision = 1
     p.max_contacts = 40
     p.kp_scale = 1.0
@@ -143,10 +143,18 @@ def default_sim_params(**kw) -> HeSimParams:
     p.bias_midpoint = 1  # explicit bias pumps energy under per-step random targets
     p.substeps = 2  # gymapi.SimParams.substeps default (not set by isaacgym_env.py:6-35)
     p.max_joint_velocity = 100.0  # PhysX articulation joint maxJointVelocity default
-    p.solver_type = 0  # 0 PGS (velocity level, solver_iterations sweeps), 1 TGS (isaacgym_env.py:16-18)
+    p.solver_type = 1  # TGS, the reference's solver (isaacgym_env.py:16-18); 0: PGS (pgs_sim_params)
     for k, v in kw.items():
         setattr(p, k, v)
     return p
+
+
+def pgs_sim_params(**kw) -> HeSimParams:
+    """The engine's velocity-level PGS step (solver_type 0, 8 warm-started sweeps per 1/120 s physics
+    step, the midpoint bias; rounds 1-4's default) instead of the reference's TGS."""
+    kw.setdefault("solver_type", 0)
+    kw.setdefault("solver_iterations", 8)
+    return default_sim_params(**kw)
 
 
 def imitation_params(reward=None, control_dt=1.0 / 30.0, use_power_reward=True, power_coef=0.0005,

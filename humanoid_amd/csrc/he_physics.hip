@@ -38,6 +38,7 @@ constexpr int MAXR = HE_MAX_ROWS;      // solver rows, one per lane (patch frict
 constexpr int W = 64;
 static_assert(MAXR <= W - 1, "solver rows must fit one per lane");
 constexpr int kTgsMaxIt = 16;  // TGS position iterations per physics step (he_simulate checks; oracle TGS_MAXIT)
+constexpr int kTgsBiasEvery = 2;  // TGS: the bias re-evaluated every second iteration (oracle g_bias_every)
 static_assert(MAXC < W, "one slot per lane in the row-layout pass");
 static_assert(smpl::kNG == NG && smpl::kNB == NB, "generated topology mismatch");
 
@@ -390,6 +391,40 @@ HE_DEV float reduce_scatter(float (&v)[N]) {
     }
     return v[0];
 }
+// Zh^T x into lane = dof (lane i: sum over rows r of z_r[i] x_r; lanes < 11 also dof 64 + lane in e2): the
+// same butterfly as reduce_scatter with the products formed as the first stage consumes them, so at
+// most 32 + 8 of them are live at once (the TGS iterations run it beside the rows' Zh and columns)
+HE_DEV void reduce_scatter_z(const regla::ZVec& z, float x, int lane, float& e1, float& e2) {
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        float a = ZV(z, j) * x, b = ZV(z, j + 32) * x;
+        swap32(a, b);
+        v[j] = a + b;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { swap16(v[j], v[j + 16]); v[j] += v[j + 16]; }
+    rs_dpp<8, 0x140, 0xFF00FF00FF00FF00ull>(v);
+    rs_dpp<4, 0x141, 0xF0F0F0F0F0F0F0F0ull>(v);
+    rs_dpp<2, 0x4E, 0xCCCCCCCCCCCCCCCCull>(v);
+    rs_dpp<1, 0xB1, 0xAAAAAAAAAAAAAAAAull>(v);
+    e1 = v[0];
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        float a = 64 + j < NG ? ZV(z, 64 + j < NG ? 64 + j : 0) * x : 0.f;
+        float b = 72 + j < NG ? ZV(z, 72 + j < NG ? 72 + j : 0) * x : 0.f;
+        swap32(a, b);
+        w[j] = a + b;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { swap16(w[j], w[j + 4]); w[j] += w[j + 4]; }
+    rs_dpp<2, 0x140, 0xFF00FF00FF00FF00ull>(w);
+    rs_dpp<1, 0x141, 0xF0F0F0F0F0F0F0F0ull>(w);
+    w[0] += dpp<0x4E>(w[0]);
+    w[0] += dpp<0xB1>(w[0]);
+    e2 = __shfl(w[0], 4 * (lane & 15), W);
+}
 // at most 32 rows (<= 10 contacts): only the rows-0-31 x columns-0-31 tile is needed (one MFMA per
 // dof pair instead of four); rows >= 32 of acol are never read then
 HE_DEV void delassus_mfma32(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
@@ -498,8 +533,8 @@ HE_DEV void delassus_mfma(const regla::ZVec& z, float (&acol)[MAXR], uint32_t li
 // One Gauss-Seidel sweep, branch-free: every row up to a compile-time class bound N (16, 32, 48,
 // 63) by the row count, with no per-row row-count branch (a row-count exit every 4 rows); rows nr..N-1 are empty rows (zero columns and
 // bound weights in every lane, zero cd and bounds in their own lanes: a +-0 change).
-template <int R, int N>
-HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[MAXR], int nr) {
+template <int R, int N, int M = MAXR>
+HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f2v (&ak)[M], int nr) {
     if constexpr (R < N) {
         if constexpr (R > 0 && R % 4 == 0) {  // a row-count exit every 4 rows
             if (R >= nr) return;
@@ -508,7 +543,7 @@ HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f
         ch = __builtin_elementwise_fma(ak[R], regla::f2v{d, d}, ch);
         lo = fmaf(-ak[R].y, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
-        pgs_sweep_fix<R + 1, N>(ch, dvec, lo, ak, nr);
+        pgs_sweep_fix<R + 1, N, M>(ch, dvec, lo, ak, nr);
     }
 }
 
@@ -516,20 +551,24 @@ HE_DEV void pgs_sweep_fix(regla::f2v& ch, float& dvec, float& lo, const regla::f
 // patch mask (2 VALU off the dependent chain) instead of a second register per row: the scaled
 // columns, the rows' Zh and the sweep state stay in registers through the position iterations'
 // triangular solves, bias passes and integrations
-template <int R, int N>
-HE_DEV void pgs_sweep_tgs(regla::f2v& ch, float& dvec, float& lo, const float (&ap)[MAXR], uint32_t mlo, uint32_t mhi,
+template <int R, int N, int M>
+HE_DEV void pgs_sweep_tgs(regla::f2v& ch, float& dvec, float& lo, const float (&ap)[M], uint32_t mlo, uint32_t mhi,
                           float muw, int nr) {
+    static_assert(N <= M, "the sweep's rows within the columns held");
     if constexpr (R < N) {
         if constexpr (R > 0 && R % 4 == 0) {  // a row-count exit every 4 rows
             if (R >= nr) return;
         }
         const float d = regla::rdlane(__builtin_amdgcn_fmed3f(ch.x, lo, ch.y), R);
         const int sel = __builtin_amdgcn_sbfe((int)(R < 32 ? mlo : mhi), R & 31, 1);
-        const regla::f2v a = {ap[R], __int_as_float(sel & __float_as_int(muw))};
-        ch = __builtin_elementwise_fma(a, regla::f2v{d, d}, ch);
-        lo = fmaf(-a.y, d, lo);
+        const float wr = __int_as_float(sel & __float_as_int(muw));
+        // scalar FMAs: a packed pair built from ap[R] makes the compiler load ap as overlapping
+        // two-float vectors, which keeps the whole column array in scratch
+        ch.x = fmaf(ap[R], d, ch.x);
+        ch.y = fmaf(wr, d, ch.y);
+        lo = fmaf(-wr, d, lo);
         dvec = regla::wrlane<R>(d, dvec);
-        pgs_sweep_tgs<R + 1, N>(ch, dvec, lo, ap, mlo, mhi, muw, nr);
+        pgs_sweep_tgs<R + 1, N, M>(ch, dvec, lo, ap, mlo, mhi, muw, nr);
     }
 }
 
@@ -1127,11 +1166,30 @@ HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_para
 // for dof lane and dof 64 + lane (lanes < NH).
 HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, const float* vel, float& c1,
                         float& c2) {
+    // in short phases through LDS (the body velocities V and joint velocities vj in the V / F words, dead
+    // from the row set-up to the next kinematics), so that each phase's temporaries fit beside the
+    // iterations' long-lived rows and columns
     const bool bl = lane < NB;
     const int b = bl ? lane : 0;
-    float Fb[6];
-    {
-        const uint32_t jp = bl ? T.jump4[b] : 0xFFFFFFFFu;
+    const uint32_t jp = bl ? T.jump4[b] : 0xFFFFFFFFu;
+    auto prefix6 = [&](float (&y)[6]) {
+        auto round = [&](auto kc) {
+            constexpr int K = decltype(kc)::value;
+            const int j = jump_of<K>(jp);
+            const int src = j < 0 ? lane : j;
+            float ya[6];
+#pragma unroll
+            for (int x = 0; x < 6; ++x) ya[x] = __shfl(y[x], src, W);
+            if (j >= 0)
+#pragma unroll
+                for (int x = 0; x < 6; ++x) y[x] += ya[x];
+        };
+        round(std::integral_constant<int, 0>{});
+        round(std::integral_constant<int, 1>{});
+        round(std::integral_constant<int, 2>{});
+        if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
+    };
+    {  // joint velocities vj = S_b u_b and body velocities V = prefix of vj (+ the root's)
         float vj[6];
         if (b == 0) {
             for (int x = 0; x < 6; ++x) vj[x] = vel[x];
@@ -1140,50 +1198,45 @@ HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params
             const float u0_ = vel[d0], u1_ = vel[d0 + 1], u2_ = vel[d0 + 2];
             for (int x = 0; x < 6; ++x) vj[x] = L.S[d0][x] * u0_ + L.S[d0 + 1][x] * u1_ + L.S[d0 + 2][x] * u2_;
         }
+        if (bl)
+            for (int x = 0; x < 6; ++x) L.F[b][x] = vj[x];
         float V[6];
         for (int x = 0; x < 6; ++x) V[x] = vj[x];
-        auto prefix6 = [&](float (&y)[6]) {
-            auto round = [&](auto kc) {
-                constexpr int K = decltype(kc)::value;
-                const int j = jump_of<K>(jp);
-                const int src = j < 0 ? lane : j;
-                float ya[6];
-#pragma unroll
-                for (int x = 0; x < 6; ++x) ya[x] = __shfl(y[x], src, W);
-                if (j >= 0)
-#pragma unroll
-                    for (int x = 0; x < 6; ++x) y[x] += ya[x];
-            };
-            round(std::integral_constant<int, 0>{});
-            round(std::integral_constant<int, 1>{});
-            round(std::integral_constant<int, 2>{});
-            if constexpr (kKinRounds == 4) round(std::integral_constant<int, 3>{});
-        };
         prefix6(V);
-        const float v6[6] = {vel[0], vel[1], vel[2], vel[3], vel[4], vel[5]};
         if (b != 0)
-            for (int x = 0; x < 6; ++x) V[x] += v6[x];
-        const f3 vxw = cross3(f3{v6[3], v6[4], v6[5]}, f3{v6[0], v6[1], v6[2]});
-        const float A0[6] = {0.f, 0.f, 0.f, vxw.x - p.gravity[0], vxw.y - p.gravity[1], vxw.z - p.gravity[2]};
-        float A[6];
-        if (b == 0) {
-            for (int x = 0; x < 6; ++x) A[x] = A0[x];
-        } else {
-            crm(V, vj, A);
-        }
-        prefix6(A);
-        if (b != 0)
-            for (int x = 0; x < 6; ++x) A[x] += A0[x];
-        float IA[6], IV[6], X[6];
-        si_apply(L.Ib[b], A, IA);
-        si_apply(L.Ib[b], V, IV);
-        crf(V, IV, X);
-        for (int x = 0; x < 6; ++x) Fb[x] = IA[x] + X[x];
+            for (int x = 0; x < 6; ++x) V[x] += vel[x];
+        if (bl)
+            for (int x = 0; x < 6; ++x) L.V[b][x] = V[x];
     }
     sync();
-    if (bl)
-        for (int x = 0; x < 6; ++x) L.Acc[b][x] = Fb[x];
+    __builtin_amdgcn_sched_barrier(0);
+    {  // bias accelerations A = prefix of V x vj (+ the base's), then the body forces
+        float A[6];
+        {
+            const f3 vxw = cross3(f3{vel[3], vel[4], vel[5]}, f3{vel[0], vel[1], vel[2]});
+            if (b == 0) {
+                A[0] = 0.f; A[1] = 0.f; A[2] = 0.f;
+                A[3] = vxw.x - p.gravity[0]; A[4] = vxw.y - p.gravity[1]; A[5] = vxw.z - p.gravity[2];
+            } else {
+                crm(L.V[b], L.F[b], A);  // joint b's velocity-product term V_b x S_b u_b
+            }
+        }
+        prefix6(A);
+        if (b != 0) {
+            const f3 vxw = cross3(f3{vel[3], vel[4], vel[5]}, f3{vel[0], vel[1], vel[2]});
+            A[3] += vxw.x - p.gravity[0]; A[4] += vxw.y - p.gravity[1]; A[5] += vxw.z - p.gravity[2];
+        }
+        float IA[6], IV[6], X[6], Vb[6];
+        for (int x = 0; x < 6; ++x) Vb[x] = L.V[b][x];
+        si_apply(L.Ib[b], A, IA);
+        si_apply(L.Ib[b], Vb, IV);
+        crf(Vb, IV, X);
+        sync();
+        if (bl)
+            for (int x = 0; x < 6; ++x) L.Acc[b][x] = IA[x] + X[x];
+    }
     sync();
+    __builtin_amdgcn_sched_barrier(0);
     subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.Acc[0][0], nullptr, lane);
     c1 = dot6(L.S[lane], L.Acc[dof_body(lane)]);
     c2 = lane < regla::NH ? dot6(L.S[64 + lane], L.Acc[(64 + lane - 6) / 3 + 1]) : 0.f;
@@ -1216,10 +1269,8 @@ HE_DEV void tgs_velocity(Lds& L, const BodyTopo& T, int lane, float e1, float e2
     using regla::NH;
     float yl = (e1 + L.yh[lane]) * L.sDinv[lane];
     float y2 = lane < NH ? (e2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
-    float r1[regla::kRowRegs], r2[regla::kRowRegs];
-    load_rows(L, T, lane, r1, r2);
     __builtin_amdgcn_s_setprio(kPrioSerial);
-    solve_L(r1, r2, lane, yl, y2);
+    regla::solve_L_streamed(L.Lp + T.pack_start[lane], L.Lp + T.pack_start[lane < NH ? 64 + lane : 0], yl, y2);
     __builtin_amdgcn_s_setprio(kPrioDefault);
     L.u0[lane] += yl;
     if (lane < NH) L.u0[64 + lane] += y2;
@@ -1465,7 +1516,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         kp *= sc;
         kd *= sc;
         if (jd) L.dforce[d] = TGS ? kp : tau;  // TGS: the scaled stiffness, for the iterations' drives
-        if constexpr (TGS) L.uf[i] = bias;       // TGS: the bias at u0 (bias_midpoint 0 keeps it)
+        if constexpr (TGS) L.uf[i] = bias;       // TGS: the bias at u0, until an iteration re-evaluates it
         L.rhs[i] = hs * (jd ? tau - bias : -bias);
         L.coef[i] = jd ? hs * kp + kd : 0.f;
     };
@@ -1979,18 +2030,28 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     // TGS: what follows a position iteration's velocity update: its drive torques, the positions by hs
     // (the last iteration: the step's output velocity), then (not the last) the next iteration's bias
     // and free motion
-    auto tgs_advance = [&](bool lastit) {
+    auto tgs_advance = [&](int it) {
+        const bool lastit = it + 1 == K;
         tgs_drive_acc(L, lane, tf1, tf2);
         integrate_bodies(L, T, lane, p, hs, damp, L.u0, lastit, lastit && !last);
+        __builtin_amdgcn_sched_barrier(0);
+        STAMP(12);
         if (!lastit) {
-            float c1, c2;
-            if (p.bias_midpoint) {
-                tgs_bias_at(L, T, lane, p, L.u0, c1, c2);
-            } else {
-                c1 = L.uf[lane];
-                c2 = lane < NH ? L.uf[64 + lane] : 0.f;
+            // the velocity-dependent bias: re-evaluated at the start of every second iteration (oracle
+            // g_bias_every: as stable as every iteration at half the passes), else the one in L.uf
+            if (p.bias_midpoint && ((it + 1) % kTgsBiasEvery) == 0) {
+                float b1, b2;
+                tgs_bias_at(L, T, lane, p, L.u0, b1, b2);
+                L.uf[lane] = b1;
+                if (lane < NH) L.uf[64 + lane] = b2;
             }
+            const float c1 = L.uf[lane];
+            const float c2 = lane < NH ? L.uf[64 + lane] : 0.f;
+            __builtin_amdgcn_sched_barrier(0);
+            STAMP(29);
             tgs_rhs(L, T, lane, hs, c1, c2);
+            __builtin_amdgcn_sched_barrier(0);
+            STAMP(30);
         }
     };
     // TGS: the reported drive force, the iterations' mean (the joint-limit force is added by the caller)
@@ -2084,42 +2145,41 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const float invd = 1.0f / (act ? diag + 1e-12f : 1.f);
             const float ninvd = -invd;
             const int nrb = __builtin_amdgcn_readfirstlane(nr);
-            float ap[MAXR];  // -A[r][lane] / A[lane][lane], the row-count class's rows
-            {
-                auto prep = [&](auto r0c) {
-                    constexpr int R0 = decltype(r0c)::value;
+            // the first iteration starts from the cached (previous step's) impulses' per-iteration share g0;
+            // its residual w = brow + A g0 (lane c of acol holds A[r][c] = A[c][r])
+            const float g0 = lam0 * (1.0f / (float)K);
+            float w0 = brow;
+            if (__ballot(g0 != 0.f)) {  // wave-uniform; rows >= nr hold no impulse
+                auto aw = [&](auto nrows) {
+                    constexpr int NRW = decltype(nrows)::value;
+                    float wa[4] = {0.f, 0.f, 0.f, 0.f};
+                    regla::static_for<0, NRW, 4>([&](auto rc) {
+                        constexpr int r0 = decltype(rc)::value;
+                        float sv[4];
+                        regla::rdlane4<r0>(g0, sv);
 #pragma unroll
-                    for (int r = R0; r < (R0 + 16 < MAXR ? R0 + 16 : MAXR); ++r) ap[r] = acol[r] * ninvd;
+                        for (int q = 0; q < 4; ++q)
+                            if (r0 + q < NRW) wa[(r0 + q) & 3] = fmaf(acol[r0 + q < NRW ? r0 + q : 0], sv[q], wa[(r0 + q) & 3]);
+                    });
+                    w0 += (wa[0] + wa[1]) + (wa[2] + wa[3]);
                 };
-                prep(std::integral_constant<int, 0>{});
-                if (nrb > 16) prep(std::integral_constant<int, 16>{});
-                if (nrb > 32) prep(std::integral_constant<int, 32>{});
-                if (nrb > 48) prep(std::integral_constant<int, 48>{});
+                if (nrb <= 16) aw(std::integral_constant<int, 16>{});
+                else if (nrb <= 32) aw(std::integral_constant<int, 32>{});
+                else if (nrb <= 48) aw(std::integral_constant<int, 48>{});
+                else aw(std::integral_constant<int, MAXR>{});
             }
-            // sum_R ap[R] x_R (x_R from lane R, four lanes per block of SGPRs)
-            auto aprod = [&](float x) {
-                float acc = 0.f;
-                if (__ballot(x != 0.f)) {  // wave-uniform; rows >= nr hold nothing
-                    auto aw = [&](auto nrows) {
-                        constexpr int NRW = decltype(nrows)::value;
-                        float wa[4] = {0.f, 0.f, 0.f, 0.f};
-                        regla::static_for<0, NRW, 4>([&](auto rc) {
-                            constexpr int r0 = decltype(rc)::value;
-                            float sv[4];
-                            regla::rdlane4<r0>(x, sv);
-#pragma unroll
-                            for (int q = 0; q < 4; ++q)
-                                if (r0 + q < NRW) wa[(r0 + q) & 3] = fmaf(ap[r0 + q < NRW ? r0 + q : 0], sv[q], wa[(r0 + q) & 3]);
-                        });
-                        acc = (wa[0] + wa[1]) + (wa[2] + wa[3]);
-                    };
-                    if (nrb <= 16) aw(std::integral_constant<int, 16>{});
-                    else if (nrb <= 32) aw(std::integral_constant<int, 32>{});
-                    else if (nrb <= 48) aw(std::integral_constant<int, 48>{});
-                    else aw(std::integral_constant<int, MAXR>{});
-                }
-                return acc;
-            };
+            float dl = 0.f;
+            // the iterations, for one row-count class of columns held in registers (<= 32 rows: a
+            // standing body's 28; more: the 63-row form), so that the common case keeps 31 registers free
+            // for the phases between the sweeps
+            auto tgs_solve = [&](auto ncls) {
+            constexpr int NC = decltype(ncls)::value;
+            // the sweep's columns -A[r][lane] / A[lane][lane] of the class's rows; up to 32 rows packed
+            // with their bound weights as the PGS sweep's (pgs_sweep_fix), past 32 the weights rebuilt
+            // per row (pgs_sweep_tgs: 63 registers fewer)
+            constexpr bool PACK = NC <= 32;
+            float ap[PACK ? 1 : NC];
+            regla::f2v ak[PACK ? NC : 1];
             const bool isn = kind == 0;
             const float muw = L.lam[lane];  // the friction bound weight parked by the row set-up
             uint32_t mlo = 0u, mhi = 0u;
@@ -2130,6 +2190,26 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 mhi = (uint32_t)(pm >> 32);
             }
             const int n0 = act && !isn ? (int)__builtin_ctzll(((uint64_t)mhi << 32) | mlo) : 0;
+            {
+                auto prep = [&](auto r0c) {
+                    constexpr int R0 = decltype(r0c)::value;
+#pragma unroll
+                    for (int r = R0; r < (R0 + 16 < NC ? R0 + 16 : NC); ++r) {
+                        if constexpr (PACK) {
+                            const int sel = __builtin_amdgcn_sbfe((int)(r < 32 ? mlo : mhi), r & 31, 1);
+                            ak[r] = regla::f2v{acol[r] * ninvd, __int_as_float(sel & __float_as_int(muw))};
+                        } else {
+                            ap[r] = acol[r] * ninvd;
+                        }
+                    }
+                };
+                prep(std::integral_constant<int, 0>{});
+                if (nrb > 16) prep(std::integral_constant<int, 16>{});
+                if constexpr (NC > 32) {
+                    if (nrb > 32) prep(std::integral_constant<int, 32>{});
+                    if (nrb > 48) prep(std::integral_constant<int, 48>{});
+                }
+            }
             auto patch_bound = [&](float lv) {  // muw x the patch's normal impulses (<= 4 rows)
                 float bnd = 0.f;
 #pragma unroll
@@ -2148,12 +2228,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             float sep = act && isn ? L.cgap[rs_] : 0.f;  // the row's separation (a limit row: its angle gap)
             float bb = act && isn ? gbias(sep) : 0.f;   // its bias (brow holds it)
             float applied = 0.f;                         // the impulse already in the working velocity
-            lamv = lam0;
-            float cd = act ? -brow * invd + aprod(lam0) : 0.f;
+            lamv = g0;
+            float cd = act ? -w0 * invd : 0.f;
             float bnd = patch_bound(lamv);
             float lo = isn ? -lamv : -bnd - lamv;
             float hi = isn ? kInf : bnd - lamv;
-            float dl = 0.f;
             const int nru = __builtin_amdgcn_readfirstlane(nr);
             for (int it = 0; it < K; ++it) {
                 float dvec = 0.f;
@@ -2161,32 +2240,36 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 asm volatile("" : "+s"(nrs));
                 regla::f2v ch = {cd, hi};
                 __builtin_amdgcn_s_setprio(kPrioSerial);
-                if (nrs <= 16) pgs_sweep_tgs<0, 16>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
-                else if (nrs <= 32) pgs_sweep_tgs<0, 32>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
-                else if (nrs <= 48) pgs_sweep_tgs<0, 48>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
-                else pgs_sweep_tgs<0, MAXR>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                if constexpr (PACK) {
+                    if (nrs <= 16) pgs_sweep_fix<0, 16, NC>(ch, dvec, lo, ak, nrs);
+                    else pgs_sweep_fix<0, 32, NC>(ch, dvec, lo, ak, nrs);
+                } else {
+                    if (nrs <= 48) pgs_sweep_tgs<0, 48, NC>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                    else pgs_sweep_tgs<0, MAXR, NC>(ch, dvec, lo, ap, mlo, mhi, muw, nrs);
+                }
                 __builtin_amdgcn_s_setprio(kPrioDefault);
+                STAMP(10);
                 cd = ch.x;
                 lamv += dvec;
                 dl = act ? lamv - applied : 0.f;  // this iteration's impulse change
                 applied = lamv;
                 const float v = act ? -cd * (diag + 1e-12f) - bb : 0.f;  // J_r u after the sweep
-                {  // the working velocity: u += L^-1 D^-1/2 (yh + Zh^T dl)
-                    float v64[64], v16[16];
-#pragma unroll
-                    for (int i = 0; i < 64; ++i) v64[i] = ZV(z, i) * dl;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) v16[i] = 64 + i < NG ? ZV(z, 64 + i < NG ? 64 + i : 0) * dl : 0.f;
-                    const float e1 = reduce_scatter<64>(v64);
-                    const float e2 = __shfl(reduce_scatter<16>(v16), 4 * (lane & 15), W);
-                    tgs_velocity(L, T, lane, e1, lane < NH ? e2 : 0.f);
-                }
+                float e1, e2;  // Zh^T dl, lane = dof (and 64 + lane): also the next start's A dl = Zh (Zh^T dl)
+                __builtin_amdgcn_sched_barrier(0);  // phase fences: each phase's temporaries beside the
+                reduce_scatter_z(z, dl, lane, e1, e2);  // loop's long-lived rows and columns, not several
+                __builtin_amdgcn_sched_barrier(0);
+                e2 = lane < NH ? e2 : 0.f;
+                tgs_velocity(L, T, lane, e1, e2);  // the working velocity: u += L^-1 D^-1/2 (yh + Zh^T dl)
+                __builtin_amdgcn_sched_barrier(0);
+                STAMP(11);
                 if (isn) sep += hs * v;
                 const bool lastit = it + 1 == K;
-                tgs_advance(lastit);
+                tgs_advance(it);
+                __builtin_amdgcn_sched_barrier(0);
                 if (!lastit) {
-                    // the next sweep's start: w = J u + zh . yh + bias(sep) + A dl about lambda = applied + dl
-                    const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
+                    // the next sweep's start about lambda = applied + dl: w = J u + zh . yh + bias(sep) + A dl,
+                    // with zh . yh + A dl = zh . (yh + Zh^T dl), one dot product
+                    const float yhl = L.yh[lane] + e1, yh2 = lane < NH ? L.yh[64 + lane] + e2 : 0.f;
                     float yacc[4] = {0.f, 0.f, 0.f, 0.f};
                     regla::static_for<0, NG, 4>([&](auto ic) {
                         constexpr int i0 = decltype(ic)::value;
@@ -2200,15 +2283,18 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     const float zy = (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
                     bb = act && isn ? gbias(sep) : 0.f;
                     lamv = applied + dl;
-                    cd = act ? -(v + zy + bb) * invd + aprod(dl) : 0.f;
+                    cd = act ? -(v + zy + bb) * invd : 0.f;
                     bnd = patch_bound(lamv);
                     lo = isn ? -lamv : -bnd - lamv;
                     hi = isn ? kInf : bnd - lamv;
+                    STAMP(31);
                 }
             }
-            // the cache keeps the last iteration's change (the next step's first start); the reported
-            // forces take the accumulated impulses
-            L.lam[lane] = act ? dl : 0.f;
+            };
+            if (nrb <= 32) tgs_solve(std::integral_constant<int, 32>{});
+            else tgs_solve(std::integral_constant<int, MAXR>{});
+            // the cache and the reported forces take the step's accumulated impulses
+            L.lam[lane] = act ? lamv : 0.f;
             if (lane == 0) L.nwc = p.warm_start ? nr : 0;
             tgs_drive_out();
             // the joint-limit force (dof_force = drive and limit together): limit row c = slot c
@@ -2396,7 +2482,8 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     if (TGS && nr == 0) {  // TGS without contact rows: the iterations' drives and bias only
         for (int it = 0; it < K; ++it) {
             tgs_velocity(L, T, lane, 0.f, 0.f);
-            tgs_advance(it + 1 == K);
+            STAMP(11);
+            tgs_advance(it);
         }
         tgs_drive_out();
     }

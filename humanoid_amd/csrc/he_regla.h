@@ -276,6 +276,42 @@ __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const 
     }
 }
 
+// the same sweep with the packed rows streamed from LDS four levels at a time, one 16-byte block a
+// level-group ahead (16 registers instead of solve_L_rows' 64 preloaded): for phases where the rows
+// compete with long-lived state for registers (the TGS iterations' velocity updates). p1 / p2: the
+// lane's rows of dof lane and dof 64 + lane (16-byte aligned, as load_rows); only entries below the
+// dof's depth are used, as in solve_L_rows.
+template <int D>
+__device__ __forceinline__ void solve_L_stream(const f4v* p1, const f4v* p2, f4v c1, f4v c2, f4v n1, f4v n2, float& yl,
+                                               float& y2) {
+    if constexpr (D < kNumLevels - 1) {
+        if constexpr (D > 0 && D % 4 == 0) {
+            c1 = n1;
+            c2 = n2;
+            if constexpr (D / 4 + 1 < kRowRegs / 4) {
+                int off = 0;
+                asm volatile("" : "+v"(off));  // the next block's loads stay here, a group ahead
+                n1 = *reinterpret_cast<const f4v*>(reinterpret_cast<const char*>(p1 + D / 4 + 1) + off);
+                n2 = *reinterpret_cast<const f4v*>(reinterpret_cast<const char*>(p2 + D / 4 + 1) + off);
+            }
+        }
+        constexpr uint64_t ulo = level_desc_lo<D>();
+        constexpr uint64_t uhi = level_desc_hi<D>();
+        if constexpr (ulo != 0 || uhi != 0) {
+            float t1 = 0.f, t2 = 0.f;
+            level_pick<D, kLevelStart[D]>(yl, y2, t1, t2);
+            if constexpr (ulo != 0) yl = lanes<ulo>() ? yl - c1[D % 4] * t1 : yl;
+            if constexpr (uhi != 0) y2 = lanes<uhi>() ? y2 - c2[D % 4] * t2 : y2;
+        }
+        solve_L_stream<D + 1>(p1, p2, c1, c2, n1, n2, yl, y2);
+    }
+}
+__device__ __forceinline__ void solve_L_streamed(const float* row1, const float* row2, float& yl, float& y2) {
+    const f4v* p1 = reinterpret_cast<const f4v*>(row1);
+    const f4v* p2 = reinterpret_cast<const f4v*>(row2);
+    solve_L_stream<0>(p1, p2, p1[0], p2[0], p1[1], p2[1], yl, y2);
+}
+
 // ---------------------------------------------------------------- y <- L^-T y, one vector
 // Lane j holds y_j (and y_{64+j} in y2). The elimination's forward substitution replayed from the
 // stored factor: pivots in kElimOrder (deepest first, so every descendant of K is final before K

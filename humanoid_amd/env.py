@@ -110,7 +110,11 @@ class EnvConfig:  # config.py:89-157
     # engine extensions (not in the reference config)
     seed: int = 0
     max_contacts: int = 40
-    solver_iterations: int = 8  # PGS sweeps per physics step
+    # the physics solver (isaacgym_env.py:16-18 sets PhysX TGS, 4 position iterations): solver_type 1
+    # TGS with solver_iterations position iterations per physics step; 0 the engine's PGS step
+    # (solver_iterations velocity-level sweeps, 8 recommended)
+    solver_type: int = 1
+    solver_iterations: int = 4
 
     @property
     def device(self) -> str:
@@ -164,7 +168,7 @@ class HumanoidPHC:
         self.num_obs, self.num_actions = NUM_OBS, NUM_ACTIONS
         sim = _abi.default_sim_params(self_collision=int(cfg.robot.has_self_collision), kp_scale=cfg.kp_scale,
                                       kd_scale=cfg.kd_scale, max_contacts=cfg.max_contacts,
-                                      solver_iterations=cfg.solver_iterations)
+                                      solver_type=cfg.solver_type, solver_iterations=cfg.solver_iterations)
         # start pose z=0.89 + U(-1,1) xy jitter (humanoid_phc.py:340-347)
         rng = np.random.default_rng(cfg.seed)
         self.engine = Engine(self.model, n, device=self.device.index or 0, sim_params=sim,

@@ -1243,11 +1243,20 @@ static void substep(const he_model* m, const topo* t, const he_sim_params* p, en
  *     velocity (the solver's velocity itself is not clamped; the last iteration's clamped one is the
  *     step's output);
  *   - the rows' impulses accumulate over the iterations (the step's total: the bounds and the reported
- *     forces); each iteration's sweep starts from the previous iteration's change (the first: the
- *     previous step's last change, the warm-start cache), as a small-step solver warm-starts each
- *     sub-step from the last; the drive force is the iterations' mean.
+ *     forces, and the warm-start cache, as PGS's); each iteration's sweep starts from the accumulated
+ *     impulses plus the previous iteration's change (the first: the previous step's total / K, its
+ *     per-iteration share), as a small-step solver warm-starts each sub-step from the last; the drive
+ *     force is the iterations' mean.
  * The velocity-dependent bias is taken at u0 for the whole step (bias_midpoint 0) or re-evaluated at
- * each iteration's start velocity with the step's kinematics (bias_midpoint 1). */
+ * the start velocity of every second iteration with the step's kinematics (bias_midpoint 1,
+ * g_bias_every above). */
+/* TGS: the velocity-dependent bias is re-evaluated every g_bias_every-th position iteration (2: at
+ * iterations 2, 4, ... with the step's start bias before): as stable under saturated random actions
+ * as every iteration (airborne internal KE 759 against 768 J, the standing U(+-1) tail 7.9 m/s) and
+ * with half the free-flight angular-momentum drift, at half the RNEA passes; every 4th (frozen over
+ * the step) pumps energy (3.6 kJ). Study switch: ho_set_bias_every (tests/diag/tgs_study.py). */
+static int g_bias_every = 2;
+void ho_set_bias_every(int k) { g_bias_every = k < 1 ? 1 : k; }
 static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p, env_state* s, const R* mass_scale,
                         R mu, int terrain_kind, step_out* out, warm_cache* ws) {
     static __thread kin k;
@@ -1332,7 +1341,7 @@ static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p
         for (int r = 0; r < nr; ++r)
             for (int j = 0; j < ws->n; ++j)
                 if (ws->key[j] == rows[r].key) {
-                    guess[r] = ws->lam[j];
+                    guess[r] = ws->lam[j] / K; /* the cache holds the previous step's total */
                     break;
                 }
 #define TGS_BOUND(r) ({ R b_ = 0; for (int k_ = 0; k_ < rows[r].cnt; ++k_) b_ += lam[rows[r].n0 + k_]; rows[r].muw * b_; })
@@ -1345,7 +1354,7 @@ static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p
     R bias_it[NG];
     memcpy(bias_it, bias, sizeof(bias_it));
     for (int it = 0; it < K; ++it) {
-        if (it > 0 && p->bias_midpoint) { /* the velocity-dependent bias at this iteration's velocity */
+        if (it > 0 && p->bias_midpoint && (it % g_bias_every) == 0) { /* the velocity-dependent bias at this iteration's velocity */
             env_state sv = *s;
             for (int c = 0; c < 3; ++c) { sv.root_w[c] = u[c]; sv.root_v[c] = u[3 + c]; }
             for (int d = 0; d < ND; ++d) sv.u[d] = u[6 + d];
@@ -1444,11 +1453,11 @@ static void substep_tgs(const he_model* m, const topo* t, const he_sim_params* p
         }
     }
 #undef TGS_BOUND
-    if (ws) { /* the last iteration's changes: the next step's first guess */
+    if (ws) { /* the step's accumulated impulses: the next step's first guess is their per-iteration share */
         ws->n = nr;
         for (int r = 0; r < nr; ++r) {
             ws->key[r] = rows[r].key;
-            ws->lam[r] = guess[r];
+            ws->lam[r] = lam[r];
         }
     }
     for (int d = 0; d < ND; ++d) out->dof_force[d] = dfor[d] / K + lim_tau[d];

@@ -51,7 +51,9 @@ def test_gpu_free_fall_is_the_discrete_parabola(he_model):
         eng.simulate(2)
     torch.cuda.synchronize()
     r = eng.root_states.cpu().numpy()
-    sub = eng.params.substeps  # physics steps of dt / substeps per simulate() (SimParams.substeps)
+    # semi-implicit sub-steps of h per simulate(): SimParams.substeps physics steps, each (TGS) of
+    # solver_iterations position iterations
+    sub = eng.params.substeps * (eng.params.solver_iterations if eng.params.solver_type == 1 else 1)
     k = 2 * steps * sub
     dt = 1.0 / 60.0 / sub
     assert (eng.num_contacts.cpu().numpy() == 0).all()

@@ -112,7 +112,7 @@ def test_warm_start_converges_on_lying_bodies(he_model):
     targets = np.zeros((n, 69), np.float32)
     res = {}
     for ws in (0, 1):
-        sp = _abi.default_sim_params(warm_start=ws)
+        sp = _abi.pgs_sim_params(warm_start=ws)
         r, d = root.copy(), dof.copy()
         cache = O.new_cache(n)
         rr = []
@@ -164,7 +164,7 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
     dof[:, 3 * j:3 * j + 3, 0] = (axis * (np.pi - 0.025)).astype(np.float32)
     dof[:, 3 * j:3 * j + 3, 1] = (axis * 60.0).astype(np.float32)
     # one physics step of 1/60 s (substeps 1): the backstop's own case
-    sp = _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0, warm_start=0,
+    sp = _abi.pgs_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0, warm_start=0,
                                  substeps=1)
     r, d = root.copy(), dof.copy()
     O.physics_step(he_model, sp, r, d, np.zeros((n, 69), np.float32), 1)
@@ -176,7 +176,7 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
     assert ((u * q).sum(1) / t <= 1e-6).all()  # no outward rate left
     # the other joints equal a run without limits (the backstop acts only past pi - 0.01)
     r2, d2 = root.copy(), dof.copy()
-    O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0,
+    O.physics_step(he_model, _abi.pgs_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, solver_iterations=0,
                                                      warm_start=0, joint_limits=0, substeps=1),
                    r2, d2, np.zeros((n, 69), np.float32), 1)
     others = [k for k in range(23) if k != j]
@@ -184,7 +184,7 @@ def test_limit_backstop_holds_a_joint_the_rows_cannot(he_model, model):
     np.testing.assert_array_equal(qs, d2[:, :, 0].reshape(n, 23, 3)[:, others])
     # with the sweeps, the limit row holds it first, at pi - 0.02
     r3, d3 = root.copy(), dof.copy()
-    O.physics_step(he_model, _abi.default_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, substeps=1), r3, d3,
+    O.physics_step(he_model, _abi.pgs_sim_params(self_collision=0, kp_scale=0.0, kd_scale=0.0, substeps=1), r3, d3,
                    np.zeros((n, 69), np.float32), 1)
     t3 = np.linalg.norm(d3[:, 3 * j:3 * j + 3, 0].astype(np.float64), axis=1)
     assert (t3 < np.pi - 0.015).all() and (t3 > np.pi - 0.03).all()
@@ -290,7 +290,7 @@ def test_row_budget_caps_the_solve_at_63_rows(he_model, model):
     rng = np.random.default_rng(5)
     n = 32
     root, dof = cases.lying_state(n, rng, on_floor=True, model=model)
-    sp = _abi.default_sim_params()
+    sp = _abi.pgs_sim_params()
     cache = O.new_cache(n)
     tgt = dof[..., 0].copy()
     for _ in range(40):

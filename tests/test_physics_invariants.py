@@ -15,6 +15,10 @@ step. These tests pin the oracle against physics itself instead (SURVEY §7 step
 * penetration: standing and lying bodies settle with every contact candidate within the
   Baumgarte steady state, far inside contact_offset (0.02 m).
 The GPU engine is then held to this oracle (tests/test_gpu_parity.py).
+
+These are the invariants of the PGS step (he_sim_params.solver_type 0, _abi.pgs_sim_params: 8
+velocity-level sweeps per physics step, the midpoint bias), rounds 1-4's default; the engine's default
+since round 5 is the reference's TGS (solver_type 1), whose invariants are tests/test_tgs.py.
 """
 import numpy as np
 import pytest
@@ -28,7 +32,7 @@ G = 9.81
 
 
 def _run(he_model, root, dof, targets, steps, substeps=2, **sim):
-    sp = _abi.default_sim_params(**sim)
+    sp = _abi.pgs_sim_params(**sim)
     r, d = root.copy(), dof.copy()
     cache = O.new_cache(r.shape[0])
     out = None
@@ -45,7 +49,7 @@ def _drives_off(**kw):
 
 
 def _com_velocity(model, he_model, root, dof):
-    me = O.momentum_energy(he_model, _abi.default_sim_params(), root, dof)
+    me = O.momentum_energy(he_model, _abi.pgs_sim_params(), root, dof)
     return me[:, :3] / float(np.sum(model.mass))
 
 
@@ -73,7 +77,7 @@ def _flight_drifts(model, he_model, root, dof, gravity, dt_div, seconds=1.0):
     sim = _drives_off(gravity=gravity, dt=1.0 / 60.0 / dt_div)
     steps = int(round(30 * seconds * dt_div))
     n = root.shape[0]
-    sp0 = _abi.default_sim_params(**sim)
+    sp0 = _abi.pgs_sim_params(**sim)
     me0 = O.momentum_energy(he_model, sp0, root, dof)
     r, d, out, sp = _run(he_model, root, dof, np.zeros((n, 69), np.float32), steps, **sim)
     assert (out["num_contacts"] == 0).all()
@@ -176,7 +180,7 @@ def test_pd_stand_still_equilibrium(he_model, model):
     n = 8
     root, dof = cases.standing_state(model, n, rng, xy_jitter=1.0)
     targets = np.zeros((n, 69), np.float32)
-    sp = _abi.default_sim_params()
+    sp = _abi.pgs_sim_params()
     r, d = root.copy(), dof.copy()
     cache = O.new_cache(n)
     ncs = []
@@ -224,7 +228,7 @@ def _random_action_run(he_model, model, amp, n, steps, airborne=False, seed=8, *
     if airborne:
         root[:, 2] += 200.0
         sim.setdefault("self_collision", 0)
-    sp = _abi.default_sim_params(**sim)
+    sp = _abi.pgs_sim_params(**sim)
     cache = O.new_cache(n)
     vmax = np.zeros(n)
     for _ in range(steps):
@@ -276,7 +280,7 @@ def test_sliding_body_decelerates_at_mu_g(he_model, model, mu):
     n = 8
     root, dof = cases.lying_state(n, rng, on_floor=True, model=model)
     tgt = dof[..., 0].copy()
-    sp = _abi.default_sim_params()
+    sp = _abi.pgs_sim_params()
     cache = O.new_cache(n)
     for _ in range(45):  # settle 1.5 s
         O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache)
@@ -316,12 +320,12 @@ def test_runaway_tail_is_a_wedged_limb_launched_off_the_ground(he_model, model):
     root, dof, cache = d["root"][i][None].copy(), d["dof"][i][None].copy(), d["cache"][i][None].copy()
     tg = d["targets"][i][None].copy()
     r2, d2, c2 = root.copy(), dof.copy(), cache.copy()
-    O.physics_step(he_model, _abi.default_sim_params(), r2, d2, tg, 2, cache=c2)
+    O.physics_step(he_model, _abi.pgs_sim_params(), r2, d2, tg, 2, cache=c2)
     v_engine = float(np.linalg.norm(d["root_after"][i][7:10]))
     assert v_engine > 15.0
     assert abs(float(np.linalg.norm(r2[0, 7:10])) - v_engine) < 0.01 * v_engine
     # one physics step at a time: the same arithmetic as 2 simulate() x 2 substeps
-    sp = _abi.default_sim_params(dt=1.0 / 120.0, substeps=1)
+    sp = _abi.pgs_sim_params(dt=1.0 / 120.0, substeps=1)
     names = lambda b: BODY_NAMES[b] if b >= 0 else {-1: "terrain", -2: "limit"}[b]  # noqa: E731
     com_v, rows = [], []
     for _ in range(4):
@@ -349,7 +353,7 @@ def test_runaway_tail_is_a_wedged_limb_launched_off_the_ground(he_model, model):
     lam_w, gap_w = rows[jump][("R_Wrist", "terrain")]
     assert lam_w > 500.0, rows[jump]
     # dt/4 from 6 steps before the peak: no launch
-    sp4 = _abi.default_sim_params(substeps=8)
+    sp4 = _abi.pgs_sim_params(substeps=8)
     r4, d4 = d["root"][0][None].copy(), d["dof"][0][None].copy()
     c4 = O.new_cache(1)
     vmax4 = 0.0

@@ -20,7 +20,8 @@ PHASES = ["kinematics", "inertia+rnea", "subtree sums", "bias/IS/drives", "crba"
           "contact: limit slots", "self: pair tests+slots", "terrain: rank+prefix", "terrain: slots",
           "terrain: geometry (to P0/P1)", "self: segment tests", "rows: J^T + bias", "rows: L^-T sweep",
           "pgs: set-up", "(unused)", "fused imitation",
-          "mid: um sweep", "mid: velocities + rnea", "mid: subtree + dc", "mid: L^-T"]  # slots 25-28: the midpoint bias; slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22 out of "pgs" (its set-up before the sweeps)
+          "mid: um sweep", "mid: velocities + rnea", "mid: subtree + dc", "mid: L^-T",
+          "tgs: bias rnea", "tgs: rhs L^-T", "tgs: next sweep set-up"]  # slots 25-28: the midpoint bias; slots 14-19 are carved out of "contact gen", 20-21 out of "Z rows", 22 out of "pgs" (its set-up before the sweeps); 29-31 the TGS iterations (TGS: "pgs" = the sweeps, "du solve" = the velocity updates, "integrate" = drive force + integration, per iteration)
 
 
 def main():
@@ -31,7 +32,7 @@ def main():
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--max-contacts", type=int, default=40)
     ap.add_argument("--fused", action="store_true")
-    ap.add_argument("--scheme", choices=["default", "r02"], default="default")
+    ap.add_argument("--scheme", choices=["default", "r02", "tgs", "tgs_small"], default="default")
     args = ap.parse_args()
     import numpy as np
     import torch

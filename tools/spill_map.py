@@ -4,7 +4,7 @@ launch bound: 256 / W VGPRs), disassembled and split at its s_memtime stamps as 
 tools/isa_phase_counts.py; per phase the scratch stores and loads the allocator inserted, and the
 kernel's resource report.
 
-  python tools/spill_map.py [W]      (default 4)
+  python tools/spill_map.py [W] [KERNEL]      (default 4, physics_kernel; physics_kernel_tgs: the TGS one)
 """
 import json
 import os
@@ -24,6 +24,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 def main():
     w = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    kname = sys.argv[2] if len(sys.argv) > 2 else "physics_kernel"
     src = os.path.join(B.CSRC, "he_physics.hip")
     flags = dict(B.SOURCES)["he_physics.hip"]
     with tempfile.TemporaryDirectory() as td:
@@ -37,7 +38,7 @@ def main():
     report = {}
     lines = r.stderr.splitlines()
     for i, ln in enumerate(lines):
-        if "Function Name:" in ln and "physics_kernel" in ln:
+        if "Function Name:" in ln and re.search(r"\d" + kname + r"E", ln):
             for ln2 in lines[i + 1:i + 14]:
                 if "Function Name:" in ln2:
                     break
@@ -45,6 +46,10 @@ def main():
                 if m:
                     report[m.group(1).strip()] = m.group(2)
     L = dis.split("\n")
+    # the kernel's own disassembly: from its label to the next function label
+    start = next(i for i, ln in enumerate(L) if re.search(r"\d" + kname + r"E\w*>:", ln))
+    end = next((i for i in range(start + 1, len(L)) if re.match(r"^[0-9a-f]+ <", L[i])), len(L))
+    L = L[start:end]
     cuts = [i for i, ln in enumerate(L) if "s_memtime" in ln]
     phases = {}
     for a, b in zip(cuts, cuts[1:]):
