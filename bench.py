@@ -666,7 +666,13 @@ def main():
                 "physics_kernel": phys_roof,
                 "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS,
                                      "unit": "GB/s", "frac": round(imit_gbs / HBM_PEAK_GBS, 5),
-                                     "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic}},
+                                     "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic,
+                                     # the bytes that reached HBM (PMC FETCH_SIZE + WRITE_SIZE per launch,
+                                     # profiles/pmc_traffic.json) over the same launch time: with one clip
+                                     # (configs[1]) most motion reads hit the caches, so this is well under
+                                     # the algorithmic figure above
+                                     "hbm_frac_counter": (round(imit_traffic / (imit_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                                          if imit_traffic else None)}},
         }
         if not args.no_tracking and world == 1 and args.scheme == "default":
             try:

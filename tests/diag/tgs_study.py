@@ -1,31 +1,30 @@
-"""How far is the shipped solver from a TGS-style step? (VERDICT r03 missing 2 / next 6.)
+"""How close are the engine's physics steps to PhysX's TGS?
 
 The reference runs PhysX TGS with 4 position iterations and 0 velocity iterations
-(isaacgym_env.py:16-18). TGS ("temporal Gauss-Seidel") sub-steps inside the solver: every position
-iteration integrates the bodies by dt/4 with the velocities of that iteration, and the next iteration
-solves against the separations that motion left. Its published basis is the small-step equivalence
-(one solver iteration per sub-step, with a fresh integration per sub-step, converges like many
-iterations of one large step). The engine's solver is velocity-level PGS with 8 warm-started sweeps
-per 1/120 s physics step.
+(isaacgym_env.py:16-18). Round 5 built it in-step (he_sim_params.solver_type 1, oracle substep_tgs,
+physics_kernel_tgs; the default since): each 1/120 s physics step keeps its factor and contact set and
+runs 4 position iterations of 1/480 s -- the drives implicit per iteration, one Gauss-Seidel sweep
+against separations advanced by the iterations' motion, the positions integrated per iteration.
 
-Every scheme below is the fp64 oracle (oracle/he_oracle_physics.c), from the same start state, fed
-the same PD targets, for 30 policy steps (2 simulate() calls each):
-  shipped       2 substeps of 1/120 s per simulate, 8 PGS sweeps (the engine default)
-  tgs_4x1       8 substeps of 1/480 s per simulate, 1 sweep each: TGS's 4 position iterations per
-                1/120 s physics step, each re-integrating dt/4, 0 velocity iterations (the contacts,
-                mass matrix and drives are also re-evaluated per sub-step: PhysX TGS keeps the
-                contact set of the step and moves the separations linearly)
-  tgs_4x2       as tgs_4x1 with 2 sweeps per sub-step
-  pgs_4         2 substeps of 1/120 s, 4 sweeps (PhysX's iteration count at the engine's step)
-  fine_8        8 substeps of 1/480 s, 8 sweeps: a converged small-step reference
-  shipped+1e-6  the shipped scheme from the start state with joint angles moved by 1e-6 rad: the
-                chaos floor (any scheme difference at or below it is invisible over 30 steps)
-Distances to `shipped` per env over the 30 steps: max joint-angle L2 (69 exp-map coordinates) and
-max CoM distance; reported as median / p90 / max over envs, and at step 1, 5, 10, 30.
-Cases (48 envs each): standing (PD stand-still, actions 0), tumbling (lying bodies thrown out of
-the plane, actions 0), tracking (configs[2]-style: synthetic clips, a = clip(ref_dof_pos / scale)).
+Every scheme is the fp64 oracle (oracle/he_oracle_physics.c), from the same start state, fed the same
+PD targets, for 30 policy steps (2 simulate() calls each):
+  tgs           the engine default: 2 substeps of 1/120 s, TGS in-step, 4 position iterations
+  pgs           rounds 1-4's default: 2 substeps of 1/120 s, velocity-level PGS, 8 sweeps, midpoint bias
+  tgs_fixed     TGS in-step with the drive implicit over the whole 1/120 s step (one factor, the
+                iterations only re-solve the contacts; solver_type 2, study only): what sub-stepping the
+                drives contributes
+  tgs_4x1       TGS's small-step form: 8 substeps of 1/480 s per simulate, one PGS sweep each, contacts,
+                mass matrix and drives regenerated per sub-step (PhysX TGS keeps the step's contacts)
+  pgs_4         2 substeps of 1/120 s, 4 PGS sweeps (PhysX's iteration count at the engine's step)
+  fine_8        8 substeps of 1/480 s, 8 PGS sweeps: a converged small-step reference
+  floor         the default from the start state with joint angles moved by 1e-6 rad: the chaos floor
+Distances per env over the 30 steps: max joint-angle L2 (69 exp-map coordinates) and max CoM
+distance; median / p90 / max over envs, and at step 1, 5, 10, 30; each against `tgs` (the default),
+`tgs_4x1` and `fine_8`.
+Cases (48 envs each): standing (PD stand-still, actions 0), tumbling (lying bodies thrown out of the
+plane, actions 0), tracking (configs[2]-style: synthetic clips, a = clip(ref_dof_pos / scale)).
 
-  python tests/diag/tgs_study.py > profiles/r04/tgs_study.json
+  python tests/diag/tgs_study.py > profiles/r05/tgs_study.json
 """
 import json
 import os
@@ -43,11 +42,13 @@ from humanoid_amd.model import load_default_model, pd_action_offset_scale  # noq
 from humanoid_amd.synthetic import make_clip  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
-SCHEMES = {"shipped": dict(substeps=2, solver_iterations=8),
-           "tgs_4x1": dict(substeps=8, solver_iterations=1),
-           "tgs_4x2": dict(substeps=8, solver_iterations=2),
-           "pgs_4": dict(substeps=2, solver_iterations=4),
-           "fine_8": dict(substeps=8, solver_iterations=8)}
+SCHEMES = {"tgs": dict(solver_type=1, solver_iterations=4),
+           "pgs": dict(solver_type=0, solver_iterations=8),
+           "tgs_fixed": dict(solver_type=2, solver_iterations=4),
+           "tgs_4x1": dict(solver_type=0, substeps=8, solver_iterations=1),
+           "pgs_4": dict(solver_type=0, solver_iterations=4),
+           "fine_8": dict(solver_type=0, substeps=8, solver_iterations=8)}
+REFS = ("tgs", "tgs_4x1", "fine_8")
 STEPS = 30
 MARKS = (1, 5, 10, 30)
 
@@ -108,18 +109,15 @@ def main():
     for name, (root, dof, tg) in {"standing": (*standing, lambda t: rest),
                                   "tumbling": (*lying, lambda t: rest),
                                   "tracking": tracking_case(model, n, np.random.default_rng(33))}.items():
-        base = run(hm, model, root, dof, tg, SCHEMES["shipped"])
-        case = {"chaos_floor (shipped+1e-6 rad)": distances(run(hm, model, root, dof, tg, SCHEMES["shipped"], 1e-6), base)}
-        for k, sch in SCHEMES.items():
-            if k != "shipped":
-                case[k] = distances(run(hm, model, root, dof, tg, sch), base)
-        fine = run(hm, model, root, dof, tg, SCHEMES["fine_8"])
-        case["shipped_vs_fine_8"] = distances(base, fine)
-        case["tgs_4x1_vs_fine_8"] = distances(run(hm, model, root, dof, tg, SCHEMES["tgs_4x1"]), fine)
+        runs = {k: run(hm, model, root, dof, tg, sch) for k, sch in SCHEMES.items()}
+        runs["floor"] = run(hm, model, root, dof, tg, SCHEMES["tgs"], 1e-6)
+        case = {}
+        for ref in REFS:
+            case[f"vs_{ref}"] = {k: distances(v, runs[ref]) for k, v in runs.items() if k != ref}
         res[name] = case
-        print(name, {k: round(v["joint_l2_max_over_steps_rad"]["median"], 6) for k, v in case.items()},
-              file=sys.stderr, flush=True)
-    res["definition"] = __doc__.split("\n\n")[2].strip()
+        print(name, {ref: {k: round(v["com_max_over_steps_m"]["median"], 6) for k, v in case[f"vs_{ref}"].items()}
+                     for ref in REFS}, file=sys.stderr, flush=True)
+    res["definition"] = __doc__.split("\n\n")[3].strip()
     res["schemes"] = SCHEMES
     print(json.dumps(res, indent=1))
 

@@ -57,8 +57,11 @@ def test_gpu_free_fall_is_the_discrete_parabola(he_model):
     k = 2 * steps * sub
     dt = 1.0 / 60.0 / sub
     assert (eng.num_contacts.cpu().numpy() == 0).all()
-    np.testing.assert_allclose(r[:, 2], root[:, 2] - G * dt * dt * k * (k + 1) / 2, atol=2e-5)
-    np.testing.assert_allclose(r[:, 9], -G * dt * k, atol=2e-5)
+    # fp32: each sub-step's velocity and position update rounds once, so the bound grows with their
+    # count (80 sub-steps of the PGS step 2e-5; TGS's 320 of 1/480 s 8e-5)
+    tol = 2.5e-7 * k
+    np.testing.assert_allclose(r[:, 2], root[:, 2] - G * dt * dt * k * (k + 1) / 2, atol=tol)
+    np.testing.assert_allclose(r[:, 9], -G * dt * k, atol=tol)
     # in float32 the gravity bias cancels to rounding only: 80 physics steps accumulate <= ~1e-4 rad
     np.testing.assert_allclose(eng.dof_state.view(n, 69, 2).cpu().numpy()[..., 0], dof[..., 0], atol=2e-4)
 

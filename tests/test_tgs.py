@@ -174,3 +174,23 @@ def test_tgs_is_closer_than_pgs_to_the_small_step_form(he_model, model):
     e_tgs = np.median(np.linalg.norm(com_traj(**TGS) - small, axis=-1).max(0))
     e_pgs = np.median(np.linalg.norm(com_traj(solver_type=0, solver_iterations=8) - small, axis=-1).max(0))
     assert e_tgs < 0.5 * e_pgs, (e_tgs, e_pgs)
+
+
+def test_tgs_replays_the_runaway_trace_without_the_launch(he_model):
+    """Round 4's fastest root (tests/data/trace_runaway_0.75.npz: env 3261 of the U(+-0.75) study,
+    engine state, warm-start cache and PD targets from 6 policy steps before its 17.4 m/s peak; DESIGN
+    §5 "the runaway tail"), replayed under TGS from the first recorded state: the forearm never wedges
+    into the thigh and the root stays under 5 m/s over the whole interval (measured max 3.2 m/s), as
+    under the PGS step at dt/4; the PGS step itself reproduces the launch (> 15 m/s at the peak)."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "data", "trace_runaway_0.75.npz"))
+    out = {}
+    for name, sp in (("tgs", _abi.default_sim_params(**TGS)), ("pgs", _abi.pgs_sim_params())):
+        r, dd = d["root"][0][None].copy(), d["dof"][0][None].copy()
+        c = d["cache"][0][None].copy()
+        vs = []
+        for i in range(d["targets"].shape[0]):
+            O.physics_step(he_model, sp, r, dd, d["targets"][i][None].copy(), 2, cache=c)
+            vs.append(float(np.linalg.norm(r[0, 7:10])))
+        out[name] = max(vs)
+    assert out["pgs"] > 15.0 and out["tgs"] < 5.0, out
