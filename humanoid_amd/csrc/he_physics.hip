@@ -2292,7 +2292,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             }
             };
             if (nrb <= 32) tgs_solve(std::integral_constant<int, 32>{});
+#ifdef HE_TGS_CLASS32_ONLY  // diagnostic A/B only (wrong past 32 rows): what the 63-row class costs the common path
+            else tgs_solve(std::integral_constant<int, 32>{});
+#else
             else tgs_solve(std::integral_constant<int, MAXR>{});
+#endif
             // the cache and the reported forces take the step's accumulated impulses
             L.lam[lane] = act ? lamv : 0.f;
             if (lane == 0) L.nwc = p.warm_start ? nr : 0;
