@@ -86,6 +86,12 @@ struct he_engine {
     int64_t m_frames = 0;
     int m_motions = 0;
     unsigned long long* stamps = nullptr;
+    // the physics launch's dispatch order (he_kernels.h launch_physics_order), rebuilt from the envs'
+    // cycle counts every order_every launches; HE_PHYS_ORDER=0 keeps workgroup id = env
+    int32_t* order = nullptr;    // [N]
+    uint32_t* cost = nullptr;    // [N]
+    int order_every = 8;
+    long long launches = 0;
 };
 
 extern "C" {
@@ -209,6 +215,14 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     HE_CHECK(hipMemset(h->cache, 0, (size_t)N * HE_CACHE_WORDS * sizeof(float)));
     HE_CHECK(dalloc(&h->meta_cache, (size_t)N * 8));
     HE_CHECK(hipMemset(h->meta_cache, 0xFF, (size_t)N * 8 * sizeof(int32_t)));  // motion -1: empty
+    // dispatch order: the identity until the first rebuild
+    std::vector<int32_t> ord((size_t)N);
+    for (int e = 0; e < N; ++e) ord[e] = e;
+    HE_CHECK(dalloc(&h->order, (size_t)N));
+    HE_CHECK(hipMemcpy(h->order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HE_CHECK(dalloc(&h->cost, (size_t)N));
+    HE_CHECK(hipMemset(h->cost, 0, (size_t)N * sizeof(uint32_t)));
+    if (const char* v = std::getenv("HE_PHYS_ORDER")) h->order_every = std::atoi(v);
     h->num_envs = N;
     return 0;
 }
@@ -218,7 +232,7 @@ int he_destroy(he_engine* h) {
     hipSetDevice(h->device);
     void* ptrs[] = {h->d_model, h->d_topo, h->root, h->dof_state, h->rb, h->cf, h->dof_force, h->targets,
                     h->num_contacts, h->dropped, h->cache, h->init_root, h->meta_cache, h->d_rest, h->pd_offset, h->pd_scale, h->frozen, h->m_hot, h->m_cold, h->m_lengths,
-                    h->m_dt, h->m_starts, h->m_nframes};
+                    h->m_dt, h->m_starts, h->m_nframes, h->order, h->cost};
     for (void* p : ptrs)
         if (p) hipFree(p);
     delete h;
@@ -369,16 +383,28 @@ static PhysArgs phys_args(he_engine* h, int num_simulate, const float* actions) 
     a.num_envs = h->num_envs;
     a.substeps = num_simulate * h->params.substeps;
     a.stamps = h->stamps;
+    const bool ordered = h->order_every > 0;
+    a.order = ordered ? h->order : nullptr;
+    a.cost = ordered ? h->cost : nullptr;
     return a;
 }
 }  // namespace
+
+// the physics launch, then every order_every launches the next launches' dispatch order from this
+// one's per-env cycles (heavy envs first, he_kernels.h launch_physics_order)
+static int physics_and_order(he_engine* h, const PhysArgs& a, hipStream_t stream) {
+    HE_CHECK(launch_physics(a, stream));
+    if (a.order && ++h->launches % h->order_every == 0)
+        HE_CHECK(launch_physics_order(h->cost, h->order, h->num_envs, stream));
+    return 0;
+}
 
 int he_simulate(he_engine* h, int num_simulate, void* stream) {
     if (!h || !h->num_envs) return fail("he_simulate: no envs");
     if (h->params.joint_limits && h->component_limits)
         return fail("he_simulate: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
     if (num_simulate < 1) return fail("he_simulate: num_simulate must be >= 1");
-    HE_CHECK(launch_physics(phys_args(h, num_simulate, nullptr), (hipStream_t)stream));
+    if (physics_and_order(h, phys_args(h, num_simulate, nullptr), (hipStream_t)stream)) return 1;
     return 0;
 }
 
@@ -388,7 +414,7 @@ int he_step_actions(he_engine* h, const float* actions, int num_simulate, void* 
     if (h->params.joint_limits && h->component_limits)
         return fail("he_step_actions: dof ranges inside +-(pi - 0.02) need per-component limit rows (not implemented)");
     if (num_simulate < 1) return fail("he_step_actions: num_simulate must be >= 1");
-    HE_CHECK(launch_physics(phys_args(h, num_simulate, actions), (hipStream_t)stream));
+    if (physics_and_order(h, phys_args(h, num_simulate, actions), (hipStream_t)stream)) return 1;
     return 0;
 }
 
@@ -661,6 +687,8 @@ int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion*
     PhysArgs pa = phys_args(h, num_simulate, actions);
     pa.fused = 1;
     pa.im = a;
+    pa.order = nullptr;  // one round of waves (auto): the dispatch order does not matter
+    pa.cost = nullptr;
     HE_CHECK(launch_physics(pa, (hipStream_t)stream));
     HE_CHECK(amp_after(h, a, 1, (hipStream_t)stream));
     return 0;

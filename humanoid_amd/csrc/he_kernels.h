@@ -110,6 +110,8 @@ struct PhysArgs {
     int num_envs;
     int substeps;
     unsigned long long* stamps;  // diagnostics: [N][16] phase cycles or null
+    const int32_t* order;        // [N] env of each workgroup (launch_physics_order), or null: env = workgroup id
+    uint32_t* cost;              // [N] each env's cycles in this launch (for launch_physics_order), or null
     int fused;                   // 1: the imitation step (mode 1) runs in the epilogue (he_env_step)
     ImitArgs im;                 // its arguments when fused
 };
@@ -119,6 +121,13 @@ hipError_t launch_amp(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_amp_function(const AmpArgs& a, hipStream_t stream);
 hipError_t launch_motion_state(const MotionStateArgs& a, hipStream_t stream);
 hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);
+// The physics launch's dispatch order, heavy envs first. A launch's 4096 one-wave workgroups fill the
+// chip's 2048 wave slots twice, and the hardware hands the second round out in workgroup order as
+// slots free: an expensive env dispatched late sets the launch's end. One 1024-thread workgroup reads
+// the envs' cycle counts of the last launch (PhysArgs.cost) and writes order[] as a stable partition:
+// the envs over the mean by 1/16 first, then the rest, each in env order. Results do not depend on the order
+// (envs never interact). The engine runs it every few physics launches (he_engine.cpp).
+hipError_t launch_physics_order(const uint32_t* cost, int32_t* order, int num_envs, hipStream_t stream);
 // First-dispatch warm-up (he_create_envs): every product kernel of the TU launched once with no work
 // (count 0, one block that exits at its guard), so the one-time first-dispatch cost of each kernel
 // (~0.4-0.8 ms on the MI355X, 16-30 ms under rocprofv3's kernel tracing) is paid at engine

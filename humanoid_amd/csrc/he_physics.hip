@@ -81,6 +81,8 @@ struct Lds {
     uint32_t limmask;              // bodies whose joint-angle limit row is emitted this substep
     int ncand;                     // contacts generated (dropped = ncand - nc), last substep
     alignas(8) int imbook[14];     // fused imitation: the env's bookkeeping + motion metadata (ImitBook)
+    unsigned long long sch_t0;     // dispatch order: the workgroup's start cycle (PhysArgs.cost)
+    int sch_e;                     // this workgroup's env (PhysArgs.order; no register held through the substeps)
     int ckey[MAXC];                // 16-bit key of each slot's normal row (include/humanoid_engine.h)
     int wckey[W];                  // the previous solve's row keys (its impulses: lam)
     int nwc;                       // rows cached in wckey / lam
@@ -2541,9 +2543,16 @@ template <bool TGS>
 HE_DEV void physics_body(const PhysArgs& a) {
     extern __shared__ float smem[];
     Lds& L = *reinterpret_cast<Lds*>(smem);
-    const int e = blockIdx.x;
-    if (e >= a.num_envs) return;  // the first-dispatch warm-up (warm_physics_kernels): no env
+    if ((int)blockIdx.x >= a.num_envs) return;  // the first-dispatch warm-up (warm_physics_kernels): no env
     const int lane = threadIdx.x;
+    // the env of this workgroup (launch_physics_order: heavy envs first); it and the start cycle wait
+    // in LDS for the epilogue (no registers held through the substeps)
+    const int e0 = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+    int e = e0;
+    if (lane == 0) {
+        L.sch_t0 = __builtin_readcyclecounter();
+        L.sch_e = e0;
+    }
     const he_model& m = *a.model;
     // ---- body-level tree tables into LDS
     if (lane < NB) {
@@ -2638,6 +2647,7 @@ HE_DEV void physics_body(const PhysArgs& a) {
         iraw = imitation_frames_load(a.im, lane, bk);  // loads only: the blends wait for the epilogue
     }
     // ---- outputs: generalized state, FK rigid-body state, forces
+    e = L.sch_e;  // from LDS: not held through the substeps
     kinematics<false>(L, m, lane, a.p, a.substeps > 0);
     STAMP(13);
     float* rso = a.root_states + (size_t)e * 13;
@@ -2691,6 +2701,10 @@ HE_DEV void physics_body(const PhysArgs& a) {
             cw[W + lane] = a.p.warm_start && r < nwc ? L.lam[r] : 0.f;
         }
     }
+    if (a.cost && lane == 0) {  // this env's cycles, for the next launch's order
+        const unsigned long long cyc = __builtin_readcyclecounter() - L.sch_t0;
+        a.cost[e] = cyc > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cyc;
+    }
 }
 
 // he_sim_params.solver_type 0 (PGS) and 1 (TGS): one instantiation each, so that the TGS iterations'
@@ -2707,6 +2721,46 @@ static_assert(sizeof(Lds) <= 20480, "two workgroups per SIMD (8 per CU) need <= 
 size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16 + HE_LDS_EXTRA; }
 
 bool physics_phase_stamps() { return HE_PHASE_STAMPS != 0; }
+
+namespace {
+// launch_physics_order (he_kernels.h): one workgroup of 1024 threads, thread t owns the contiguous
+// chunk [t c, t c + c) of envs (c = ceil(N / 1024)); the mean cost, then per chunk its heavy count,
+// a block-wide exclusive scan of the counts, and the chunk's envs written heavy-first / light-after
+constexpr int kOrderThreads = 1024;
+__global__ void __launch_bounds__(kOrderThreads) physics_order_kernel(const uint32_t* cost, int32_t* order, int n) {
+    __shared__ unsigned long long red[kOrderThreads / 64];
+    __shared__ int scan[kOrderThreads];
+    const int t = threadIdx.x;
+    const int c = (n + kOrderThreads - 1) / kOrderThreads;
+    const int b0 = t * c < n ? t * c : n, b1 = (t + 1) * c < n ? (t + 1) * c : n;
+    unsigned long long s = 0;
+    for (int i = b0; i < b1; ++i) s += cost[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if ((t & 63) == 0) red[t >> 6] = s;
+    __syncthreads();
+    unsigned long long tot = 0;
+    for (int w = 0; w < kOrderThreads / 64; ++w) tot += red[w];
+    // heavy: over the mean by 1/16 (a uniform workload keeps the identity order, and its locality)
+    const unsigned long long mean = n > 0 ? tot / (unsigned long long)n + tot / (16ull * (unsigned long long)n) : 0ull;
+    int h = 0;
+    for (int i = b0; i < b1; ++i) h += cost[i] > mean ? 1 : 0;
+    scan[t] = h;
+    __syncthreads();
+    for (int o = 1; o < kOrderThreads; o <<= 1) {  // inclusive Hillis-Steele scan of the heavy counts
+        const int v = t >= o ? scan[t - o] : 0;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+    }
+    const int heavy_before = scan[t] - h;
+    const int heavy_total = scan[kOrderThreads - 1];
+    int ph = heavy_before, pl = heavy_total + (b0 - heavy_before);  // light before = envs before - heavy before
+    for (int i = b0; i < b1; ++i) {
+        if (cost[i] > mean) order[ph++] = i;
+        else order[pl++] = i;
+    }
+}
+}  // namespace
 
 namespace {
 __global__ void warm_tu_kernel() {}
@@ -2726,6 +2780,15 @@ hipError_t warm_physics_kernels(hipStream_t stream, int mode) {
     physics_kernel<<<1, W, physics_lds_bytes(), stream>>>(pa);
     HE_RETURN_IF(hipGetLastError());
     physics_kernel_tgs<<<1, W, physics_lds_bytes(), stream>>>(pa);
+    HE_RETURN_IF(hipGetLastError());
+    physics_order_kernel<<<1, kOrderThreads, 0, stream>>>(nullptr, nullptr, 0);
+    return hipGetLastError();
+}
+
+
+hipError_t launch_physics_order(const uint32_t* cost, int32_t* order, int num_envs, hipStream_t stream) {
+    if (num_envs <= 0) return hipSuccess;
+    physics_order_kernel<<<1, kOrderThreads, 0, stream>>>(cost, order, num_envs);
     return hipGetLastError();
 }
 

@@ -51,6 +51,26 @@ def test_full_size_deterministic_and_finite(model, config):
         assert torch.equal(x, y), "the step must be bit-reproducible"
 
 
+def test_dispatch_order_leaves_the_step_unchanged(model):
+    """configs[4] with the heavy-first dispatch order rebuilt after every launch (HE_PHYS_ORDER=1,
+    he_kernels.h launch_physics_order) against workgroup id = env (HE_PHYS_ORDER=0): envs never
+    interact, so 12 steps (11 reorders, over slope, stairs and flat envs of unequal cost) must give
+    the same state to the bit."""
+    outs = []
+    for v in ("0", "1"):
+        os.environ["HE_PHYS_ORDER"] = v
+        try:
+            ro = _rollout("dr", model)
+        finally:
+            os.environ.pop("HE_PHYS_ORDER", None)
+        for _ in range(12):
+            ro.step()
+        torch.cuda.synchronize()
+        outs.append(_state(ro) + (ro.eng.contact_cache.clone(), ro.eng.rb_state.clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y), "the dispatch order must not change any env's step"
+
+
 def test_full_size_standstill_invariant(model):
     ro = _rollout("standstill", model)
     z0 = ro.eng.root_states[:, 2].clone()

@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--max-contacts", type=int, default=40)
     ap.add_argument("--fused", action="store_true")
-    ap.add_argument("--scheme", choices=["default", "r02", "tgs", "tgs_small"], default="default")
+    ap.add_argument("--scheme", choices=["default", "pgs", "r02", "tgs_small"], default="default")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -57,9 +57,18 @@ def main():
     total = mean[:len(PHASES)].sum()
     rows = {PHASES[i]: {"cycles": round(float(mean[i])), "share": round(float(mean[i] / total), 4)}
             for i in range(len(PHASES))}
+    # the launch waits for its slowest waves: the per-env distribution, and the phases of the slowest 2 %
+    tot = cyc[:, :len(PHASES)].sum(1)
+    slow = tot >= np.percentile(tot, 98)
+    ms = cyc[slow].mean(0)
+    slow_rows = {PHASES[i]: round(float(ms[i])) for i in range(len(PHASES)) if ms[i] > 0}
+    dist = {"p50": round(float(np.percentile(tot, 50))), "p90": round(float(np.percentile(tot, 90))),
+            "p98": round(float(np.percentile(tot, 98))), "max": round(float(tot.max())),
+            "mean": round(float(tot.mean())), "slowest_2pct_phases": slow_rows}
     print(json.dumps({"config": args.config, "num_envs": args.num_envs, "mean_contacts": float(np.mean(nc)),
                       "scheme": args.scheme,
-                      "cycles_per_env_step": round(float(total)), "phases": rows}, indent=1))
+                      "cycles_per_env_step": round(float(total)), "phases": rows,
+                      "per_env_cycles": dist}, indent=1))
 
 
 if __name__ == "__main__":
