@@ -1,5 +1,5 @@
 """Contact-slot histograms on the GPU: how many contact slots envs use and how
-many contacts the 20-slot capacity drops, for lying bodies (cases.lying_state: limbs start inside the
+many contacts the engine capacity (he_sim_params.max_contacts slots, 63 solver rows) drops, for lying bodies (cases.lying_state: limbs start inside the
 plane, the overflow case) and for configs[4] (mass / friction randomisation + plane / 10 deg slope /
 box steps, the divergent contact-set stress config). Writes JSON to stdout."""
 import argparse
@@ -61,7 +61,7 @@ def main():
                        "dropped_mean": float(dr[tk == k].mean())}
                 for k, kind in enumerate(("plane", "slope10", "steps"))}
     out["configs4_dr"] = dr_hist
-    out["capacity"] = 20
+    out["capacity"] = {"slots": int(_abi.default_sim_params().max_contacts), "rows": int(_abi.MAX_ROWS)}
     print(json.dumps(out))
 
 
