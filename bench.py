@@ -35,6 +35,21 @@ PHYS_FLOP_PER_SUBSTEP = 654_639            # dense-equivalent physics per physic
 # SURVEY's 1,309,278 FLOP/env-step counts 2 physics steps; the engine runs gym.simulate() x 2 with
 # SimParams.substeps = 2 (Isaac Gym's default), i.e. 4 physics steps of 1/120 s per env-step
 IMIT_FLOP_PER_ENV_STEP = 30_000             # the imitation step (≈0.03 MFLOP)
+
+
+def canonical_flop_per_physics_step(m):
+    """SURVEY §8(d)'s dense-equivalent count per physics step with m contact rows (n = 75): mass
+    matrix 135,756 + factorisation n^3/3 + bias 6,000 + 2 triangular solves 2 n^2 + contacts
+    2 n^2 m + 2 n m^2 + 4 x 2 m^2 (654,639 at m = 3 x 8)."""
+    n = 75
+    return 135_756 + n ** 3 / 3 + 6_000 + 2 * n * n + 2 * n * n * m + 2 * n * m * m + 8 * m * m
+
+
+def canonical_at_rows(m, physics_steps, envs, launch_ms):
+    flop = canonical_flop_per_physics_step(m) * physics_steps
+    tf = flop * envs / (launch_ms * 1e-3) / 1e12
+    return {"rows_mean": round(m, 2), "flop_per_env_step": round(flop), "achieved": round(tf, 4),
+            "frac": round(tf / FP32_PEAK_TFLOPS, 6)}
 IMIT_BYTES_PER_ENV_STEP = 13_200            # fused imitation kernel share of the 16.0 KB/env-step
 
 
@@ -541,6 +556,8 @@ def main():
     elapsed = time.perf_counter() - t0
     nc = ro.eng.num_contacts.cpu().numpy()
     dropped = ro.eng.dropped_contacts.cpu().numpy()
+    # solver rows of each env's last solve: word 7 of the warm-start cache (include/humanoid_engine.h)
+    rows = ro.eng.contact_cache[:, 7].contiguous().view(torch.int32).cpu().numpy()
     # kernel durations: a pass of EV_STEPS further steps (untimed, the same workload continuing) with
     # HIP events around the launches of EVERY step, on the engine's stream (torch's current stream);
     # the medians are the per-launch figures (compare the rocprofv3 averages of the same command)
@@ -624,7 +641,10 @@ def main():
                      "kernel": f"{'physics_kernel_tgs' if scheme_params(args).get('solver_type', 1) == 1 else 'physics_kernel'} "
                                f"(fp32 VALU + MFMA; SURVEY §8d canonical 0.6546 MFLOP per physics step "
                                f"x {2 * sim_substeps(args)} physics steps per env-step)",
-                     "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma}
+                     "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma,
+                     # "report n_c as measured" -- the same count with the measured mean
+                     # solver rows as m (patch friction: a standing body 28 rows, not 3 x 16 slots)
+                     "at_measured_rows": canonical_at_rows(float(rows.mean()), 2 * sim_substeps(args), n, phys_ms)}
         if split is not None:  # the fused launch (physics + the imitation epilogue) is the dominant kernel
             f_tflops = (phys_flop + IMIT_FLOP_PER_ENV_STEP) * n / (fused_ms * 1e-3) / 1e12
             roof = {"bound": "latency", "achieved": round(f_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
