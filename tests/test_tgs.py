@@ -179,18 +179,35 @@ def test_tgs_is_closer_than_pgs_to_the_small_step_form(he_model, model):
 def test_tgs_replays_the_runaway_trace_without_the_launch(he_model):
     """Round 4's fastest root (tests/data/trace_runaway_0.75.npz: env 3261 of the U(+-0.75) study,
     engine state, warm-start cache and PD targets from 6 policy steps before its 17.4 m/s peak; DESIGN
-    §5 "the runaway tail"), replayed under TGS from the first recorded state: the forearm never wedges
-    into the thigh and the root stays under 5 m/s over the whole interval (measured max 3.2 m/s), as
-    under the PGS step at dt/4; the PGS step itself reproduces the launch (> 15 m/s at the peak)."""
+    §5 "the runaway tail"), replayed one physics step (1/120 s) at a time from the first recorded
+    state, every row's gap at the step's start recorded (oracle row-gap diagnostic):
+    * under the PGS step the right forearm and hand wedge into the thigh (self rows 8.5 cm deep) and
+      the root is launched past 15 m/s;
+    * under TGS no self contact gets deeper than 3 cm (measured 2.4 cm: the 2 cm contact offset plus
+      one step's approach) and the root stays under 5 m/s (measured max 3.2 m/s), as under the PGS
+      step at dt/4."""
     import os
     d = np.load(os.path.join(os.path.dirname(__file__), "data", "trace_runaway_0.75.npz"))
     out = {}
-    for name, sp in (("tgs", _abi.default_sim_params(**TGS)), ("pgs", _abi.pgs_sim_params())):
+    for name, sp in (("tgs", _abi.default_sim_params(dt=1.0 / 120.0, substeps=1, **TGS)),
+                     ("pgs", _abi.pgs_sim_params(dt=1.0 / 120.0, substeps=1))):
         r, dd = d["root"][0][None].copy(), d["dof"][0][None].copy()
         c = d["cache"][0][None].copy()
-        vs = []
+        vmax, self_gap = 0.0, 0.0
         for i in range(d["targets"].shape[0]):
-            O.physics_step(he_model, sp, r, dd, d["targets"][i][None].copy(), 2, cache=c)
-            vs.append(float(np.linalg.norm(r[0, 7:10])))
-        out[name] = max(vs)
-    assert out["pgs"] > 15.0 and out["tgs"] < 5.0, out
+            for _ in range(4):  # a policy step: 2 simulate() x 2 substeps
+                gp = np.zeros((1, _abi.MAX_ROWS), np.float32)
+                O.set_row_gap_out(gp)
+                try:
+                    O.physics_step(he_model, sp, r, dd, d["targets"][i][None].copy(), 1, cache=c)
+                finally:
+                    O.set_row_gap_out(None)
+                n, keys, _ = _abi.cache_rows(c)
+                for k in range(int(n[0])):
+                    b0, b1, sub, kind = _abi.key_fields(keys[0, k])
+                    if kind == 0 and b1 >= 0:  # a self pair's normal row
+                        self_gap = min(self_gap, float(gp[0, k]))
+                vmax = max(vmax, float(np.linalg.norm(r[0, 7:10])))
+        out[name] = (vmax, self_gap)
+    assert out["pgs"][0] > 15.0 and out["pgs"][1] < -0.05, out
+    assert out["tgs"][0] < 5.0 and out["tgs"][1] > -0.03, out
