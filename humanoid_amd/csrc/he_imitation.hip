@@ -165,9 +165,6 @@ HE_DEV void eval_record(const he_eval_buffers& ev, int e, int lane, bool act, f3
     }
 }
 
-#ifndef HE_IMIT_PREFETCH  // time-out resets' frames loaded with the step's (he_imitation_env.h ResetPre)
-#define HE_IMIT_PREFETCH 0
-#endif
 // EVAL: eval recording compiled in (its fp64 Procrustes solve would otherwise set the register
 // budget of every launch)
 #ifndef HE_IMIT_THREADS  // threads per workgroup of the imitation kernel
@@ -222,15 +219,8 @@ __global__ void __launch_bounds__(HE_IMIT_THREADS, HE_IMIT_MIN_WAVES) imitation_
                               (int)((uint64_t)mm.start >> 32));
         }
     }
-#if HE_IMIT_PREFETCH
-    const ImitBook bk{mid, off, start, soff, prog, mm};
-    const ImitRaw raw = imitation_frames_load(a, lane, bk);
-    const ResetPre pre = reset_prefetch(a, e, lane, bk, raw.t);
-    imitation_finish<EVAL, true>(a, slot, e, lane, lane == 0, imitation_frames_blend(raw), s, pw, &pre);
-#else
     imitation_finish<EVAL>(a, slot, e, lane, lane == 0,
                            imitation_frames(a, lane, ImitBook{mid, off, start, soff, prog, mm}), s, pw);
-#endif
 }
 
 // MotionLibBase.get_motion_state for K queries (motion_lib.py:549-626)

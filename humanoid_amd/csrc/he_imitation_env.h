@@ -404,35 +404,9 @@ HE_DEV ImitRef imitation_ref(const ImitArgs& a, int lane, int64_t mid, f3 off, f
     return imitation_frames(a, lane, imitation_book(a, mid, off, start, soff, prog));
 }
 
-// A time-out reset's frames, loaded with the step's own frames (mode 1): whether the episode's time
-// runs out (reset = pass_time || fallen) and the reset draw (hash of seed, step, env) are known once
-// the motion metadata is, so their records ride the step's frame round trip instead of a dependent
-// one at the end. Envs not timing out load the step's first sample again (cache hits): the loads stay
-// unconditional, so no branch's phi makes the wave wait for them.
-struct ResetPre {
-    bool valid;  // the env times out this step and resets to a reference state (the rows below)
-    RefRows h0;
-    ColdRows c0;
-    RefRows n2;
-};
-HE_DEV ResetPre reset_prefetch(const ImitArgs& a, int e, int lane, const ImitBook& k, float t) {
-    ResetPre r;
-    const int b = lane < NB ? lane : 0;
-    const he_imitation_params& p = a.p;
-    float ph = 0.0f;
-    const bool ref_init = resolve_init(p, hash_uniform(a.seed, a.step, (uint32_t)e), ph);
-    const float rt = ref_init ? sample_time_interval(ph, k.mm.len) : 0.0f;
-    r.valid = a.mode == 1 && t >= k.mm.len && ref_init;
-    const FrameSel f1 = frame_select(k.mm, r.valid ? rt : t);
-    r.h0 = body_ref_load(a.m, f1, b);
-    r.c0 = body_cold_load(a.m, f1, b);
-    r.n2 = body_ref_load(a.m, frame_select(k.mm, r.valid ? env_time(1, p.control_dt, rt, 0.0f) : t), b);
-    return r;
-}
-
-template <bool EVAL, bool PRE = false>
+template <bool EVAL>
 HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool leader, const ImitRef& x, SimBody s,
-                             float pw, const ResetPre* pre = nullptr) {
+                             float pw) {
     const bool act = lane < NB;
     const int b = act ? lane : 0;
     const he_imitation_params& p = a.p;
@@ -540,18 +514,10 @@ HE_DEV void imitation_finish(const ImitArgs& a, int slot, int e, int lane, bool 
     } else if (do_reset) {  // the group's branch is uniform
         // the reset frames (hot and cold records) and the next observation's frames, loaded
         // together: one round trip (the metadata is the step's)
-        RefRows h0, n2;
-        ColdRows c0;
-        if (PRE && pre->valid) {  // a time-out: its frames came with the step's (reset_prefetch)
-            h0 = pre->h0;
-            c0 = pre->c0;
-            n2 = pre->n2;
-        } else {
-            const FrameSel fs = frame_select(mm, reset_time);
-            h0 = body_ref_load(a.m, fs, b);
-            c0 = body_cold_load(a.m, fs, b);
-            n2 = body_ref_load(a.m, frame_select(mm, env_time(1, p.control_dt, reset_time, 0.0f)), b);
-        }
+        const FrameSel fs = frame_select(mm, reset_time);
+        const RefRows h0 = body_ref_load(a.m, fs, b);
+        const ColdRows c0 = body_cold_load(a.m, fs, b);
+        const RefRows n2 = body_ref_load(a.m, frame_select(mm, env_time(1, p.control_dt, reset_time, 0.0f)), b);
         const BodyRef r0 = body_ref_blend(h0, off);
         if (act) reset_body_write(a, e, b, r0, c0);
         s = SimBody{r0.pos, r0.vel, r0.ang, r0.rot};  // the row this lane wrote (lane b = 0's on idle lanes)

@@ -38,9 +38,6 @@ constexpr int MAXR = HE_MAX_ROWS;      // solver rows, one per lane (patch frict
 constexpr int W = 64;
 static_assert(MAXR <= W - 1, "solver rows must fit one per lane");
 constexpr int kTgsMaxIt = 16;  // TGS position iterations per physics step (he_simulate checks; oracle TGS_MAXIT)
-#ifndef HE_TGS_INTERLEAVE  // A/B: the integration inside the bias RNEA's first region (1) or before it (0)
-#define HE_TGS_INTERLEAVE 0
-#endif
 constexpr int kTgsBiasEvery = 2;  // TGS: the bias re-evaluated every second iteration (oracle g_bias_every)
 static_assert(MAXC < W, "one slot per lane in the row-layout pass");
 static_assert(smpl::kNG == NG && smpl::kNB == NB, "generated topology mismatch");
@@ -1169,9 +1166,8 @@ HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_para
 // accelerations by pointer jumping, their forces, the subtree sums by body levels (L.Acc scratch: the
 // contact phase's bounding spheres and patch radii are dead after the row set-up). Returns b_i = S_i . F
 // for dof lane and dof 64 + lane (lanes < NH).
-template <class Also>
 HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, const float* vel, float& c1,
-                        float& c2, Also&& also) {
+                        float& c2) {
     // in short phases through LDS (the body velocities V and joint velocities vj in the V / F words, dead
     // from the row set-up to the next kinematics), so that each phase's temporaries fit beside the
     // iterations' long-lived rows and columns
@@ -1214,7 +1210,6 @@ HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params
         if (bl)
             for (int x = 0; x < 6; ++x) L.V[b][x] = V[x];
     }
-    also();  // independent lane work the first region's chain can hide (the iteration's integration)
     sync();
     __builtin_amdgcn_sched_barrier(0);
     {  // bias accelerations A = prefix of V x vj (+ the base's), then the body forces
@@ -1325,7 +1320,6 @@ HE_DEV SimBody body_row(const Lds& L, int b) {
 // L.u0). write_out: the damped, clamped velocity becomes the state's (PGS always; TGS the last
 // position iteration only: the solver's own velocity is not clamped, oracle substep_tgs). detect: the
 // next substep's limit rows from the new state.
-template <bool SYNC = true>
 HE_DEV void integrate_bodies(Lds& L, const BodyTopo& T, int lane, const he_sim_params& p, float hs, float damp,
                              const float* src, bool write_out, bool detect) {
     // damping, the angular-velocity clamps and the semi-implicit position update in one pass per
@@ -1415,7 +1409,7 @@ HE_DEV void integrate_bodies(Lds& L, const BodyTopo& T, int lane, const he_sim_p
         }
     }
     if (p.joint_limits && detect) limit_detect(L, lane, lane >= 1 && lane < NB, lim_th, lim_u, p);
-    if constexpr (SYNC) sync();
+    sync();
 }
 
 // ---------------------------------------------------------------------------------- one substep
@@ -2041,22 +2035,15 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
     auto tgs_advance = [&](int it) {
         const bool lastit = it + 1 == K;
         tgs_drive_acc(L, lane, tf1, tf2);
-        // the velocity-dependent bias: re-evaluated at the start of every second iteration (oracle
-        // g_bias_every: as stable as every iteration at half the passes), else the one in L.uf. It
-        // reads only u and the step's kinematics, so the integration (which writes the positions)
-        // runs inside its first region, the two chains interleaved
-        const bool rebias = !lastit && p.bias_midpoint && ((it + 1) % kTgsBiasEvery) == 0;
-        if (!HE_TGS_INTERLEAVE || !rebias) {
-            integrate_bodies(L, T, lane, p, hs, damp, L.u0, lastit, lastit && !last);
-            __builtin_amdgcn_sched_barrier(0);
-            STAMP(12);
-        }
+        integrate_bodies(L, T, lane, p, hs, damp, L.u0, lastit, lastit && !last);
+        __builtin_amdgcn_sched_barrier(0);
+        STAMP(12);
         if (!lastit) {
-            if (rebias) {
+            // the velocity-dependent bias: re-evaluated at the start of every second iteration (oracle
+            // g_bias_every: as stable as every iteration at half the passes), else the one in L.uf
+            if (p.bias_midpoint && ((it + 1) % kTgsBiasEvery) == 0) {
                 float b1, b2;
-                tgs_bias_at(L, T, lane, p, L.u0, b1, b2, [&]() {
-                    if constexpr (HE_TGS_INTERLEAVE) integrate_bodies<false>(L, T, lane, p, hs, damp, L.u0, false, false);
-                });
+                tgs_bias_at(L, T, lane, p, L.u0, b1, b2);
                 L.uf[lane] = b1;
                 if (lane < NH) L.uf[64 + lane] = b2;
             }
