@@ -245,17 +245,20 @@ constexpr uint64_t level_desc_hi() {
     if constexpr (J < kLevelStart[D + 1]) return kDescHi[kLevelDofs[J]] | level_desc_hi<D, J + 1>();
     else return 0ull;
 }
-// per level: every descendant lane picks the y of its (unique) ancestor at this depth
-template <int D, int J>
+// per level: every descendant lane picks the y of its (unique) ancestor at this depth. The first
+// dof of the level with descendants in a register set is written to every lane of it (a plain
+// broadcast, no select): the caller's update is restricted to the level's descendant lanes, so what
+// the others hold does not matter, and t1 / t2 need no zero fill
+template <int D, int J, bool F1 = true, bool F2 = true>
 __device__ __forceinline__ void level_pick(float yl, float y2, float& t1, float& t2) {
     if constexpr (J < kLevelStart[D + 1]) {
         constexpr int K = kLevelDofs[J];
         if constexpr (kDescLo[K] != 0 || kDescHi[K] != 0) {
             const float yk = K < 64 ? rdlane(yl, K) : rdlane(y2, K - 64);
-            if constexpr (kDescLo[K] != 0) t1 = lanes<kDescLo[K]>() ? yk : t1;
-            if constexpr (kDescHi[K] != 0) t2 = lanes<(uint64_t)kDescHi[K]>() ? yk : t2;
+            if constexpr (kDescLo[K] != 0) t1 = F1 ? yk : (lanes<kDescLo[K]>() ? yk : t1);
+            if constexpr (kDescHi[K] != 0) t2 = F2 ? yk : (lanes<(uint64_t)kDescHi[K]>() ? yk : t2);
         }
-        level_pick<D, J + 1>(yl, y2, t1, t2);
+        level_pick<D, J + 1, F1 && kDescLo[K] == 0, F2 && kDescHi[K] == 0>(yl, y2, t1, t2);
     }
 }
 // y <- L^-1 y by depth levels, shallowest first: the dofs of one level have disjoint descendant
@@ -267,7 +270,9 @@ __device__ __forceinline__ void solve_L_rows(const float (&r1)[kRowRegs], const 
         constexpr uint64_t ulo = level_desc_lo<D>();
         constexpr uint64_t uhi = level_desc_hi<D>();
         if constexpr (ulo != 0 || uhi != 0) {
-            float t1 = 0.f, t2 = 0.f;
+            float t1, t2;  // written by level_pick on every lane of a set the level touches
+            undef_reg(t1);
+            undef_reg(t2);
             level_pick<D, kLevelStart[D]>(yl, y2, t1, t2);
             if constexpr (ulo != 0) yl = lanes<ulo>() ? yl - r1[D] * t1 : yl;
             if constexpr (uhi != 0) y2 = lanes<uhi>() ? y2 - r2[D] * t2 : y2;
@@ -298,7 +303,9 @@ __device__ __forceinline__ void solve_L_stream(const f4v* p1, const f4v* p2, f4v
         constexpr uint64_t ulo = level_desc_lo<D>();
         constexpr uint64_t uhi = level_desc_hi<D>();
         if constexpr (ulo != 0 || uhi != 0) {
-            float t1 = 0.f, t2 = 0.f;
+            float t1, t2;  // written by level_pick on every lane of a set the level touches
+            undef_reg(t1);
+            undef_reg(t2);
             level_pick<D, kLevelStart[D]>(yl, y2, t1, t2);
             if constexpr (ulo != 0) yl = lanes<ulo>() ? yl - c1[D % 4] * t1 : yl;
             if constexpr (uhi != 0) y2 = lanes<uhi>() ? y2 - c2[D % 4] * t2 : y2;
