@@ -160,22 +160,65 @@ HE_DEV void crf(const float* V, const float* Fm, float* O) {
 }
 
 
-// rotation-vector exponential / logarithm for the physics kernel: one sincos range reduction and
-// v_rcp_f32 quotients (1 ulp; the fp64 oracle's tolerance covers it). The imitation kernel keeps
-// he_math.h's forms, which follow torch's rounding.
+// rotation-vector exponential / logarithm for the physics kernel, short instruction sequences (the
+// integration runs them in every TGS position iteration): v_sqrt_f32 and v_rcp_f32 (1 ulp), sin / cos
+// of the half angle by their Taylor series up to x^9 / x^10 (|x| <= 1: error < 3e-8, below fp32
+// rounding; a step turning a joint by more than 2 rad takes ocml's sincosf), atan on [0, 1] by
+// Abramowitz-Stegun 4.4.49 (|error| <= 1e-8). The fp64 oracle's tolerance covers them. The imitation
+// kernel keeps he_math.h's forms, which follow torch's rounding.
+// a polynomial's second coefficient materialised where it is used (the FMAs take the others as
+// literals): left to the compiler, it is hoisted out of the TGS iterations into a register held
+// through them, and that register pushes the loop's long-lived state into scratch
+template <uint32_t BITS>
+HE_DEV float here(void) {
+    float r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "n"(BITS));
+    return r;
+}
+HE_DEV void half_sincos(float x, float& sn, float& cs) {
+    if (__builtin_expect(x > 1.0f, 0)) {
+        sincosf(x, &sn, &cs);
+        return;
+    }
+    const float x2 = x * x;
+    float ps = fmaf(x2, 2.75573192e-6f, here<0xb9500d01u>());  // -1.98412698e-4
+    ps = fmaf(x2, ps, 8.33333333e-3f);
+    ps = fmaf(x2, ps, -1.66666667e-1f);
+    sn = fmaf(x * x2, ps, x);
+    float pc = fmaf(x2, -2.75573192e-7f, here<0x37d00d01u>());  // 2.48015873e-5
+    pc = fmaf(x2, pc, -1.38888889e-3f);
+    pc = fmaf(x2, pc, 4.16666667e-2f);
+    pc = fmaf(x2, pc, -0.5f);
+    cs = fmaf(x2, pc, 1.0f);
+}
+HE_DEV float atan01(float t) {  // t in [0, 1]
+    const float t2 = t * t;
+    float p = fmaf(t2, 0.0028662257f, here<0xbc846e02u>());  // -0.0161657367
+    p = fmaf(t2, p, 0.0429096138f);
+    p = fmaf(t2, p, -0.0752896400f);
+    p = fmaf(t2, p, 0.1065626393f);
+    p = fmaf(t2, p, -0.1420889944f);
+    p = fmaf(t2, p, 0.1999355085f);
+    p = fmaf(t2, p, -0.3333314528f);
+    return fmaf(t * t2, p, t);
+}
 HE_DEV f4 pqexp(f3 v) {
-    const float th = norm3(v);
+    const float th = __builtin_amdgcn_sqrtf(dot3(v, v));
     if (th < 1e-8f) return qnormalize(f4{0.5f * v.x, 0.5f * v.y, 0.5f * v.z, 1.f});
     float sh, ch;
-    sincosf(0.5f * th, &sh, &ch);
+    half_sincos(0.5f * th, sh, ch);
     const float s = sh * __builtin_amdgcn_rcpf(th);
     return f4{v.x * s, v.y * s, v.z * s, ch};
 }
 HE_DEV f3 pqlog(f4 q) {
     if (q.w < 0.f) q = qneg(q);
-    const float s = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+    const float s = __builtin_amdgcn_sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
     if (s < 1e-8f) return f3{2.f * q.x, 2.f * q.y, 2.f * q.z};
-    const float k = 2.f * atan2f(s, q.w) * __builtin_amdgcn_rcpf(s);
+    // atan2(s, w) on the first quadrant (s > 0, w >= 0): the smaller over the larger, then pi / 2 - a
+    const float lo = fminf(s, q.w), hi = fmaxf(s, q.w);
+    const float a = atan01(lo * __builtin_amdgcn_rcpf(hi));
+    const float ang = s > q.w ? 1.57079632679f - a : a;
+    const float k = 2.f * ang * __builtin_amdgcn_rcpf(s);
     return f3{q.x * k, q.y * k, q.z * k};
 }
 

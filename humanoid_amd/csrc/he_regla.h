@@ -383,20 +383,19 @@ struct LTGroup {
     static constexpr int S0 = G < kLTPipeGroups.count ? kLTPipeGroups.start[G] : 0;
     static constexpr int N = G < kLTPipeGroups.count ? kLTPipeGroups.start[G + 1] - S0 : 1;
 };
+// p1 = Lp + dj, p2 = Lp + dj2 (the lane's depth offsets, added once per group): each entry is one LDS
+// read at an immediate offset, no per-pivot address arithmetic. A lane that is not an ancestor of
+// K reads past row K (other rows of the factor, or the words after it); lt_group_apply's select
+// never lets that value in.
 template <int S0, int Q, int N>
-__device__ __forceinline__ void lt_group_load(const float* Lp, int dj, int dj2, float (&l1)[N], float (&l2)[N]) {
+__device__ __forceinline__ void lt_group_load(const float* p1, const float* p2, float (&l1)[N], float (&l2)[N]) {
     if constexpr (Q < N) {
         constexpr int K = kElimOrder[S0 + Q];
-        constexpr int top = kPackStart[K] + (kDofNanc[K] > 1 ? kDofNanc[K] - 2 : 0);  // the row's last entry
         if constexpr (kDofNanc[K] - 1 > 0) {
-            const int o1 = kPackStart[K] + dj;
-            l1[Q] = Lp[o1 < top ? o1 : top];
-            if constexpr (K > 64) {
-                const int o2 = kPackStart[K] + dj2;
-                l2[Q] = Lp[o2 < top ? o2 : top];
-            }
+            l1[Q] = p1[kPackStart[K]];
+            if constexpr (K > 64) l2[Q] = p2[kPackStart[K]];
         }
-        lt_group_load<S0, Q + 1, N>(Lp, dj, dj2, l1, l2);
+        lt_group_load<S0, Q + 1, N>(p1, p2, l1, l2);
     }
 }
 template <int S0, int Q, int N>
@@ -425,7 +424,7 @@ __device__ __forceinline__ void solve_LT_vec_pipe(const float* Lp, int dj, int d
         if constexpr (G + 1 < kLTPipeGroups.count) {
             int off = 0;
             asm volatile("" : "+v"(off));  // the loads stay here, one group ahead
-            lt_group_load<Nx::S0, 0, Nx::N>(Lp + off, dj, dj2, n1, n2);
+            lt_group_load<Nx::S0, 0, Nx::N>(Lp + (off + dj), Lp + (off + dj2), n1, n2);
         }
         float yk[C::N];
         lt_group_read<C::S0, 0, C::N>(yk, yl, y2);
@@ -436,7 +435,7 @@ __device__ __forceinline__ void solve_LT_vec_pipe(const float* Lp, int dj, int d
 }
 __device__ __forceinline__ void solve_LT_vec_pipelined(const float* Lp, int dj, int dj2, float& yl, float& y2) {
     float l1[LTGroup<0>::N], l2[LTGroup<0>::N];
-    lt_group_load<LTGroup<0>::S0, 0, LTGroup<0>::N>(Lp, dj, dj2, l1, l2);
+    lt_group_load<LTGroup<0>::S0, 0, LTGroup<0>::N>(Lp + dj, Lp + dj2, l1, l2);
     solve_LT_vec_pipe<0>(Lp, dj, dj2, yl, y2, l1, l2);
 }
 
