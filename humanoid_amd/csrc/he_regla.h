@@ -422,9 +422,9 @@ __device__ __forceinline__ void solve_LT_vec_pipe(const float* Lp, int dj, int d
         using Nx = LTGroup<G + 1>;
         float n1[Nx::N], n2[Nx::N];
         if constexpr (G + 1 < kLTPipeGroups.count) {
-            int off = 0;
-            asm volatile("" : "+v"(off));  // the loads stay here, one group ahead
-            lt_group_load<Nx::S0, 0, Nx::N>(Lp + (off + dj), Lp + (off + dj2), n1, n2);
+            // the loads stay here, one group ahead: the group's sched_barrier below keeps them in
+            // this region (no opaque offset: its per-group address arithmetic cost 4 VALU)
+            lt_group_load<Nx::S0, 0, Nx::N>(Lp + dj, Lp + dj2, n1, n2);
         }
         float yk[C::N];
         lt_group_read<C::S0, 0, C::N>(yk, yl, y2);
