@@ -14,7 +14,7 @@ MAX_PAIRS = 256
 OBS_SELF, OBS_TASK, OBS_DIM = 358, 576, 934
 
 (BUF_ROOT_STATE, BUF_DOF_STATE, BUF_RB_STATE, BUF_CONTACT_FORCE, BUF_DOF_FORCE, BUF_DOF_TARGET, BUF_NUM_CONTACTS,
- BUF_DROPPED_CONTACTS, BUF_CONTACT_CACHE, BUF_INIT_ROOT_STATE) = range(10)
+ BUF_DROPPED_CONTACTS, BUF_CONTACT_CACHE, BUF_INIT_ROOT_STATE, BUF_PHYS_ORDER, BUF_PHYS_COST) = range(12)
 # StateInit (envs/state_init.py) -> he_imitation_params.state_init
 STATE_INIT = {"Default": 0, "Start": 1, "Random": 2, "Hybrid": 3}
 CACHE_WORDS, CACHE_KEYS, CACHE_LAMBDA = 104, 8, 40  # he_sim_params warm-start cache layout (row keys, impulses)

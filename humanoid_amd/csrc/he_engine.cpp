@@ -255,6 +255,8 @@ int he_get_buffer(he_engine* h, int kind, void** dptr, int64_t* shape, int* ndim
         case HE_BUF_DROPPED_CONTACTS: *dptr = h->dropped; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
         case HE_BUF_CONTACT_CACHE: *dptr = h->cache; *ndim = 2; shape[0] = N; shape[1] = HE_CACHE_WORDS; break;
         case HE_BUF_INIT_ROOT_STATE: *dptr = h->init_root; *ndim = 2; shape[0] = N; shape[1] = 13; break;
+        case HE_BUF_PHYS_ORDER: *dptr = h->order; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
+        case HE_BUF_PHYS_COST: *dptr = h->cost; *ndim = 1; shape[0] = N; *dtype = HE_DTYPE_I32; break;
         default: return fail("he_get_buffer: unknown buffer kind %d", kind);
     }
     return 0;

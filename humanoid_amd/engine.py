@@ -216,6 +216,17 @@ class Engine:
         Default / Hybrid state init resets to; writable."""
         return self.buffer(_abi.BUF_INIT_ROOT_STATE)
 
+    @property
+    def physics_order(self):
+        """i32 [N]: the physics launch's dispatch order (the env of each workgroup, expensive envs
+        first; diagnostics, DESIGN §4.1 "Dispatch order")."""
+        return self.buffer(_abi.BUF_PHYS_ORDER)
+
+    @property
+    def physics_cost(self):
+        """i32 [N]: each env's wave cycles in the last physics launch (the order's input)."""
+        return self.buffer(_abi.BUF_PHYS_COST)
+
     # ------------------------------------------------------------------ state writes
     def _contig(self, t, dtype=None):
         import torch

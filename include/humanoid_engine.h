@@ -173,7 +173,12 @@ typedef enum he_buf_kind {
                                   facade's prepare_sim writes the actors' own creation poses
                                   here when they differ; the Default / Hybrid state init resets
                                   to it */
-    HE_BUF_COUNT = 10
+    HE_BUF_PHYS_ORDER = 10,    /* i32 [N] the physics launch's dispatch order: the env of each workgroup,
+                                  expensive envs first (engine extension, read-only diagnostics;
+                                  rebuilt every HE_PHYS_ORDER launches, default 8) */
+    HE_BUF_PHYS_COST = 11,     /* i32 [N] each env's wave cycles in the last physics launch (the order's
+                                  input; read-only diagnostics) */
+    HE_BUF_COUNT = 12
 } he_buf_kind;
 
 #define HE_DTYPE_F32 1   /* GymTensor.h:23 eGymDataTypeFp32 */

@@ -71,6 +71,28 @@ def test_dispatch_order_leaves_the_step_unchanged(model):
         assert torch.equal(x, y), "the dispatch order must not change any env's step"
 
 
+def test_dispatch_order_is_a_heavy_first_stable_partition(model):
+    """configs[4], order rebuilt every 8 launches (the default): after 16 steps the order buffer is a
+    permutation of the envs; it lists first, in env order, exactly the envs whose cycle count in the
+    launch the order was built from was over mean + mean / 16, then the rest in env order (he_kernels.h
+    launch_physics_order). The order is rebuilt at launch 16, from launch 16's cycle counts, which the
+    cost buffer still holds."""
+    ro = _rollout("dr", model)
+    for _ in range(16):
+        ro.step()
+    torch.cuda.synchronize()
+    order = ro.eng.physics_order.cpu().numpy()
+    cost = ro.eng.physics_cost.cpu().numpy().view(np.uint32).astype(np.int64)
+    assert np.array_equal(np.sort(order), np.arange(4096))
+    tot = int(cost.sum())
+    thr = tot // 4096 + tot // (16 * 4096)
+    heavy = np.nonzero(cost > thr)[0]
+    light = np.nonzero(cost <= thr)[0]
+    assert 0 < len(heavy) < 4096 // 2, len(heavy)
+    assert np.array_equal(order[:len(heavy)], heavy)
+    assert np.array_equal(order[len(heavy):], light)
+
+
 def test_full_size_standstill_invariant(model):
     ro = _rollout("standstill", model)
     z0 = ro.eng.root_states[:, 2].clone()
