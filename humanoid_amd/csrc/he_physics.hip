@@ -439,16 +439,30 @@ HE_DEV float reduce_scatter(float (&v)[N]) {
 // Zh^T x into lane = dof (lane i: sum over rows r of z_r[i] x_r; lanes < 11 also dof 64 + lane in e2): the
 // same butterfly as reduce_scatter with the products formed as the first stage consumes them, so at
 // most 32 + 8 of them are live at once (the TGS iterations run it beside the rows' Zh and columns)
+// The products and the first two stages' sums run on the register pairs (v_pk_mul / v_pk_add: half the
+// VALU of the scalar forms, the same IEEE results)
 HE_DEV void reduce_scatter_z(const regla::ZVec& z, float x, int lane, float& e1, float& e2) {
+    using regla::f2v;
+    const f2v xx = f2v{x, x};
     float v[32];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        float a = ZV(z, j) * x, b = ZV(z, j + 32) * x;
-        swap32(a, b);
-        v[j] = a + b;
+    for (int j = 0; j < 32; j += 2) {
+        const f2v pa = z.p[j >> 1] * xx, pb = z.p[(j + 32) >> 1] * xx;
+        float a0 = pa.x, b0 = pb.x, a1 = pa.y, b1 = pb.y;
+        swap32(a0, b0);
+        swap32(a1, b1);
+        const f2v s = f2v{a0, a1} + f2v{b0, b1};
+        v[j] = s.x;
+        v[j + 1] = s.y;
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) { swap16(v[j], v[j + 16]); v[j] += v[j + 16]; }
+    for (int j = 0; j < 16; j += 2) {
+        swap16(v[j], v[j + 16]);
+        swap16(v[j + 1], v[j + 17]);
+        const f2v s = f2v{v[j], v[j + 1]} + f2v{v[j + 16], v[j + 17]};
+        v[j] = s.x;
+        v[j + 1] = s.y;
+    }
     rs_dpp<8, 0x140, 0xFF00FF00FF00FF00ull>(v);
     rs_dpp<4, 0x141, 0xF0F0F0F0F0F0F0F0ull>(v);
     rs_dpp<2, 0x4E, 0xCCCCCCCCCCCCCCCCull>(v);
