@@ -439,6 +439,24 @@ HE_DEV float reduce_scatter(float (&v)[N]) {
 // Zh^T x into lane = dof (lane i: sum over rows r of z_r[i] x_r; lanes < 11 also dof 64 + lane in e2): the
 // same butterfly as reduce_scatter with the products formed as the first stage consumes them, so at
 // most 32 + 8 of them are live at once (the TGS iterations run it beside the rows' Zh and columns)
+// zh_r . y with y_i broadcast from lane i (yl: dofs 0..63, y2: dofs 64..74 on lanes 0..10): the
+// readlanes in blocks of four SGPRs (one hazard nop per block), the products on the register pairs
+// (v_pk_fma: half the VALU), the four partial sums of the scalar form (dof i into sum i mod 4),
+// so the result is that form's to the bit
+HE_DEV float zdot_lanes(const regla::ZVec& z, float yl, float y2) {
+    using regla::f2v;
+    f2v a = f2v{0.f, 0.f}, b = f2v{0.f, 0.f};
+    regla::static_for<0, NG, 4>([&](auto ic) {
+        constexpr int i0 = decltype(ic)::value;
+        float sv[4];
+        if constexpr (i0 < 64) regla::rdlane4<i0>(yl, sv);
+        else regla::rdlane4<i0 - 64>(y2, sv);
+        a = __builtin_elementwise_fma(z.p[i0 >> 1], f2v{sv[0], sv[1]}, a);
+        if constexpr (i0 + 3 < NG) b = __builtin_elementwise_fma(z.p[(i0 >> 1) + 1], f2v{sv[2], sv[3]}, b);
+        else if constexpr (i0 + 2 < NG) b.x = fmaf(ZV(z, i0 + 2), sv[2], b.x);
+    });
+    return (a.x + a.y) + (b.x + b.y);
+}
 // The products and the first two stages' sums run on the register pairs (v_pk_mul / v_pk_add: half the
 // VALU of the scalar forms, the same IEEE results)
 HE_DEV void reduce_scatter_z(const regla::ZVec& z, float x, int lane, float& e1, float& e2) {
@@ -2147,7 +2165,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 }
             }
 #pragma unroll
-            for (int i = 0; i < NG; ++i) bacc[i & 3] = fmaf(ZV(z, i), L.u0[i], bacc[i & 3]);  // J_r u0
+            for (int k = 0; k < NG / 2; ++k) {  // J_r u0 on the register pairs (dof i into sum i mod 4)
+                const regla::f2v u = *reinterpret_cast<const regla::f2v*>(&L.u0[2 * k]);
+                regla::f2v acc = regla::f2v{bacc[(2 * k) & 3], bacc[(2 * k + 1) & 3]};
+                acc = __builtin_elementwise_fma(z.p[k], u, acc);
+                bacc[(2 * k) & 3] = acc.x;
+                bacc[(2 * k + 1) & 3] = acc.y;
+            }
+            bacc[(NG - 1) & 3] = fmaf(ZV(z, NG - 1), L.u0[NG - 1], bacc[(NG - 1) & 3]);
             brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
             if (act && kind == 0) {
                 const float g = L.cgap[rs_];
@@ -2165,24 +2190,20 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             scale_rows<0>(z, sdl, sdl2);
             float dacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < NG; ++i) dacc[i & 3] = fmaf(ZV(z, i), ZV(z, i), dacc[i & 3]);
+            for (int k = 0; k < NG / 2; ++k) {  // |zh_r|^2 on the register pairs (dof i into sum i mod 4)
+                regla::f2v acc = regla::f2v{dacc[(2 * k) & 3], dacc[(2 * k + 1) & 3]};
+                acc = __builtin_elementwise_fma(z.p[k], z.p[k], acc);
+                dacc[(2 * k) & 3] = acc.x;
+                dacc[(2 * k + 1) & 3] = acc.y;
+            }
+            dacc[(NG - 1) & 3] = fmaf(ZV(z, NG - 1), ZV(z, NG - 1), dacc[(NG - 1) & 3]);
             diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
             {  // J_r (uf - u0) = zh_r . yh, yh_i broadcast from lane i (v_readlane: no LDS loads to
                // hoist into registers at the phase's register peak), four lanes per block into four
                // SGPRs (one hazard nop per block; through one SGPR the 75 products serialised:
                // this phase -10 %, the launch -0.5 % by A/B, bit-identical, round 4)
                 const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
-                float yacc[4] = {0.f, 0.f, 0.f, 0.f};
-                regla::static_for<0, NG, 4>([&](auto ic) {
-                    constexpr int i0 = decltype(ic)::value;
-                    float sv[4];
-                    if constexpr (i0 < 64) regla::rdlane4<i0>(yhl, sv);
-                    else regla::rdlane4<i0 - 64>(yh2, sv);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (i0 + q < NG) yacc[(i0 + q) & 3] = fmaf(ZV(z, i0 + q), sv[q], yacc[(i0 + q) & 3]);
-                });
-                brow += (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
+                brow += zdot_lanes(z, yhl, yh2);
             }
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
@@ -2329,17 +2350,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     // the next sweep's start about lambda = applied + dl: w = J u + zh . yh + bias(sep) + A dl,
                     // with zh . yh + A dl = zh . (yh + Zh^T dl), one dot product
                     const float yhl = L.yh[lane] + e1, yh2 = lane < NH ? L.yh[64 + lane] + e2 : 0.f;
-                    float yacc[4] = {0.f, 0.f, 0.f, 0.f};
-                    regla::static_for<0, NG, 4>([&](auto ic) {
-                        constexpr int i0 = decltype(ic)::value;
-                        float sv[4];
-                        if constexpr (i0 < 64) regla::rdlane4<i0>(yhl, sv);
-                        else regla::rdlane4<i0 - 64>(yh2, sv);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            if (i0 + q < NG) yacc[(i0 + q) & 3] = fmaf(ZV(z, i0 + q < NG ? i0 + q : 0), sv[q], yacc[(i0 + q) & 3]);
-                    });
-                    const float zy = (yacc[0] + yacc[1]) + (yacc[2] + yacc[3]);
+                    const float zy = zdot_lanes(z, yhl, yh2);
                     bb = act && isn ? gbias(sep) : 0.f;
                     lamv = applied + dl;
                     cd = act ? -(v + zy + bb) * invd : 0.f;
