@@ -18,7 +18,8 @@ The GPU engine is then held to this oracle (tests/test_gpu_parity.py).
 
 These are the invariants of the PGS step (he_sim_params.solver_type 0, _abi.pgs_sim_params: 8
 velocity-level sweeps per physics step, the midpoint bias), rounds 1-4's default; the engine's default
-since round 5 is the reference's TGS (solver_type 1), whose invariants are tests/test_tgs.py.
+since round 5 is the reference's TGS (solver_type 1), whose own invariants are tests/test_tgs.py. The
+ballistic CoM, the dt refinement and the mu g deceleration run under both solvers here.
 """
 import numpy as np
 import pytest
@@ -31,8 +32,8 @@ import cases
 G = 9.81
 
 
-def _run(he_model, root, dof, targets, steps, substeps=2, **sim):
-    sp = _abi.pgs_sim_params(**sim)
+def _run(he_model, root, dof, targets, steps, substeps=2, solver="pgs", **sim):
+    sp = (_abi.pgs_sim_params if solver == "pgs" else _abi.default_sim_params)(**sim)
     r, d = root.copy(), dof.copy()
     cache = O.new_cache(r.shape[0])
     out = None
@@ -130,9 +131,11 @@ def test_free_flight_momentum_and_energy(he_model, model):
     assert dPg < 0.015 * P and dLg < 0.006 * L
 
 
-def test_com_follows_ballistic_parabola_under_drives(he_model, model):
+@pytest.mark.parametrize("solver", ["pgs", "tgs"])
+def test_com_follows_ballistic_parabola_under_drives(he_model, model, solver):
     """Actuated tumbling in the air (PD drives on, random targets): the internal torques cannot move
-    the centre of mass, which follows c0 + v0 t - g t^2/2 up to the integrator's O(dt) drift."""
+    the centre of mass, which follows c0 + v0 t - g t^2/2 up to the integrator's O(dt) drift (the PGS
+    step and TGS alike)."""
     rng = np.random.default_rng(2)
     n = 8
     root, dof = cases.random_state(n, rng, height=(4.0, 5.0), vel=0.5, ang=0.5)
@@ -142,8 +145,8 @@ def test_com_follows_ballistic_parabola_under_drives(he_model, model):
     errs = []
     for div in (1, 2):
         steps = 15 * div
-        r, d, out, sp = _run(he_model, root, dof, targets, steps, self_collision=0, angular_damping=0.0,
-                             dt=1.0 / 60.0 / div)
+        r, d, out, sp = _run(he_model, root, dof, targets, steps, solver=solver, self_collision=0,
+                             angular_damping=0.0, dt=1.0 / 60.0 / div)
         assert (out["num_contacts"] == 0).all()
         t = steps * 2 * sp.dt
         c = cases.center_of_mass(model, out["rb_state"])
@@ -153,16 +156,18 @@ def test_com_follows_ballistic_parabola_under_drives(he_model, model):
     assert 0.3 < errs[1] / errs[0] < 0.7, errs
 
 
-def test_dt_refinement_converges_first_order(he_model):
+@pytest.mark.parametrize("solver", ["pgs", "tgs"])
+def test_dt_refinement_converges_first_order(he_model, solver):
     """Random actuated airborne state for 0.5 s at dt, dt/2, dt/4: |x(dt) - x(dt/4)| / |x(dt/2) -
-    x(dt/4)| is 3 for a first-order method (joint angles and root position)."""
+    x(dt/4)| is 3 for a first-order method (joint angles and root position), the PGS step and TGS
+    alike."""
     rng = np.random.default_rng(3)
     n = 8
     root, dof = cases.random_state(n, rng, height=(3.0, 4.0), vel=0.5, ang=0.4)
     targets = rng.uniform(-0.5, 0.5, (n, 69)).astype(np.float32)
     res = {}
     for div in (1, 2, 4):
-        r, d, _, _ = _run(he_model, root, dof, targets, 15 * div, self_collision=0, dt=1.0 / 60.0 / div)
+        r, d, _, _ = _run(he_model, root, dof, targets, 15 * div, solver=solver, self_collision=0, dt=1.0 / 60.0 / div)
         res[div] = np.concatenate([r[:, :3], d[..., 0]], axis=1).astype(np.float64)
     e1 = np.linalg.norm(res[1] - res[4], axis=1)
     e2 = np.linalg.norm(res[2] - res[4], axis=1)
@@ -269,9 +274,11 @@ def test_saturated_random_actions_stay_physical(he_model, model):
     assert (vexp > 10.0).sum() > 8, vexp  # the explicit scheme's runaway in the same run
 
 
+@pytest.mark.parametrize("solver", ["pgs", "tgs"])
 @pytest.mark.parametrize("mu", [0.25, 0.5])
-def test_sliding_body_decelerates_at_mu_g(he_model, model, mu):
-    """Coulomb friction with patch friction rows: a lying body, settled, then given
+def test_sliding_body_decelerates_at_mu_g(he_model, model, mu, solver):
+    """Coulomb friction with patch friction rows, under the PGS step and under TGS (whose
+    friction bounds follow the accumulated normal impulses of the iterations): a lying body, settled, then given
     3 m/s along x (every body), slides on its contact patches and decelerates at mu g while it
     slides (the tangent basis of the plane's normal has t1 = x, so the pyramid bound is mu lambda_n
     along the motion). Median over 8 envs of the fitted deceleration within 5 % of mu g (an env
@@ -280,7 +287,7 @@ def test_sliding_body_decelerates_at_mu_g(he_model, model, mu):
     n = 8
     root, dof = cases.lying_state(n, rng, on_floor=True, model=model)
     tgt = dof[..., 0].copy()
-    sp = _abi.pgs_sim_params()
+    sp = _abi.pgs_sim_params() if solver == "pgs" else _abi.default_sim_params()
     cache = O.new_cache(n)
     for _ in range(45):  # settle 1.5 s
         O.physics_step(he_model, sp, root, dof, tgt, 2, cache=cache)
