@@ -185,9 +185,7 @@ __device__ __forceinline__ typename RowOf<K>::T row_if_live(const float* Lp, uin
     typename RowOf<K>::T r;
     if constexpr (K >= 1) {
         if (body_live<K>(lb)) {
-            int off = 0;
-            asm volatile("" : "+v"(off));
-            r = load_row_if<K>(Lp, off);
+            r = load_row_if<K>(Lp, 0);  // the callers' sched_barriers keep it where it is issued
         } else {
             undef_row(r);
         }
@@ -200,9 +198,9 @@ __device__ __forceinline__ typename RowOf<K>::T row_if_live(const float* Lp, uin
 template <int K, int K0>
 __device__ __forceinline__ void zbs_in_body(const float* Lp, ZVec& z, const typename RowOf<K>::T& rk) {
     if constexpr (K > K0 && K >= 1) {
-        int off = 0;
-        asm volatile("" : "+v"(off));
-        const typename RowOf<K - 1>::T nx = load_row_if<K - 1>(Lp, off);
+        // the next row's broadcast, issued before this row's updates; the sched_barrier after them
+        // keeps it here (no opaque offset: its address arithmetic cost 2 VALU per row)
+        const typename RowOf<K - 1>::T nx = load_row_if<K - 1>(Lp, 0);
         zbs_anc<K, 0, kDofNanc[K] - 1>(rk, z);
         __builtin_amdgcn_sched_barrier(0);
         zbs_in_body<K - 1, K0>(Lp, z, nx);
