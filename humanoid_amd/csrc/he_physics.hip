@@ -1407,9 +1407,9 @@ HE_DEV void integrate_bodies(Lds& L, const BodyTopo& T, int lane, const he_sim_p
     float w[3] = {src[d0] * damp, src[d0 + 1] * damp, src[d0 + 2] * damp};
     {
         // the joint's relative rate: PhysX articulation joint maxJointVelocity
-        const float nrm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        if (!root && nrm > p.max_joint_velocity) {
-            const float s = p.max_joint_velocity / nrm;
+        const float n2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];  // squared: the norm only where it acts
+        if (!root && n2 > p.max_joint_velocity * p.max_joint_velocity) {
+            const float s = p.max_joint_velocity / sqrtf(n2);
             w[0] *= s; w[1] *= s; w[2] *= s;
         }
         // the link's WORLD angular velocity (asset max_angular_velocity, PxRigidBody): w_b = w_parent +
@@ -1418,7 +1418,7 @@ HE_DEV void integrate_bodies(Lds& L, const BodyTopo& T, int lane, const he_sim_p
         // no link can be over when |w_root| + (joints on the longest chain) x max_j |u_j| stays under
         // the cap (triangle inequality; a 1 % margin covers the prefix's rounding): the prefix and
         // the clamp are then skipped (wave-uniform), with the result they would give
-        const float un = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        const float un = __builtin_amdgcn_sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);  // a skip test with a 1 % margin
         const float wroot = regla::rdlane(un, 0);
         const bool may = bl && !root && un * (float)(smpl::kNumBodyLevels - 1) > 0.99f * p.max_angular_velocity - wroot;
         if (__ballot(may) != 0ull) {
