@@ -1234,6 +1234,12 @@ HE_DEV void bias_midpoint(Lds& L, const BodyTopo& T, int lane, const he_sim_para
     STAMP(28);
 }
 
+// lane predicates of the TGS iterations' helpers as constant exec masks, rematerialised at each use
+// (regla::lanes: two s_mov): a v_cmp result would be hoisted out of the iterations into an SGPR pair
+// held through them, and the kernel runs out of SGPRs
+HE_DEV bool lanes_body() { return regla::lanes<(1ull << NB) - 1ull>(); }        // lane < NB
+HE_DEV bool lanes_hi() { return regla::lanes<(1ull << regla::NH) - 1ull>(); }   // lane < NH (dofs 64..74)
+HE_DEV bool lanes_joint_dof() { return regla::lanes<~0x3Full>(); }             // lane >= 6
 // ---------------------------------------------------------------------------------- TGS iterations
 // he_sim_params.solver_type 1 (oracle/he_oracle_physics.c substep_tgs): the velocity-dependent bias of
 // the next position iteration at the working velocity `vel` (L.u0), with the step's kinematics (S, V
@@ -1246,7 +1252,7 @@ HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params
     // in short phases through LDS (the body velocities V and joint velocities vj in the V / F words, dead
     // from the row set-up to the next kinematics), so that each phase's temporaries fit beside the
     // iterations' long-lived rows and columns
-    const bool bl = lane < NB;
+    const bool bl = lanes_body();
     const int b = bl ? lane : 0;
     const uint32_t jp = bl ? T.jump4[b] : 0xFFFFFFFFu;
     auto prefix6 = [&](float (&y)[6]) {
@@ -1316,7 +1322,7 @@ HE_DEV void tgs_bias_at(Lds& L, const BodyTopo& T, int lane, const he_sim_params
     __builtin_amdgcn_sched_barrier(0);
     subtree_levels<6, smpl::kNumBodyLevels - 2>(&L.Acc[0][0], nullptr, lane);
     c1 = dot6(L.S[lane], L.Acc[dof_body(lane)]);
-    c2 = lane < regla::NH ? dot6(L.S[64 + lane], L.Acc[(64 + lane - 6) / 3 + 1]) : 0.f;
+    c2 = lanes_hi() ? dot6(L.S[64 + lane], L.Acc[(64 + lane - 6) / 3 + 1]) : 0.f;
 }
 
 // the next position iteration's free motion: yh = D^-1/2 L^-T hs (kp (tgt - q) - c u - b) per dof (lane,
@@ -1331,12 +1337,12 @@ HE_DEV void tgs_rhs(Lds& L, const BodyTopo& T, int lane, float hs, float c1, flo
         return hs * (drive - b);
     };
     float y1 = rhs(lane, c1);
-    float y2 = lane < NH ? rhs(64 + lane, c2) : 0.f;
+    float y2 = lanes_hi() ? rhs(64 + lane, c2) : 0.f;
     __builtin_amdgcn_s_setprio(kPrioSerial);
-    regla::solve_LT_vec_pipelined(L.Lp, T.dof_depth[lane], lane < NH ? T.dof_depth[64 + lane] : 0, y1, y2);
+    regla::solve_LT_vec_pipelined(L.Lp, T.dof_depth[lane], lanes_hi() ? T.dof_depth[64 + lane] : 0, y1, y2);
     __builtin_amdgcn_s_setprio(kPrioDefault);
     L.yh[lane] = y1 * L.sDinv[lane];
-    if (lane < NH) L.yh[64 + lane] = y2 * L.sDinv[64 + lane];
+    if (lanes_hi()) L.yh[64 + lane] = y2 * L.sDinv[64 + lane];
     sync();
 }
 
@@ -1345,12 +1351,12 @@ HE_DEV void tgs_rhs(Lds& L, const BodyTopo& T, int lane, float hs, float c1, flo
 HE_DEV void tgs_velocity(Lds& L, const BodyTopo& T, int lane, float e1, float e2) {
     using regla::NH;
     float yl = (e1 + L.yh[lane]) * L.sDinv[lane];
-    float y2 = lane < NH ? (e2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
+    float y2 = lanes_hi() ? (e2 + L.yh[64 + lane]) * L.sDinv[64 + lane] : 0.f;
     __builtin_amdgcn_s_setprio(kPrioSerial);
-    regla::solve_L_streamed(L.Lp + T.pack_start[lane], L.Lp + T.pack_start[lane < NH ? 64 + lane : 0], yl, y2);
+    regla::solve_L_streamed(L.Lp + T.pack_start[lane], L.Lp + T.pack_start[lanes_hi() ? 64 + lane : 0], yl, y2);
     __builtin_amdgcn_s_setprio(kPrioDefault);
     L.u0[lane] += yl;
-    if (lane < NH) L.u0[64 + lane] += y2;
+    if (lanes_hi()) L.u0[64 + lane] += y2;
     sync();
 }
 
@@ -1361,8 +1367,8 @@ HE_DEV void tgs_drive_acc(const Lds& L, int lane, float& f1, float& f2) {
         const int d = i - 6;
         return L.dforce[d] * (L.tgt[d] - L.q[d]) - L.coef[i] * L.u0[i];
     };
-    if (lane >= 6) f1 += tq(lane >= 6 ? lane : 6);
-    if (lane < regla::NH) f2 += tq(64 + lane);
+    if (lanes_joint_dof()) f1 += tq(lane >= 6 ? lane : 6);
+    if (lanes_hi()) f2 += tq(64 + lane);
 }
 
 // ---------------------------------------------------------------------------------- fused imitation
@@ -1401,8 +1407,8 @@ HE_DEV void integrate_bodies(Lds& L, const BodyTopo& T, int lane, const he_sim_p
     // body: the root composes exp(dt w) (x) q, a ball joint log(exp(q) (x) exp(dt u)); both as
     // normalize(e1 (x) e2) with the operands selected, so the two cases share one code path
     f3 lim_th = f3{0.f, 0.f, 0.f}, lim_u = f3{0.f, 0.f, 0.f};  // the joint's new q and u
-    const bool bl = lane < NB;
-    const bool root = lane == 0;
+    const bool bl = lanes_body();
+    const bool root = regla::lanes<1ull>();
     const int d0 = root ? 0 : 6 + 3 * ((bl ? lane : 1) - 1);
     float w[3] = {src[d0] * damp, src[d0 + 1] * damp, src[d0 + 2] * damp};
     {
