@@ -1617,3 +1617,58 @@ void ho_momentum_energy(const he_model* m, const he_sim_params* p, int n, const 
         o[6] = ke; o[7] = pe;
     }
 }
+
+/* The step's dynamics terms for the independent pins (tests/test_independent_dynamics.py): the CRBA
+ * joint-space inertia H [N,75,75] (no armature) and the RNEA bias [N,75] (gravity + Coriolis /
+ * gyroscopic at the state's velocities), as dynamics_terms computes them for substep. */
+void ho_dynamics_terms(const he_model* m, const he_sim_params* p, int n, const float* root_states,
+                       const float* dof_state, double* H_out, double* bias_out) {
+    topo t;
+    build_topo(m, &t);
+    for (int e = 0; e < n; ++e) {
+        env_state s;
+        const float* rs = root_states + (size_t)e * 13;
+        for (int c = 0; c < 3; ++c) { s.root_pos[c] = rs[c]; s.root_v[c] = rs[7 + c]; s.root_w[c] = rs[10 + c]; }
+        for (int c = 0; c < 4; ++c) s.root_q[c] = rs[3 + c];
+        for (int d = 0; d < ND; ++d) { s.q[d] = dof_state[((size_t)e * ND + d) * 2]; s.u[d] = dof_state[((size_t)e * ND + d) * 2 + 1]; }
+        static __thread kin k;
+        static __thread R H[NG][NG];
+        sinertia I[NB];
+        R bias[NG];
+        dynamics_terms(m, &t, p, &s, NULL, &k, I, bias, H);
+        memcpy(H_out + (size_t)e * NG * NG, H, sizeof(R) * NG * NG);
+        memcpy(bias_out + (size_t)e * NG, bias, sizeof(R) * NG);
+    }
+}
+
+/* J^T of a contact row on body b at world point x along direction d (the terrain case of
+ * row_jacobian: rho = (x - o) x d over b's chain), per env: z [N,75] */
+void ho_point_jacobian(const he_model* m, int n, const float* root_states, const float* dof_state, const int* body,
+                       const double* x, const double* d, double* z_out) {
+    topo t;
+    build_topo(m, &t);
+    for (int e = 0; e < n; ++e) {
+        env_state s;
+        const float* rs = root_states + (size_t)e * 13;
+        for (int c = 0; c < 3; ++c) { s.root_pos[c] = rs[c]; s.root_v[c] = rs[7 + c]; s.root_w[c] = rs[10 + c]; }
+        for (int c = 0; c < 4; ++c) s.root_q[c] = rs[3 + c];
+        for (int q = 0; q < ND; ++q) { s.q[q] = dof_state[((size_t)e * ND + q) * 2]; s.u[q] = dof_state[((size_t)e * ND + q) * 2 + 1]; }
+        kin k;
+        kinematics(m, &t, &s, &k);
+        srow w;
+        memset(&w, 0, sizeof(w));
+        w.b0 = body[e];
+        w.b1 = -1;
+        const R r[3] = {x[3 * e] - k.o[0], x[3 * e + 1] - k.o[1], x[3 * e + 2] - k.o[2]};
+        for (int c = 0; c < 3; ++c) w.dir[c] = d[3 * e + c];
+        cross3(r, w.dir, w.rho);
+        contact cdummy;
+        memset(&cdummy, 0, sizeof(cdummy));
+        row_jacobian(&t, &k, &w, &cdummy, z_out + (size_t)e * NG);
+    }
+}
+
+/* J_r^-1(th) [3x3] row by row as the limit rows use it (jr_inv_row), for the independent pin */
+void ho_jr_inv(const double* th, double* out) {
+    for (int c = 0; c < 3; ++c) jr_inv_row(th, c, out + 3 * c);
+}

@@ -227,6 +227,35 @@ def momentum_energy(model, sim, root_states, dof_state):
     return out
 
 
+def dynamics_terms(model, sim, root_states, dof_state):
+    """The oracle's joint-space inertia H [N,75,75] (CRBA, no armature) and bias [N,75] (RNEA: gravity,
+    Coriolis / gyroscopic) at the given states, as its physics step forms them."""
+    n = root_states.shape[0]
+    H = np.zeros((n, 75, 75), np.float64)
+    bias = np.zeros((n, 75), np.float64)
+    lib().ho_dynamics_terms(C.byref(model), C.byref(sim), C.c_int(n), _p(f32(root_states)), _p(f32(dof_state)),
+                            _p(H), _p(bias))
+    return H, bias
+
+
+def point_jacobian(model, root_states, dof_state, body, x, d):
+    """J^T [N,75] of a terrain contact row on body[e] at world point x[e] along d[e] (row_jacobian)."""
+    n = root_states.shape[0]
+    z = np.zeros((n, 75), np.float64)
+    lib().ho_point_jacobian(C.byref(model), C.c_int(n), _p(f32(root_states)), _p(f32(dof_state)),
+                            _p(np.ascontiguousarray(body, np.int32)), _p(np.ascontiguousarray(x, np.float64)),
+                            _p(np.ascontiguousarray(d, np.float64)), _p(z))
+    return z
+
+
+def jr_inv(th):
+    """The inverse right Jacobian of SO(3) at rotation vector th [3] (the joint-limit rows' map from a
+    ball joint's child-frame rate to its exp-map coordinate rates)."""
+    out = np.zeros((3, 3), np.float64)
+    lib().ho_jr_inv(_p(np.ascontiguousarray(th, np.float64)), _p(out))
+    return out
+
+
 def imitation_from_ref(params, pos, rot, vel, ang, rpos, rrot, rvel, rang, progress, pass_time):
     n = pos.shape[0]
     out = dict(rew=np.zeros(n, np.float32), reward_raw=np.zeros((n, 4), np.float32), reset=np.zeros(n, np.uint8),
