@@ -86,10 +86,21 @@ template <uint64_t C>
 __device__ __forceinline__ bool lanes() {
     // the constant is materialised here by two s_mov_b32 (volatile: never hoisted out of the
     // substep loop, where dozens of distinct masks would otherwise be kept live and spilled)
-    uint32_t lo, hi;
-    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)C));
-    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(C >> 32)));
-    return __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hi << 32) | lo);
+#ifndef HE_LANES_B64
+#define HE_LANES_B64 1
+#endif
+    if constexpr (HE_LANES_B64 && C < 0x80000000ull) {
+        // lanes < 31 only: one s_mov_b64 of a non-negative 32-bit constant (a 64-bit SALU move
+        // zero-extends its 32-bit literal, so a mask with lanes >= 32 set needs the pair)
+        uint64_t m;
+        asm volatile("s_mov_b64 %0, %1" : "=s"(m) : "i"((int32_t)(uint32_t)C));
+        return __builtin_amdgcn_inverse_ballot_w64(m);
+    } else {
+        uint32_t lo, hi;
+        asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)C));
+        asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(C >> 32)));
+        return __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hi << 32) | lo);
+    }
 }
 
 // z -= a * b as an ordered instruction: the DAG linearisation would otherwise sink the whole
