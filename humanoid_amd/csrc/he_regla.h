@@ -89,7 +89,19 @@ __device__ __forceinline__ bool lanes() {
 #ifndef HE_LANES_B64
 #define HE_LANES_B64 1
 #endif
-    if constexpr (HE_LANES_B64 && C < 0x80000000ull) {
+#ifndef HE_LANES_BFM
+#define HE_LANES_BFM 1
+#endif
+    constexpr int kOff = C == 0 ? 0 : __builtin_ctzll(C);
+    constexpr int kLen = C == 0 ? 0 : 64 - __builtin_clzll(C) - kOff;
+    constexpr bool kRun = C != 0 && kLen < 64 && C == (((1ull << kLen) - 1ull) << kOff);
+    if constexpr (HE_LANES_BFM && kRun) {
+        // a run of lanes (descendant sets are runs in the DFS dof order): one s_bfm_b64 of two
+        // inline constants, ((1 << len) - 1) << off
+        uint64_t m;
+        asm volatile("s_bfm_b64 %0, %1, %2" : "=s"(m) : "i"(kLen), "i"(kOff));
+        return __builtin_amdgcn_inverse_ballot_w64(m);
+    } else if constexpr (HE_LANES_B64 && C < 0x80000000ull) {
         // lanes < 31 only: one s_mov_b64 of a non-negative 32-bit constant (a 64-bit SALU move
         // zero-extends its 32-bit literal, so a mask with lanes >= 32 set needs the pair)
         uint64_t m;
