@@ -689,9 +689,10 @@ int he_env_step(he_engine* h, const he_imitation_params* p, const he_env_motion*
     PhysArgs pa = phys_args(h, num_simulate, actions);
     pa.fused = 1;
     pa.im = a;
-    pa.order = nullptr;  // one round of waves (auto): the dispatch order does not matter
-    pa.cost = nullptr;
-    HE_CHECK(launch_physics(pa, (hipStream_t)stream));
+    // with the heavy-first dispatch order as the two-launch form (the epilogue indexes the ordered
+    // env): bit-identical to the unordered launch; at 4096 envs configs[4] 5 % faster, configs[1] / [2]
+    // within 0.3 % (profiles/r05/ab_fused_order.txt)
+    if (physics_and_order(h, pa, (hipStream_t)stream)) return 1;
     HE_CHECK(amp_after(h, a, 1, (hipStream_t)stream));
     return 0;
 }

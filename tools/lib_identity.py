@@ -1,5 +1,5 @@
 """Bit-identity of two engine builds (e.g. a scheduler-flag variant): the bench rollout for 20 steps
-with each library in its own process, states compared. Usage: python tools/lib_identity.py LIB_A LIB_B [--lying]"""
+with each library in its own process, states compared. Usage: python tools/lib_identity.py LIB_A LIB_B [--lying | --fused]"""
 import os
 import subprocess
 import sys
@@ -9,7 +9,7 @@ import argparse, sys, numpy as np, torch
 sys.path.insert(0, '.')
 import bench
 from humanoid_amd.model import load_default_model
-args = argparse.Namespace(config='imitation', num_envs=4096, clips=128, seed=0, max_contacts=40)
+args = argparse.Namespace(config='imitation', num_envs=4096, clips=128, seed=0, max_contacts=40, fused=len(sys.argv) > 2)
 ro = bench.Rollout(args, load_default_model(), 0, 0)
 for _ in range(20):
     ro.tracking_actions(); ro.step()
@@ -54,7 +54,8 @@ def main():
     for k, lib in enumerate(libs[:2]):
         out = f"gpurun_out/ident_{k}.npz"
         env = dict(os.environ, HE_ENGINE_LIB=os.path.abspath(lib))
-        subprocess.run([sys.executable, "-c", CODE_LYING if lying else CODE, out], check=True, env=env, timeout=300)
+        extra = ["fused"] if "--fused" in sys.argv else []  # the rollout as the one-launch env step
+        subprocess.run([sys.executable, "-c", CODE_LYING if lying else CODE, out] + extra, check=True, env=env, timeout=300)
         outs.append(out)
     import numpy as np
     a, b = np.load(outs[0]), np.load(outs[1])
