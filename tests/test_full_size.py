@@ -4,6 +4,7 @@ stand-still invariant of configs[1], and oracle parity on a random sample of env
 full-size run (one policy step from the GPU's own state, fp64 C oracle, the physics tolerances of
 test_gpu_parity)."""
 import argparse
+import json
 import os
 import sys
 
@@ -190,6 +191,36 @@ def _tiered_close(name, g, o, probes, atol, tiers, where=None):
                               "first_event_step": int(where[2][e]), "dev": float(dev[e, j]), "sens": float(sens[e, j])}
 
 
+# HE_PARITY_DUMP=1: every env whose post-event ratio passes POST_K is written out step by step
+# (HE_RECORD_DIR/divergent_<env>.json: distances, the probes' floors, stick / slip states)
+DUMP = bool(os.environ.get("HE_PARITY_DUMP"))
+
+
+def _dump_divergent(model, idx, first, first_set, first_slip, post_env, hist, trace):
+    d = os.environ.get("HE_RECORD_DIR") or "."
+    fmt = lambda st: [[int(k), int(v)] for k, v in st]  # noqa: E731
+    for e in np.nonzero(post_env > POST_K)[0]:
+        steps = []
+        for s_, (qg, rbg, qo, rbo, qps, rbps) in enumerate(hist):
+            cg_ = cases.center_of_mass(model, rbg[e:e + 1])[0]
+            co_ = cases.center_of_mass(model, rbo[e:e + 1])[0]
+            cps = [cases.center_of_mass(model, r[e:e + 1])[0] for r in rbps]
+            t = trace[s_]
+            steps.append({"step": s_,
+                          "l2_gpu": float(np.linalg.norm(qg[e].astype(np.float64) - qo[e])),
+                          "com_gpu": float(np.abs(cg_ - co_).max()),
+                          "l2_probes": [float(np.linalg.norm(q[e].astype(np.float64) - qo[e])) for q in qps],
+                          "com_probes": [float(np.abs(c - co_).max()) for c in cps],
+                          "com_oracle": [float(x) for x in co_],
+                          "slip_gpu": fmt(t["gpu"][e]), "slip_oracle": fmt(t["oracle"][e]),
+                          "slip_probes_differ": [int(p[e] != t["oracle"][e]) for p in t["probes"]],
+                          "keys_equal": bool(t["keys_gpu"][e] == t["keys_oracle"][e])})
+        rec = {"env": int(idx[e]), "first_event": int(first[e]), "first_set": int(first_set[e]),
+               "first_slip": int(first_slip[e]), "post_event_max_ratio": float(post_env[e]), "steps": steps}
+        with open(os.path.join(d, f"divergent_{int(idx[e])}.json"), "w") as f:
+            json.dump(rec, f, indent=1)
+
+
 def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
     """STEPS policy steps of the full-size rollout `ro` (advance(step) launches the physics of all 4096
     envs and returns the sampled envs' PD targets) against the fp64 oracle on the sample `idx`: its own
@@ -212,6 +243,7 @@ def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
     first_set = np.full(n, STEPS)
     first_slip = np.full(n, STEPS)
     hist = []
+    trace = []
     for step in range(STEPS):
         tgt = advance(step)
         rw = np.zeros((n, _abi.MAX_ROWS), np.float32)  # the oracle's row bound weights (torsion stick / slip)
@@ -226,8 +258,14 @@ def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
         cg = ro.eng.contact_cache.cpu().numpy()[idx]
         tw = torsion_weights(rw, c_o)
         first_set[np.array([a != b for a, b in zip(contact_keys(cg), contact_keys(c_o))]) & (first_set == STEPS)] = step
-        slip = np.array([a != b for a, b in zip(friction_states(cg, mu, tw), friction_states(c_o, mu, tw))])
+        fs_o = friction_states(c_o, mu, tw)
+        fs_g = friction_states(cg, mu, tw)
+        slip = np.array([a != b for a, b in zip(fs_g, fs_o)])
         first_slip[slip & (first_slip == STEPS)] = step
+        if DUMP:  # diagnostics: the stick / slip states of GPU, oracle and every probe, per env
+            fs_p = [friction_states(pr[2], mu, tw) for pr in probes]
+            trace.append({"gpu": fs_g, "oracle": fs_o, "probes": fs_p,
+                          "keys_gpu": contact_keys(cg), "keys_oracle": contact_keys(c_o)})
         hist.append((ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx, :, 0].copy(),
                      ro.eng.rb_state.view(4096, 24, 13).cpu().numpy()[idx].copy(), dof[..., 0].copy(),
                      out["rb_state"].copy(), [p[1][..., 0].copy() for p in probes],
@@ -272,6 +310,8 @@ def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
             post_c.append(rc)
             post_env[post] = np.maximum(post_env[post], np.maximum(rq, rc))
     l2_all, com_all = np.stack(l2_all), np.stack(com_all)
+    if DUMP:
+        _dump_divergent(model, idx, first, first_set, first_slip, post_env, hist, trace)
     cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0)  # noqa: E731
     pre_l2, pre_com, post_q, post_c = cat(pre_l2), cat(pre_com), cat(post_q), cat(post_c)
     adj_q, adj_c = cat(adj_q), cat(adj_c)
@@ -365,6 +405,13 @@ PRE_BEYOND4_FRAC = 1e-4
 POST_K = 6.0
 
 
+def _sample_seeds(base):
+    """The samples' seeds: the two of the suite, plus more when HE_PARITY_SAMPLES asks for them (a
+    wider record, e.g. tools/gpu_full_size_parity.sh with HE_PARITY_SAMPLES=8; the same bounds)."""
+    n = int(os.environ.get("HE_PARITY_SAMPLES", "2"))
+    return tuple(base) + tuple(1000 + 17 * k + base[0] for k in range(max(0, n - len(base))))
+
+
 def _assert_parity(rec, max_set, max_slip):
     t = rec["pre_event_elements"]
     assert t["beyond_8"] == 0, t
@@ -398,7 +445,7 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     recs = []
     one_stats = {"env_steps": 0, "contact_set_differences": 0, "max_abs_dof_pos_rad": 0.0, "max_abs_com_m": 0.0}
     st1 = CondStats()
-    for sample in (12, 15):
+    for sample in _sample_seeds((12, 15)):
         idx = np.sort(np.random.default_rng(sample).choice(4096, 48, replace=False))
         props = _props(ro, idx)
 
@@ -456,7 +503,8 @@ def test_full_size_tracking_parity_30_steps(model, he_model):
     _, sc = pd_action_offset_scale(model)
     inv_scale = torch.as_tensor(1.0 / np.asarray(sc, np.float32), device=ro.eng.device)
     recs = []
-    for sample in (13, 14):
+    seeds = _sample_seeds((13, 14))
+    for sample in seeds:
         idx = np.sort(np.random.default_rng(sample).choice(4096, 48, replace=False))
         t0 = ro.prog.float() * ro.p.control_dt + ro.st + ro.so
 
@@ -468,9 +516,9 @@ def test_full_size_tracking_parity_30_steps(model, he_model):
 
         recs.append(_trajectory_parity(model, he_model, ro, idx, advance, {}, sp, seed=321 + sample))
     rec = _merge(recs)
-    rec["workload"] = ("configs[2] tracking actions, 2 x 48 of 4096 envs, 30 policy steps of physics (4 physics "
-                       "steps of 4 TGS position iterations each) after 5 bench steps, fp32 engine vs fp64 oracle "
-                       "from one start state")
+    rec["workload"] = (f"configs[2] tracking actions, {len(seeds)} x 48 of 4096 envs, 30 policy steps of physics "
+                       "(4 physics steps of 4 TGS position iterations each) after 5 bench steps, fp32 engine vs fp64 "
+                       "oracle from one start state")
     print("tracking parity:", {k: v for k, v in rec.items() if k not in ("env_ids", "events", "definition")})
     _record("parity_configs2", rec)
     _assert_parity(rec, max_set=0.25, max_slip=0.6)
