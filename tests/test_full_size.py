@@ -164,7 +164,7 @@ def _record(name, obj):
 
 
 STEPS = 30
-NPROBES = 8
+NPROBES = int(os.environ.get("HE_PARITY_PROBES", "8"))
 
 
 def _tiered_close(name, g, o, probes, atol, tiers, where=None):
