@@ -243,6 +243,107 @@ class Rollout:
         self.eng.set_fused_step(self.fused)
 
 
+def _pmc_entry(name, key):
+    """The committed rocprofv3 counter record `profiles/<name>` for workload key `config:num_envs`."""
+    f = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(f)).get(key) if os.path.exists(f) else None
+    except Exception:
+        return None
+
+
+def kernel_figures(args, config, n, phys_ms, imit_ms, rows_mean):
+    """The physics kernel's roofline entry and the imitation kernel's HBM entry for one workload:
+    launch medians (HIP events) against SURVEY §8(d)'s canonical counts, with the committed PMC
+    counter records of the same workload key (pmc_traffic.json, pmc_mfma.json) beside them."""
+    key = f"{config}:{n}"
+    tr, mf = _pmc_entry("pmc_traffic.json", key), _pmc_entry("pmc_mfma.json", key)
+    traffic = tr.get("physics_bytes_per_launch") if tr else None
+    imit_traffic = tr.get("imitation_bytes_per_launch") if tr else None
+    mfma = None
+    if mf:
+        mfma = {"util": mf["mfma_util"], "valu_issue_frac": mf["valu_issue_frac"],
+                "source": "profiles/pmc_mfma.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / "
+                          "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
+    phys_flop = PHYS_FLOP_PER_SUBSTEP * 2 * sim_substeps(args)  # per env-step: 2 simulate() x substeps
+    phys_tflops = phys_flop * n / (phys_ms * 1e-3) / 1e12
+    imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
+    # the physics kernel alone (the unfused launch): latency-bound, priced against the FP32 vector /
+    # matrix peak with the canonical dense-equivalent flop count; mfma_util is the measured
+    # matrix-core busy share (rocprofv3 SQ counters)
+    phys = {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
+            "kernel": f"{'physics_kernel_tgs' if scheme_params(args).get('solver_type', 1) == 1 else 'physics_kernel'} "
+                      f"(fp32 VALU + MFMA; SURVEY §8d canonical 0.6546 MFLOP per physics step "
+                      f"x {2 * sim_substeps(args)} physics steps per env-step)",
+            "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma,
+            # SURVEY §8d: "report n_c as measured" -- the same count with the measured mean solver
+            # rows as m (patch friction: a standing body 28 rows, not 3 x 16 slots)
+            "at_measured_rows": canonical_at_rows(rows_mean, 2 * sim_substeps(args), n, phys_ms)}
+    imit = {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(imit_gbs / HBM_PEAK_GBS, 5),
+            "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic,
+            # the bytes that reached HBM (PMC FETCH_SIZE + WRITE_SIZE per launch, profiles/pmc_traffic.json)
+            # over the same launch time: with one clip (configs[1]) most motion reads hit the caches, so
+            # this is well under the algorithmic figure above
+            "hbm_frac_counter": (round(imit_traffic / (imit_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                 if imit_traffic else None)}
+    return phys, imit
+
+
+def kernel_pass(ro, steps, before=None):
+    """`steps` further steps (untimed, the same workload continuing) with HIP events around the
+    launches of EVERY step, on the engine's stream (torch's current stream): per step the first
+    launch (physics), the second (imitation) and the whole step, in ms. `before`: called ahead of
+    each step, outside the events (the tracking leg's action launch)."""
+    import torch
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(steps)]
+    for e in ev:
+        if before is not None:
+            before()
+        ro.step(e)
+    torch.cuda.synchronize()
+    return (np.array([e[0].elapsed_time(e[1]) for e in ev]), np.array([e[1].elapsed_time(e[2]) for e in ev]),
+            np.array([e[0].elapsed_time(e[2]) for e in ev]))
+
+
+def solver_rows(ro):
+    """Solver rows of each env's last solve: word 7 of the warm-start cache (include/humanoid_engine.h)."""
+    import torch
+    return ro.eng.contact_cache[:, 7].contiguous().view(torch.int32).cpu().numpy()
+
+
+def config_leg(args, model, device_index, config, steps=50, warmup=10):
+    """Another BASELINE config on this rank's GPU, the bench's own form (two launches per step): the
+    rate over `steps` timed steps, then the kernel figures from a pass of EV_STEPS steps with events.
+    configs[4] ("dr"): mass / friction randomisation + 3 terrains, the divergent-contact stress config."""
+    import torch
+    a = argparse.Namespace(**vars(args))
+    a.config = config
+    a.fused = False
+    ro = Rollout(a, model, device_index, 0)
+    for _ in range(warmup):
+        ro.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ro.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    first, second, _ = kernel_pass(ro, EV_STEPS)
+    rows = solver_rows(ro)
+    phys, imit = kernel_figures(a, config, a.num_envs, float(np.median(first)), float(np.median(second)),
+                                float(rows.mean()))
+    nc = ro.eng.num_contacts.cpu().numpy()
+    return {"value": round(a.num_envs * steps / dt, 1), "unit": "env-steps/s", "steps": steps, "warmup": warmup,
+            "workload": {"standstill": "configs[1]", "imitation": "configs[2]",
+                         "dr": "configs[4]: 4096 envs, per-env mass scale U(0.8,1.2), friction U(0.5,1.25), terrain "
+                               "by env % 3 (plane / 10 deg slope / steps), actions = 0"}[config],
+            "physics_kernel": phys, "imitation_kernel": imit,
+            "contacts": {"slots_mean": round(float(nc.mean()), 3), "rows_mean": round(float(rows.mean()), 2),
+                         "rows_max": int(rows.max())}}
+
+
 def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
     """configs[2] with the tracking action stream: 4096 envs over 128 clips,
     actions = clip(ref_dof_pos / scale) computed on the device every step inside the timed region;
@@ -250,6 +351,7 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
     import torch
     a = argparse.Namespace(**vars(args))
     a.config = "imitation"
+    a.fused = False
     ro = Rollout(a, model, device_index, 0)
     for _ in range(warmup):
         ro.tracking_actions()
@@ -261,6 +363,9 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
         ro.step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    first, second, _ = kernel_pass(ro, EV_STEPS, before=ro.tracking_actions)
+    phys, imit = kernel_figures(a, "imitation", a.num_envs, float(np.median(first)), float(np.median(second)),
+                                float(solver_rows(ro).mean()))
     l2 = []
     for _ in range(l2_steps):
         ro.tracking_actions()
@@ -270,6 +375,7 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
     return {"value": round(a.num_envs * steps / dt, 1), "unit": "env-steps/s", "steps": steps,
             "workload": "configs[2]: 4096 envs over 128 synthetic clips, actions = clip(ref_dof_pos / scale) "
                         "computed on the device each step (inside the timed region)",
+            "physics_kernel": phys, "imitation_kernel": imit,
             "joint_pose_l2_rad": {"mean": round(float(l2.mean()), 5), "p90": round(float(np.percentile(l2, 90)), 5),
                                   "steps": l2_steps,
                                   "definition": "||q - q_ref(t)||_2 over the 69 exp-map dofs per env, mean over envs x "
@@ -336,6 +442,7 @@ def learner_leg(args, model, device_index):
     n = args.num_envs
     a = argparse.Namespace(**vars(args))
     a.config = "imitation"
+    a.fused = False
     clips = make_clips(a, model)
     pe = PHCPufferEnv(EnvConfig(num_envs=n, motion_file={f"clip{i}": c for i, c in enumerate(clips)},
                                 seed=hd.rank_seed(1, rank)))
@@ -556,19 +663,10 @@ def main():
     elapsed = time.perf_counter() - t0
     nc = ro.eng.num_contacts.cpu().numpy()
     dropped = ro.eng.dropped_contacts.cpu().numpy()
-    # solver rows of each env's last solve: word 7 of the warm-start cache (include/humanoid_engine.h)
-    rows = ro.eng.contact_cache[:, 7].contiguous().view(torch.int32).cpu().numpy()
-    # kernel durations: a pass of EV_STEPS further steps (untimed, the same workload continuing) with
-    # HIP events around the launches of EVERY step, on the engine's stream (torch's current stream);
-    # the medians are the per-launch figures (compare the rocprofv3 averages of the same command)
-    def kernel_pass(steps):
-        ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(steps)]
-        for e in ev:
-            ro.step(e)
-        torch.cuda.synchronize()
-        return (np.array([e[0].elapsed_time(e[1]) for e in ev]), np.array([e[1].elapsed_time(e[2]) for e in ev]),
-                np.array([e[0].elapsed_time(e[2]) for e in ev]))
-    first, second, whole = kernel_pass(EV_STEPS)
+    rows = solver_rows(ro)
+    # kernel durations: a pass of EV_STEPS further steps with HIP events around every launch; the
+    # medians are the per-launch figures (compare the rocprofv3 averages of the same command)
+    first, second, whole = kernel_pass(ro, EV_STEPS)
     step_ms = float(np.median(whole))
     phys_ms, imit_ms = float(np.median(first)), float(np.median(second))
     kernel_samples = {"steps": EV_STEPS, "statistic": "median", "first_launch_ms": {
@@ -578,7 +676,7 @@ def main():
     split = None
     if ro.fused:
         ro.set_fused(False)
-        a1, a2, _ = kernel_pass(EV_STEPS // 2)
+        a1, a2, _ = kernel_pass(ro, EV_STEPS // 2)
         split = (float(np.median(a1)), float(np.median(a2)))
         ro.set_fused(True)
     # the headline's max-over-ranks time is settled before any optional leg runs a collective: a leg
@@ -609,43 +707,10 @@ def main():
         if split is not None:  # fused: the one launch is the dominant kernel
             fused_ms = step_ms
             phys_ms, imit_ms = split
-        phys_flop = PHYS_FLOP_PER_SUBSTEP * 2 * sim_substeps(args)  # per env-step: 2 simulate() x substeps
-        phys_tflops = phys_flop * n / (phys_ms * 1e-3) / 1e12
-        imit_gbs = IMIT_BYTES_PER_ENV_STEP * n / (imit_ms * 1e-3) / 1e9
-        traffic = imit_traffic = mfma = None
-        mfile = os.path.join(ROOT, "profiles", "pmc_mfma.json")  # rocprofv3 SQ counters of the bench
-        if os.path.exists(mfile):
-            try:
-                e = json.load(open(mfile)).get(f"{args.config}:{n}")
-                if e:
-                    mfma = {"util": e["mfma_util"], "valu_issue_frac": e["valu_issue_frac"],
-                            "source": "profiles/pmc_mfma.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / "
-                                      "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
-            except Exception:
-                mfma = None
-        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tfile):
-            try:
-                tr = json.load(open(tfile))
-                key = f"{args.config}:{n}"
-                if key in tr:
-                    traffic = tr[key].get("physics_bytes_per_launch")
-                    imit_traffic = tr[key].get("imitation_bytes_per_launch")
-            except Exception:
-                traffic = imit_traffic = None
-        # the physics kernel alone (the unfused launch): latency-bound, priced against the FP32
-        # vector / matrix peak with the canonical dense-equivalent flop count; mfma_util is the
-        # measured matrix-core busy share (rocprofv3 SQ counters)
-        phys_roof = {"bound": "latency", "achieved": round(phys_tflops, 4), "peak": FP32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(phys_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                     "kernel": f"{'physics_kernel_tgs' if scheme_params(args).get('solver_type', 1) == 1 else 'physics_kernel'} "
-                               f"(fp32 VALU + MFMA; SURVEY §8d canonical 0.6546 MFLOP per physics step "
-                               f"x {2 * sim_substeps(args)} physics steps per env-step)",
-                     "avg_launch_ms": round(phys_ms, 4), "mfma_util": mfma,
-                     # "report n_c as measured" -- the same count with the measured mean
-                     # solver rows as m (patch friction: a standing body 28 rows, not 3 x 16 slots)
-                     "at_measured_rows": canonical_at_rows(float(rows.mean()), 2 * sim_substeps(args), n, phys_ms)}
+        phys_roof, imit_roof = kernel_figures(args, args.config, n, phys_ms, imit_ms, float(rows.mean()))
+        traffic, mfma = phys_roof["traffic"], phys_roof["mfma_util"]
         if split is not None:  # the fused launch (physics + the imitation epilogue) is the dominant kernel
+            phys_flop = PHYS_FLOP_PER_SUBSTEP * 2 * sim_substeps(args)
             f_tflops = (phys_flop + IMIT_FLOP_PER_ENV_STEP) * n / (fused_ms * 1e-3) / 1e12
             roof = {"bound": "latency", "achieved": round(f_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(f_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
@@ -682,17 +747,7 @@ def main():
             "contacts": {"slots_mean": round(float(nc.mean()), 3), "slots_max": int(nc.max()),
                          "capacity": args.max_contacts, "envs_dropping": int((dropped > 0).sum()),
                          "dropped_mean": round(float(dropped.mean()), 4)},
-            "unfused_kernels": {
-                "physics_kernel": phys_roof,
-                "imitation_kernel": {"bound": "hbm", "achieved": round(imit_gbs, 1), "peak": HBM_PEAK_GBS,
-                                     "unit": "GB/s", "frac": round(imit_gbs / HBM_PEAK_GBS, 5),
-                                     "avg_launch_ms": round(imit_ms, 4), "traffic": imit_traffic,
-                                     # the bytes that reached HBM (PMC FETCH_SIZE + WRITE_SIZE per launch,
-                                     # profiles/pmc_traffic.json) over the same launch time: with one clip
-                                     # (configs[1]) most motion reads hit the caches, so this is well under
-                                     # the algorithmic figure above
-                                     "hbm_frac_counter": (round(imit_traffic / (imit_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-                                                          if imit_traffic else None)}},
+            "unfused_kernels": {"physics_kernel": phys_roof, "imitation_kernel": imit_roof},
         }
         if not args.no_tracking and world == 1 and args.scheme == "default":
             try:
@@ -709,6 +764,11 @@ def main():
                 line["tracking_configs2"] = tracking_leg(args, model, local)
             except Exception as exc:  # report, never fake
                 line["tracking_configs2"] = {"value": None, "error": repr(exc)}
+        if not args.no_tracking and world == 1 and args.num_envs == 4096 and args.config == "standstill":
+            try:
+                line["dr_configs4"] = config_leg(args, model, local, "dr")
+            except Exception as exc:  # report, never fake
+                line["dr_configs4"] = {"value": None, "error": repr(exc)}
         if learner is not None:
             line["learner_configs3"] = learner
         if not args.no_puffer_level and world == 1:

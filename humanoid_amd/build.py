@@ -47,6 +47,9 @@ def _mtime(p):
 # kernels whose occupancy (waves per SIMD, the compiler's resource report) the build enforces: the
 # physics kernel is one wave per env and latency-bound, and at one wave per SIMD it runs ~40 % slower
 MIN_OCCUPANCY = {"he_physics.hip": ("physics_kernel", 2)}
+# how many kernels of the TU match the watched name (physics_kernel and physics_kernel_tgs): a report
+# that lists fewer fails the build, so neither can drop out of the check unnoticed
+MIN_KERNELS = {"he_physics.hip": 2}
 
 
 def _check_occupancy(src, stderr):
@@ -60,16 +63,25 @@ def _check_occupancy(src, stderr):
     seen = 0
     for i, ln in enumerate(lines):
         if "Function Name:" in ln and name in ln:
-            for ln2 in lines[i + 1:i + 16]:
+            fn = ln.split("Function Name:")[1].split()[0]
+            # every watched kernel must report its occupancy before the next function's report starts
+            occ = None
+            for ln2 in lines[i + 1:]:
+                if "Function Name:" in ln2:
+                    break
                 m = re.search(r"Occupancy \[waves/SIMD\]: (\d+)", ln2)
                 if m:
-                    if int(m.group(1)) < waves:
-                        raise RuntimeError(f"{ln.split('Function Name:')[1].split()[0]}: occupancy {m.group(1)} "
-                                           f"waves/SIMD < {waves} (register pressure; see the resource report)")
-                    seen += 1
+                    occ = int(m.group(1))
                     break
-    if not seen:
-        raise RuntimeError(f"{name}: no occupancy in the compiler's resource report")
+            if occ is None:
+                raise RuntimeError(f"{fn}: no occupancy line in the compiler's resource report")
+            if occ < waves:
+                raise RuntimeError(f"{fn}: occupancy {occ} waves/SIMD < {waves} "
+                                   "(register pressure; see the resource report)")
+            seen += 1
+    if seen < MIN_KERNELS.get(os.path.basename(src), 1):
+        raise RuntimeError(f"{name}: {seen} kernel(s) in the compiler's resource report, "
+                           f"{MIN_KERNELS.get(os.path.basename(src), 1)} expected")
 
 
 def _compile(hipcc, cmd, src, o, force, hdr_time, verbose):

@@ -92,6 +92,10 @@ struct he_engine {
     uint32_t* cost = nullptr;    // [N]
     int order_every = 8;
     long long launches = 0;
+    // the stream of the last order rebuild and an event behind it: a physics launch on another
+    // stream waits for it, so no workgroup reads a half-written order
+    hipStream_t order_stream = nullptr;
+    hipEvent_t order_ready = nullptr;
 };
 
 extern "C" {
@@ -235,6 +239,7 @@ int he_destroy(he_engine* h) {
                     h->m_dt, h->m_starts, h->m_nframes, h->order, h->cost};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    if (h->order_ready) hipEventDestroy(h->order_ready);
     delete h;
     return 0;
 }
@@ -395,9 +400,15 @@ static PhysArgs phys_args(he_engine* h, int num_simulate, const float* actions) 
 // the physics launch, then every order_every launches the next launches' dispatch order from this
 // one's per-env cycles (heavy envs first, he_kernels.h launch_physics_order)
 static int physics_and_order(he_engine* h, const PhysArgs& a, hipStream_t stream) {
+    if (a.order && h->order_ready && h->order_stream != stream)
+        HE_CHECK(hipStreamWaitEvent(stream, h->order_ready, 0));
     HE_CHECK(launch_physics(a, stream));
-    if (a.order && ++h->launches % h->order_every == 0)
+    if (a.order && ++h->launches % h->order_every == 0) {
         HE_CHECK(launch_physics_order(h->cost, h->order, h->num_envs, stream));
+        if (!h->order_ready) HE_CHECK(hipEventCreateWithFlags(&h->order_ready, hipEventDisableTiming));
+        HE_CHECK(hipEventRecord(h->order_ready, stream));
+        h->order_stream = stream;
+    }
     return 0;
 }
 

@@ -2621,7 +2621,10 @@ HE_DEV void physics_body(const PhysArgs& a) {
     const int lane = threadIdx.x;
     // the env of this workgroup (launch_physics_order: heavy envs first); it and the start cycle wait
     // in LDS for the epilogue (no registers held through the substeps)
-    const int e0 = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+    // The order is rebuilt on the launch stream (he_engine.cpp); an index outside [0, num_envs) (a
+    // stray write into the buffer) falls back to workgroup id = env instead of faulting.
+    int e0 = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
+    if ((unsigned)e0 >= (unsigned)a.num_envs) e0 = (int)blockIdx.x;
     int e = e0;
     if (lane == 0) {
         L.sch_t0 = __builtin_readcyclecounter();

@@ -219,13 +219,14 @@ class Engine:
     @property
     def physics_order(self):
         """i32 [N]: the physics launch's dispatch order (the env of each workgroup, expensive envs
-        first; diagnostics, DESIGN §4.1 "Dispatch order")."""
-        return self.buffer(_abi.BUF_PHYS_ORDER)
+        first; diagnostics, DESIGN §4.1 "Dispatch order"). A copy: the engine's own buffer is read
+        by every physics launch and must not be written from outside."""
+        return self.buffer(_abi.BUF_PHYS_ORDER).clone()
 
     @property
     def physics_cost(self):
-        """i32 [N]: each env's wave cycles in the last physics launch (the order's input)."""
-        return self.buffer(_abi.BUF_PHYS_COST)
+        """i32 [N]: each env's wave cycles in the last physics launch (the order's input; a copy)."""
+        return self.buffer(_abi.BUF_PHYS_COST).clone()
 
     # ------------------------------------------------------------------ state writes
     def _contig(self, t, dtype=None):

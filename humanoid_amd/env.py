@@ -112,9 +112,21 @@ class EnvConfig:  # config.py:89-157
     max_contacts: int = 40
     # the physics solver (isaacgym_env.py:16-18 sets PhysX TGS, 4 position iterations): solver_type 1
     # TGS with solver_iterations position iterations per physics step; 0 the engine's PGS step
-    # (solver_iterations velocity-level sweeps, 8 recommended)
+    # (solver_iterations velocity-level sweeps). None: the solver's own default (TGS 4,
+    # PGS 8). Until round 4 the count meant PGS sweeps (default 8); a TGS iteration costs about two
+    # sweeps, so an explicit count other than 4 under TGS warns (resolved_solver_iterations).
     solver_type: int = 1
-    solver_iterations: int = 4
+    solver_iterations: Optional[int] = None
+
+    def resolved_solver_iterations(self) -> int:
+        if self.solver_iterations is None:
+            return 4 if self.solver_type == 1 else 8
+        if self.solver_type == 1 and self.solver_iterations != 4:
+            import warnings
+            warnings.warn(f"solver_iterations={self.solver_iterations} counts TGS position iterations "
+                          "(solver_type 1, the reference's 4: isaacgym_env.py:17), not PGS sweeps; set "
+                          "solver_type=0 for the PGS step", stacklevel=2)
+        return int(self.solver_iterations)
 
     @property
     def device(self) -> str:
@@ -168,7 +180,8 @@ class HumanoidPHC:
         self.num_obs, self.num_actions = NUM_OBS, NUM_ACTIONS
         sim = _abi.default_sim_params(self_collision=int(cfg.robot.has_self_collision), kp_scale=cfg.kp_scale,
                                       kd_scale=cfg.kd_scale, max_contacts=cfg.max_contacts,
-                                      solver_type=cfg.solver_type, solver_iterations=cfg.solver_iterations)
+                                      solver_type=cfg.solver_type,
+                                      solver_iterations=cfg.resolved_solver_iterations())
         # start pose z=0.89 + U(-1,1) xy jitter (humanoid_phc.py:340-347)
         rng = np.random.default_rng(cfg.seed)
         self.engine = Engine(self.model, n, device=self.device.index or 0, sim_params=sim,

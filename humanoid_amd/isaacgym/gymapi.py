@@ -306,15 +306,15 @@ class Gym:
         sp, px, o = sim.params, sim.params.physx, sim.asset.options
         plane = sim.plane or PlaneParams()
         # physx.solver_type 1 (TGS, isaacgym_env.py:16) with num_position_iterations per physics step;
-        # solver_type 0 maps onto the engine's velocity-level PGS step (8 sweeps)
+        # solver_type 0 maps onto the engine's velocity-level PGS step, num_position_iterations sweeps
+        # (8 is the engine's tested count)
         if px.solver_type not in (0, 1):
             raise NotImplementedError(f"physx.solver_type {px.solver_type}: 0 (PGS) or 1 (TGS)")
         if px.solver_type == 1 and px.num_velocity_iterations != 0:
             raise NotImplementedError("TGS velocity iterations: the reference runs 0 (isaacgym_env.py:18)")
-        if px.solver_type == 1 and not 1 <= px.num_position_iterations <= 16:
-            raise NotImplementedError("TGS num_position_iterations must be in [1, 16]")
-        solver = dict(solver_type=1, solver_iterations=int(px.num_position_iterations)) if px.solver_type == 1 else \
-            dict(solver_type=0, solver_iterations=8)
+        if not 1 <= px.num_position_iterations <= 16:
+            raise NotImplementedError("num_position_iterations must be in [1, 16]")
+        solver = dict(solver_type=int(px.solver_type), solver_iterations=int(px.num_position_iterations))
         params = _abi.default_sim_params(
             dt=sp.dt, contact_offset=px.contact_offset, max_depenetration_velocity=px.max_depenetration_velocity,
             angular_damping=o.angular_damping, max_angular_velocity=o.max_angular_velocity,

@@ -107,7 +107,9 @@ def test_occupancy_guard_removes_the_rejected_object(tmp_path, monkeypatch):
     src.write_text("// fake")
     o = str(tmp_path / "he_physics.hip.o")
     stamp = o + ".cmd"
-    remark = ("remark: Function Name: physics_kernel\nremark:     VGPRs: 300\n"
+    remark = ("remark: Function Name: physics_kernel\nremark:     VGPRs: 256\n"
+              "remark:     Occupancy [waves/SIMD]: 2\n"
+              "remark: Function Name: physics_kernel_tgs\nremark:     VGPRs: 300\n"
               "remark:     Occupancy [waves/SIMD]: 1\n")
 
     def fake_run(cmd, capture_output=True, text=True):
@@ -127,3 +129,11 @@ def test_occupancy_guard_removes_the_rejected_object(tmp_path, monkeypatch):
     remark = remark.replace("SIMD]: 1", "SIMD]: 2")
     assert build._compile("hipcc", cmd, str(src), o, True, 0.0, False)
     assert os.path.exists(o) and open(stamp).read() == " ".join(cmd)
+    # a watched kernel whose report has no occupancy line, or a missing kernel, fails too
+    full = remark
+    remark = full.replace("remark:     Occupancy [waves/SIMD]: 2\n", "", 1)
+    with pytest.raises(RuntimeError, match="no occupancy line"):
+        build._compile("hipcc", cmd, str(src), o, True, 0.0, False)
+    remark = full.split("remark: Function Name: physics_kernel_tgs")[0]
+    with pytest.raises(RuntimeError, match="2 expected"):
+        build._compile("hipcc", cmd, str(src), o, True, 0.0, False)

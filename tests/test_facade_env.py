@@ -14,6 +14,22 @@ import cases
 
 
 # ----------------------------------------------------------------------------------- CPU
+def test_env_config_solver_iterations():
+    """solver_iterations counts TGS position iterations under solver_type 1 (isaacgym_env.py:17: 4)
+    and PGS sweeps under 0; unset, each solver's default; an explicit TGS count other than 4 warns
+    (it meant PGS sweeps before round 5)."""
+    import warnings
+    from humanoid_amd.env import EnvConfig
+    assert EnvConfig().resolved_solver_iterations() == 4
+    assert EnvConfig(solver_type=0).resolved_solver_iterations() == 8
+    assert EnvConfig(solver_type=0, solver_iterations=6).resolved_solver_iterations() == 6
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert EnvConfig(solver_iterations=4).resolved_solver_iterations() == 4
+    with pytest.warns(UserWarning, match="TGS position iterations"):
+        assert EnvConfig(solver_iterations=8).resolved_solver_iterations() == 8
+
+
 def test_gymapi_surface_and_errors():
     from humanoid_amd.isaacgym import gymapi, gymtorch
     from humanoid_amd.model import DEFAULT_MODEL_JSON

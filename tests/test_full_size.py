@@ -164,7 +164,13 @@ def _record(name, obj):
 
 
 STEPS = 30
-NPROBES = int(os.environ.get("HE_PARITY_PROBES", "8"))
+# The chaos floor's probe count. 8 probes missed a bifurcation that the GPU took (configs[4] env 2003
+# in the 8 x 48 record, profiles/r05/dr_events_8x48.json: post-event ratio 62 at 8 probes, 1.28 at 32):
+# a branch that a fraction p of fp32-level perturbations take is missed by K probes with probability
+# (1 - p)^K. 32 by default; an env still over POST_K is escalated (ESCALATE more probes on it alone)
+# before the bound is applied -- a sequential test, recorded per env.
+NPROBES = int(os.environ.get("HE_PARITY_PROBES", "32"))
+ESCALATE = int(os.environ.get("HE_PARITY_ESCALATE", "96"))
 
 
 def _tiered_close(name, g, o, probes, atol, tiers, where=None):
@@ -191,37 +197,56 @@ def _tiered_close(name, g, o, probes, atol, tiers, where=None):
                               "first_event_step": int(where[2][e]), "dev": float(dev[e, j]), "sens": float(sens[e, j])}
 
 
-# HE_PARITY_DUMP=1: every env whose post-event ratio passes POST_K is written out step by step
-# (HE_RECORD_DIR/divergent_<env>.json: distances, the probes' floors, stick / slip states)
+# HE_PARITY_DUMP=1: every env whose post-event ratio passes POST_K at the default probes is written
+# out step by step (HE_RECORD_DIR/divergent_<env>.json: distances, the probes' floors, stick / slip
+# states, the escalated floor, the one-step re-seeded deviation where the test has one)
 DUMP = bool(os.environ.get("HE_PARITY_DUMP"))
 
 
-def _dump_divergent(model, idx, first, first_set, first_slip, post_env, hist, trace):
+def _dump_divergent(model, idx, envs, first, first_set, first_slip, ratio0, ratio, hist, trace, esc, one_step):
     d = os.environ.get("HE_RECORD_DIR") or "."
     fmt = lambda st: [[int(k), int(v)] for k, v in st]  # noqa: E731
-    for e in np.nonzero(post_env > POST_K)[0]:
+    for e in envs:
         steps = []
         for s_, (qg, rbg, qo, rbo, qps, rbps) in enumerate(hist):
             cg_ = cases.center_of_mass(model, rbg[e:e + 1])[0]
             co_ = cases.center_of_mass(model, rbo[e:e + 1])[0]
             cps = [cases.center_of_mass(model, r[e:e + 1])[0] for r in rbps]
             t = trace[s_]
-            steps.append({"step": s_,
-                          "l2_gpu": float(np.linalg.norm(qg[e].astype(np.float64) - qo[e])),
-                          "com_gpu": float(np.abs(cg_ - co_).max()),
-                          "l2_probes": [float(np.linalg.norm(q[e].astype(np.float64) - qo[e])) for q in qps],
-                          "com_probes": [float(np.abs(c - co_).max()) for c in cps],
-                          "com_oracle": [float(x) for x in co_],
-                          "slip_gpu": fmt(t["gpu"][e]), "slip_oracle": fmt(t["oracle"][e]),
-                          "slip_probes_differ": [int(p[e] != t["oracle"][e]) for p in t["probes"]],
-                          "keys_equal": bool(t["keys_gpu"][e] == t["keys_oracle"][e])})
+            st = {"step": s_,
+                  "l2_gpu": float(np.linalg.norm(qg[e].astype(np.float64) - qo[e])),
+                  "com_gpu": float(np.abs(cg_ - co_).max()),
+                  "l2_probes": [float(np.linalg.norm(q[e].astype(np.float64) - qo[e])) for q in qps],
+                  "com_probes": [float(np.abs(c - co_).max()) for c in cps],
+                  "com_oracle": [float(x) for x in co_],
+                  "slip_gpu": fmt(t["gpu"][e]), "slip_oracle": fmt(t["oracle"][e]),
+                  "slip_probes_differ": [int(p[e] != t["oracle"][e]) for p in t["probes"]],
+                  "keys_equal": bool(t["keys_gpu"][e] == t["keys_oracle"][e])}
+            if e in esc:
+                st["l2_escalated"] = [float(x) for x in esc[e]["l2"][:, s_]]
+                st["com_escalated"] = [float(x) for x in esc[e]["com"][:, s_]]
+            if one_step is not None and (int(idx[e]), s_) in one_step:
+                st["one_step"] = one_step[(int(idx[e]), s_)]
+            steps.append(st)
         rec = {"env": int(idx[e]), "first_event": int(first[e]), "first_set": int(first_set[e]),
-               "first_slip": int(first_slip[e]), "post_event_max_ratio": float(post_env[e]), "steps": steps}
+               "first_slip": int(first_slip[e]), "ratio_at_default_probes": float(ratio0[e]),
+               "ratio_after_escalation": float(ratio[e]), "probes": NPROBES,
+               "escalated_probes": ESCALATE if e in esc else 0, "steps": steps}
         with open(os.path.join(d, f"divergent_{int(idx[e])}.json"), "w") as f:
             json.dump(rec, f, indent=1)
 
 
-def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
+def _first_events(caches, c_o, mu, tw, step, first_set, first_slip):
+    """Mark, in place, the first step at which each env's solve (`caches`) differs from the oracle's
+    in its contact set or in a friction row's stick / slip state."""
+    from test_gpu_parity import contact_keys, friction_states
+    kd = np.array([a != b for a, b in zip(contact_keys(caches), contact_keys(c_o))])
+    first_set[kd & (first_set == STEPS)] = step
+    sd = np.array([a != b for a, b in zip(friction_states(caches, mu, tw), friction_states(c_o, mu, tw))])
+    first_slip[sd & (first_slip == STEPS)] = step
+
+
+def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed, one_step=None):
     """STEPS policy steps of the full-size rollout `ro` (advance(step) launches the physics of all 4096
     envs and returns the sampled envs' PD targets) against the fp64 oracle on the sample `idx`: its own
     trajectory from the common start state and warm-start cache, and NPROBES probe trajectories with
@@ -230,22 +255,27 @@ def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
       step's discontinuities) every joint angle and the CoM elementwise at 1e-4 (_tiered_close);
     * from its first event on, the GPU's distance to the oracle -- joint-pose L2 over the 69 joint
       coordinates and CoM distance -- against the oracle's chaos floor, the probes' largest distance
-      on the same env and step (at least 1e-4): their ratio, bounded by the caller.
+      on the same env and step (at least 1e-4): their ratio, bounded by the caller. An env whose ratio
+      passes POST_K gets ESCALATE more probe trajectories of its own first (recorded).
+    The probes' own events against the oracle are counted like the GPU's: the GPU is one more fp32
+    perturbation, so its event count is bounded against theirs (the caller).
     Returns the record (also the bench line's parity figures)."""
     from humanoid_amd import _abi
-    from test_gpu_parity import contact_keys, friction_states, torsion_weights
     n = len(idx)
     root = ro.eng.root_states.cpu().numpy()[idx].copy()
     dof = ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx].copy()
     c_o = ro.eng.contact_cache.cpu().numpy()[idx].copy()
+    start = (root.copy(), dof.copy(), c_o.copy())
     probes = [[root.copy(), dof.copy(), c_o.copy(), None] for _ in range(NPROBES)]
     mu = props.get("friction", np.full(n, sp.friction, np.float32))
     first_set = np.full(n, STEPS)
     first_slip = np.full(n, STEPS)
-    hist = []
-    trace = []
+    p_set = np.full((NPROBES, n), STEPS)
+    p_slip = np.full((NPROBES, n), STEPS)
+    hist, trace, tgts = [], [], []
     for step in range(STEPS):
         tgt = advance(step)
+        tgts.append(tgt)
         rw = np.zeros((n, _abi.MAX_ROWS), np.float32)  # the oracle's row bound weights (torsion stick / slip)
         O.set_row_weight_out(rw)
         try:
@@ -256,80 +286,113 @@ def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
             pr[3] = cases.probe_physics_step(he_model, sp, pr[0], pr[1], tgt, 2, pr[2], seed + 1000 * k + step, **props)
         torch.cuda.synchronize()
         cg = ro.eng.contact_cache.cpu().numpy()[idx]
+        from test_gpu_parity import contact_keys, friction_states, torsion_weights
         tw = torsion_weights(rw, c_o)
-        first_set[np.array([a != b for a, b in zip(contact_keys(cg), contact_keys(c_o))]) & (first_set == STEPS)] = step
-        fs_o = friction_states(c_o, mu, tw)
-        fs_g = friction_states(cg, mu, tw)
-        slip = np.array([a != b for a, b in zip(fs_g, fs_o)])
-        first_slip[slip & (first_slip == STEPS)] = step
+        _first_events(cg, c_o, mu, tw, step, first_set, first_slip)
+        for k, pr in enumerate(probes):
+            _first_events(pr[2], c_o, mu, tw, step, p_set[k], p_slip[k])
         if DUMP:  # diagnostics: the stick / slip states of GPU, oracle and every probe, per env
-            fs_p = [friction_states(pr[2], mu, tw) for pr in probes]
-            trace.append({"gpu": fs_g, "oracle": fs_o, "probes": fs_p,
+            trace.append({"gpu": friction_states(cg, mu, tw), "oracle": friction_states(c_o, mu, tw),
+                          "probes": [friction_states(pr[2], mu, tw) for pr in probes],
                           "keys_gpu": contact_keys(cg), "keys_oracle": contact_keys(c_o)})
         hist.append((ro.eng.dof_state.view(4096, 69, 2).cpu().numpy()[idx, :, 0].copy(),
                      ro.eng.rb_state.view(4096, 24, 13).cpu().numpy()[idx].copy(), dof[..., 0].copy(),
                      out["rb_state"].copy(), [p[1][..., 0].copy() for p in probes],
                      [p[3]["rb_state"].copy() for p in probes]))
     first = np.minimum(first_set, first_slip)
-    tiers = {"total": 0, "needed": 0, "beyond_4": 0, "beyond_8": 0, "k_max": 0.0}
-    tiers_adj = dict(tiers)
-    l2_all, com_all, pre_l2, pre_com, post_q, post_c, adj_q, adj_c = [], [], [], [], [], [], [], []
-    post_env = np.zeros(n)
+    # per step and env: the GPU's distance to the oracle and the probes' floor (largest probe distance)
+    L2 = np.zeros((STEPS, n))
+    COM = np.zeros((STEPS, n))
+    FQ = np.zeros((STEPS, n))
+    FC = np.zeros((STEPS, n))
+    com_o = []
     for s_, (qg, rbg, qo, rbo, qps, rbps) in enumerate(hist):
         cg_, co_ = cases.center_of_mass(model, rbg), cases.center_of_mass(model, rbo)
-        cps = [cases.center_of_mass(model, r) for r in rbps]
-        l2 = np.linalg.norm(qg.astype(np.float64) - qo, axis=1)
-        com = np.abs(cg_ - co_).max(1)
-        l2_all.append(l2)
-        com_all.append(com)
-        # the policy step just before an env's first detected event is event-adjacent: the caches are
-        # compared once per policy step (4 physics steps), so an event inside it that is gone by its end
-        # (a contact or stick / slip flicker, a limit touched and left) shows only as the divergence it
-        # leaves; that step is checked against the chaos floor like the steps after the event
+        com_o.append(co_)
+        L2[s_] = np.linalg.norm(qg.astype(np.float64) - qo, axis=1)
+        COM[s_] = np.abs(cg_ - co_).max(1)
+        FQ[s_] = np.max([np.linalg.norm(q.astype(np.float64) - qo, axis=1) for q in qps], axis=0)
+        FC[s_] = np.max([np.abs(cases.center_of_mass(model, r) - co_).max(1) for r in rbps], axis=0)
+    # the steps held against the floor: from the step before an env's first detected event on (that one
+    # is event-adjacent: the caches are compared once per policy step of 4 physics steps, so an event
+    # inside it that is gone by its end shows only as the divergence it leaves)
+    steps_ix = np.arange(STEPS)[:, None]
+    held = (first[None, :] <= steps_ix + 1) & (first[None, :] < STEPS)
+
+    def ratios():
+        return np.maximum(L2 / np.maximum(FQ, 1e-4), COM / np.maximum(FC, 1e-4))
+    ratio0 = np.where(held, ratios(), 0.0).max(0)
+    esc = {}
+    for e in np.nonzero(ratio0 > POST_K)[0]:
+        pe = {k: (v[e:e + 1].copy() if isinstance(v, np.ndarray) else v) for k, v in props.items()}
+        el2, ecom = np.zeros((ESCALATE, STEPS)), np.zeros((ESCALATE, STEPS))
+        for k in range(ESCALATE):
+            r_, d_, c_ = start[0][e:e + 1].copy(), start[1][e:e + 1].copy(), start[2][e:e + 1].copy()
+            for s_ in range(STEPS):
+                o = cases.probe_physics_step(he_model, sp, r_, d_, tgts[s_][e:e + 1], 2, c_,
+                                             seed + 7919 + 1000 * k + s_, **pe)
+                el2[k, s_] = np.linalg.norm(d_[0, :, 0].astype(np.float64) - hist[s_][2][e])
+                ecom[k, s_] = np.abs(cases.center_of_mass(model, o["rb_state"])[0] - com_o[s_][e]).max()
+        FQ[:, e] = np.maximum(FQ[:, e], el2.max(0))
+        FC[:, e] = np.maximum(FC[:, e], ecom.max(0))
+        esc[e] = {"l2": el2, "com": ecom}
+    R = ratios()
+    ratio = np.where(held, R, 0.0).max(0)
+    # before the first event: elementwise at 1e-4 against the probes' sensitivity
+    tiers = {"total": 0, "needed": 0, "beyond_4": 0, "beyond_8": 0, "k_max": 0.0}
+    tiers_adj = dict(tiers)
+    pre_l2, pre_com, post_q, post_c, adj_q, adj_c = [], [], [], [], [], []
+    for s_, (qg, rbg, qo, rbo, qps, rbps) in enumerate(hist):
         adj = (first == s_ + 1) & (first < STEPS)
         pre = (first > s_) & ~adj
+        post = first <= s_
         if adj.any():
             _tiered_close("dof pos", qg[adj], qo[adj], [q[adj] for q in qps], 1e-4, tiers_adj)
-            fq = np.max([np.linalg.norm(q[adj].astype(np.float64) - qo[adj], axis=1) for q in qps], axis=0)
-            fc = np.max([np.abs(c[adj] - co_[adj]).max(1) for c in cps], axis=0)
-            adj_q.append(l2[adj] / np.maximum(fq, 1e-4))
-            adj_c.append(com[adj] / np.maximum(fc, 1e-4))
+            adj_q.append(L2[s_, adj] / np.maximum(FQ[s_, adj], 1e-4))
+            adj_c.append(COM[s_, adj] / np.maximum(FC[s_, adj], 1e-4))
         if pre.any():
+            cg_ = cases.center_of_mass(model, rbg[pre])
+            cps = [cases.center_of_mass(model, r[pre]) for r in rbps]
             w = (idx[pre], s_, first[pre])
             _tiered_close("dof pos", qg[pre], qo[pre], [q[pre] for q in qps], 1e-4, tiers, w)
-            _tiered_close("CoM", cg_[pre], co_[pre], [c[pre] for c in cps], 1e-4, tiers, w)
-            pre_l2.append(l2[pre])
-            pre_com.append(com[pre])
-        post = first <= s_
+            _tiered_close("CoM", cg_, com_o[s_][pre], cps, 1e-4, tiers, w)
+            pre_l2.append(L2[s_, pre])
+            pre_com.append(COM[s_, pre])
         if post.any():
-            fq = np.max([np.linalg.norm(q[post].astype(np.float64) - qo[post], axis=1) for q in qps], axis=0)
-            fc = np.max([np.abs(c[post] - co_[post]).max(1) for c in cps], axis=0)
-            rq = l2[post] / np.maximum(fq, 1e-4)
-            rc = com[post] / np.maximum(fc, 1e-4)
-            post_q.append(rq)
-            post_c.append(rc)
-            post_env[post] = np.maximum(post_env[post], np.maximum(rq, rc))
-    l2_all, com_all = np.stack(l2_all), np.stack(com_all)
+            post_q.append(L2[s_, post] / np.maximum(FQ[s_, post], 1e-4))
+            post_c.append(COM[s_, post] / np.maximum(FC[s_, post], 1e-4))
     if DUMP:
-        _dump_divergent(model, idx, first, first_set, first_slip, post_env, hist, trace)
+        _dump_divergent(model, idx, np.nonzero(ratio0 > POST_K)[0], first, first_set, first_slip, ratio0, ratio,
+                        hist, trace, esc, one_step)
     cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0)  # noqa: E731
     pre_l2, pre_com, post_q, post_c = cat(pre_l2), cat(pre_com), cat(post_q), cat(post_c)
     adj_q, adj_c = cat(adj_q), cat(adj_c)
     ev = first < STEPS
+    p_first = np.minimum(p_set, p_slip)
     return {
-        "envs": n, "steps": STEPS, "env_ids": [int(e) for e in idx],
-        "joint_pose_l2_vs_oracle_rad": {"mean": float(l2_all.mean()), "p90": float(np.percentile(l2_all, 90)),
-                                        "max": float(l2_all.max()),
+        "envs": n, "steps": STEPS, "env_ids": [int(e) for e in idx], "probes": NPROBES,
+        "joint_pose_l2_vs_oracle_rad": {"mean": float(L2.mean()), "p90": float(np.percentile(L2, 90)),
+                                        "max": float(L2.max()),
                                         "max_before_event": float(pre_l2.max()) if pre_l2.size else None},
-        "com_err_vs_oracle_m": {"mean": float(com_all.mean()), "max": float(com_all.max()),
+        "com_err_vs_oracle_m": {"mean": float(COM.mean()), "max": float(COM.max()),
                                 "max_before_event": float(pre_com.max()) if pre_com.size else None},
         "contact_set_events": int((first_set < STEPS).sum()),
         "stick_slip_only_events": int(((first_slip < STEPS) & (first_set == STEPS)).sum()),
         "envs_with_event": int(ev.sum()),
+        # the same counts for each fp32-noise probe against the oracle (the GPU is one more such perturbation)
+        "probe_events": {"contact_set": [int(x) for x in (p_set < STEPS).sum(1)],
+                         "stick_slip_only": [int(x) for x in ((p_slip < STEPS) & (p_set == STEPS)).sum(1)],
+                         "envs_with_event": [int(x) for x in (p_first < STEPS).sum(1)]},
         "event_first_steps": sorted(int(f) for f in first[ev]),
         "events": [{"env": int(idx[e]), "first_step": int(first[e]),
                     "kind": "contact set" if first_set[e] <= first_slip[e] else "stick/slip",
-                    "post_event_max_ratio": float(post_env[e])} for e in np.nonzero(ev)[0]],
+                    "post_event_max_ratio": float(ratio[e]),
+                    **({"ratio_at_default_probes": float(ratio0[e]), "escalated_probes": ESCALATE} if e in esc else {})}
+                   for e in np.nonzero(ev)[0]],
+        "escalated": [{"env": int(idx[e]), "ratio_at_default_probes": float(ratio0[e]),
+                       "ratio_after_escalation": float(ratio[e]),
+                       "escalated_probes_at_or_past_gpu": int(((esc[e]["l2"] >= L2[None, :, e]) & held[None, :, e]).any(1).sum())}
+                      for e in esc],
         "env_steps_before_event": int(pre_l2.size), "env_steps_after_event": int(post_q.size),
         "pre_event_elements": tiers,
         "event_adjacent": {"env_steps": int(adj_q.size),
@@ -337,8 +400,9 @@ def _trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed):
                            "com_ratio_max": float(adj_c.max()) if adj_c.size else None,
                            "elements": tiers_adj},
         "post_event": {"definition": "GPU-vs-oracle distance / the oracle's chaos floor (the largest distance of its "
-                                     f"{NPROBES} fp32-noise probe trajectories on the same env and step, at least 1e-4), "
-                                     "joint-pose L2 and CoM; every env-step from the env's first event on",
+                                     f"{NPROBES} fp32-noise probe trajectories on the same env and step, at least 1e-4; "
+                                     f"{ESCALATE} more for an env past POST_K), joint-pose L2 and CoM; every env-step "
+                                     "from the env's first event on",
                        "joint_ratio_max": float(post_q.max()) if post_q.size else None,
                        "joint_ratio_p90": float(np.percentile(post_q, 90)) if post_q.size else None,
                        "com_ratio_max": float(post_c.max()) if post_c.size else None,
@@ -358,6 +422,12 @@ def _merge(recs):
     out["env_ids"] = [e for r in recs for e in r["env_ids"]]
     out["event_first_steps"] = sorted(f for r in recs for f in r["event_first_steps"])
     out["events"] = [e for r in recs for e in r["events"]]
+    out["escalated"] = [e for r in recs for e in r["escalated"]]
+    out["probe_events"] = {k: [int(sum(r["probe_events"][k][j] for r in recs)) for j in range(len(recs[0]["probe_events"][k]))]
+                           for k in recs[0]["probe_events"]}
+    out["per_sample"] = [{"envs": r["envs"], "contact_set_events": r["contact_set_events"],
+                          "stick_slip_only_events": r["stick_slip_only_events"], "envs_with_event": r["envs_with_event"],
+                          "probe_envs_with_event_max": max(r["probe_events"]["envs_with_event"])} for r in recs]
     t = {"total": 0, "needed": 0, "beyond_4": 0, "beyond_8": 0, "k_max": 0.0}
     for r in recs:
         for k in ("total", "needed", "beyond_4", "beyond_8"):
@@ -392,33 +462,35 @@ def _merge(recs):
     return out
 
 
-# Bounds, from the TGS build's measurement over the two samples of each test (profiles/r05/
-# {dr_events,parity_configs2}.json): before an env's first event, elements past 1e-4 at most
-# NEEDED_FRAC of those compared, every one of them within 4x the oracle's own sensitivity but
-# PRE_BEYOND4_FRAC, none beyond 8x; on the event-adjacent step (the one before the first detected
-# event, measured up to 1.9x the floor, one element 8.2x its sensitivity: env 281 of the tracking
-# sample, step 12 of 13) and from the first event on, the GPU's distance at most POST_K x the oracle's
-# chaos floor on every env-step (measured max 4.5); the event counts (informational: every env is
-# compared either way) each at most the per-test bound.
+# Bounds. Before an env's first event, elements past 1e-4 at most NEEDED_FRAC of those compared,
+# every one of them within 4x the oracle's own sensitivity but PRE_BEYOND4_FRAC, none beyond 8x (the
+# TGS build's 8 x 48 records, profiles/r05/{dr_events,parity_configs2}_8x48.json: 0.01 % / 0.24 %
+# needed, one element past 4x). On the event-adjacent step and from the first event on, the GPU's
+# distance at most POST_K x the oracle's chaos floor on every env-step (after escalation; measured
+# max 1.28 at 32 probes over 8 x 48 envs of each config). Events: the GPU is one more fp32 perturbation
+# of the oracle, so the envs in which it meets an event (a contact-set or stick / slip difference) are
+# bounded by EVENT_K x the most any single probe meets plus EVENT_SLACK (the records' probe_events).
 NEEDED_FRAC = 0.01
 PRE_BEYOND4_FRAC = 1e-4
 POST_K = 6.0
+EVENT_K = 1.5
+EVENT_SLACK = 4
 
 
 def _sample_seeds(base):
-    """The samples' seeds: the two of the suite, plus more when HE_PARITY_SAMPLES asks for them (a
-    wider record, e.g. tools/gpu_full_size_parity.sh with HE_PARITY_SAMPLES=8; the same bounds)."""
-    n = int(os.environ.get("HE_PARITY_SAMPLES", "2"))
-    return tuple(base) + tuple(1000 + 17 * k + base[0] for k in range(max(0, n - len(base))))
+    """The samples' seeds: the two base seeds, then 1000 + 17 k + base[0]; HE_PARITY_SAMPLES of them
+    (default 8: 8 x 48 of the 4096 envs, each sample's 30 steps following the previous one's)."""
+    n = int(os.environ.get("HE_PARITY_SAMPLES", "8"))
+    return (tuple(base) + tuple(1000 + 17 * k + base[0] for k in range(max(0, n - len(base)))))[:max(n, 1)]
 
 
-def _assert_parity(rec, max_set, max_slip):
+def _assert_parity(rec):
     t = rec["pre_event_elements"]
     assert t["beyond_8"] == 0, t
     assert t["beyond_4"] <= PRE_BEYOND4_FRAC * t["total"], t
     assert t["needed"] <= NEEDED_FRAC * t["total"], t
-    assert rec["contact_set_events"] <= max_set * rec["envs"], rec["contact_set_events"]
-    assert rec["stick_slip_only_events"] <= max_slip * rec["envs"], rec["stick_slip_only_events"]
+    pmax = max(rec["probe_events"]["envs_with_event"])
+    assert rec["envs_with_event"] <= EVENT_K * pmax + EVENT_SLACK, (rec["envs_with_event"], rec["probe_events"])
     for pe in (rec["post_event"], rec["event_adjacent"]):
         for k in ("joint_ratio_max", "com_ratio_max"):
             assert pe[k] is None or pe[k] <= POST_K, pe
@@ -444,6 +516,7 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     zero = torch.zeros_like(ro.actions)
     recs = []
     one_stats = {"env_steps": 0, "contact_set_differences": 0, "max_abs_dof_pos_rad": 0.0, "max_abs_com_m": 0.0}
+    one_env = {}  # (env, step) -> the one-step re-seeded deviation of that env (the divergence dumps)
     st1 = CondStats()
     for sample in _sample_seeds((12, 15)):
         idx = np.sort(np.random.default_rng(sample).choice(4096, 48, replace=False))
@@ -474,14 +547,31 @@ def test_full_size_dr_sample_30_steps(model, he_model):
             _cond_close("CoM", com_g, com_o, [cases.center_of_mass(model, r) for _, r in one_pr], 1e-4, stats=st1)
             one_stats["max_abs_dof_pos_rad"] = max(one_stats["max_abs_dof_pos_rad"], float(np.abs(dg[..., 0] - d1[..., 0]).max()))
             one_stats["max_abs_com_m"] = max(one_stats["max_abs_com_m"], float(np.abs(com_g - com_o).max()))
+            dev = np.abs(dg[..., 0] - d1[..., 0]).max(1)
+            sens = np.max([np.abs(d[..., 0] - d1[..., 0]).max(1) for d, _ in one_pr], axis=0)
+            keq = [a == b for a, b in zip(contact_keys(cg), contact_keys(c1o))]
+            for j, e in enumerate(idx):
+                one_env[(int(e), step)] = {"dof_pos_dev": float(dev[j]), "dof_pos_probe_sens": float(sens[j]),
+                                           "com_dev": float(np.abs(com_g[j] - com_o[j]).max()), "keys_equal": bool(keq[j])}
             return tgt
 
-        recs.append(_trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed=123 + sample))
+        recs.append(_trajectory_parity(model, he_model, ro, idx, advance, props, sp, seed=123 + sample,
+                                       one_step=one_env))
     rec = _merge(recs)
     rec["one_step"] = dict(one_stats, widened_frac=st1.frac)
+    # every event env's largest one-step deviation: its step from each of its own GPU states against the
+    # oracle's from the same state (a GPU/oracle difference would show here, a bifurcation does not)
+    for ev in rec["events"]:
+        d = [v for (e, _), v in one_env.items() if e == ev["env"]]
+        ev["one_step_max_dof_pos_dev"] = max(v["dof_pos_dev"] for v in d)
+        ev["one_step_keys_equal"] = all(v["keys_equal"] for v in d)
+    # the regression case: env 2003 of the third sample took a contact-set branch that 8 probes missed
+    # (r05 8 x 48 record); it must be in the compared set whenever the default samples run
+    if len(_sample_seeds((12, 15))) >= 3:
+        assert 2003 in rec["env_ids"]
     print("dr parity:", {k: v for k, v in rec.items() if k not in ("env_ids", "events", "definition")})
     _record("dr_events", rec)
-    _assert_parity(rec, max_set=0.25, max_slip=0.6)
+    _assert_parity(rec)
     assert st1.frac <= 0.005
 
 
@@ -521,4 +611,4 @@ def test_full_size_tracking_parity_30_steps(model, he_model):
                        "oracle from one start state")
     print("tracking parity:", {k: v for k, v in rec.items() if k not in ("env_ids", "events", "definition")})
     _record("parity_configs2", rec)
-    _assert_parity(rec, max_set=0.25, max_slip=0.6)
+    _assert_parity(rec)
