@@ -502,6 +502,58 @@ HE_DEV void reduce_scatter_z(const regla::ZVec& z, float x, int lane, float& e1,
     w[0] += dpp<0xB1>(w[0]);
     e2 = __shfl(w[0], 4 * (lane & 15), W);
 }
+// The rows' support inside the root and the two legs (bodies 0..8: dofs 0..29, the DFS prefix; a body
+// standing or walking on its feet): Zh is zero past dof 29, so the iterations' products run over the
+// first KZ = 32 dofs (dofs 30, 31 exact zeros) with Zh's other 44 registers dead.
+#ifndef HE_TGS_LEGS  // A/B only: 0 runs every env's iterations over all 75 dofs
+#define HE_TGS_LEGS 1
+#endif
+#ifndef HE_TGS_LEGS_ROWS  // A/B only: 0 runs the rows' once-per-step dot products over all 75 dofs
+#define HE_TGS_LEGS_ROWS 1
+#endif
+constexpr uint32_t kLegBodies = 0x1FFu;
+constexpr int KZ = 32;
+static_assert(smpl::kNB > 9, "the leg prefix is bodies 0..8");
+// zdot_lanes over dofs 0..KZ-1: bit for bit the full form (its dropped terms are fma(0, y, s) = s)
+HE_DEV float zdot_lanes_legs(const regla::ZVec& z, float yl) {
+    using regla::f2v;
+    f2v a = f2v{0.f, 0.f}, b = f2v{0.f, 0.f};
+    regla::static_for<0, KZ, 4>([&](auto ic) {
+        constexpr int i0 = decltype(ic)::value;
+        float sv[4];
+        regla::rdlane4<i0>(yl, sv);
+        a = __builtin_elementwise_fma(z.p[i0 >> 1], f2v{sv[0], sv[1]}, a);
+        b = __builtin_elementwise_fma(z.p[(i0 >> 1) + 1], f2v{sv[2], sv[3]}, b);
+    });
+    return (a.x + a.y) + (b.x + b.y);
+}
+// Zh^T x over dofs 0..KZ-1 into lane = dof: the butterfly's stages inside each 32-lane half (lane bits
+// 4 .. 0: the 32 values to one per lane), then the two halves' partial sums added (lane bit 5). Lanes
+// >= KZ return 0 (e2 = 0: no dof past 63 is on the support). The same sum as reduce_scatter_z's in
+// another association order.
+HE_DEV float reduce_scatter_z_legs(const regla::ZVec& z, float x) {
+    using regla::f2v;
+    const f2v xx = f2v{x, x};
+    float v[KZ];
+#pragma unroll
+    for (int j = 0; j < KZ / 2; j += 2) {
+        const f2v pa = z.p[j >> 1] * xx, pb = z.p[(j + KZ / 2) >> 1] * xx;
+        float a0 = pa.x, b0 = pb.x, a1 = pa.y, b1 = pb.y;
+        swap16(a0, b0);
+        swap16(a1, b1);
+        const f2v s = f2v{a0, a1} + f2v{b0, b1};
+        v[j] = s.x;
+        v[j + 1] = s.y;
+    }
+    rs_dpp<8, 0x140, 0xFF00FF00FF00FF00ull>(v);
+    rs_dpp<4, 0x141, 0xF0F0F0F0F0F0F0F0ull>(v);
+    rs_dpp<2, 0x4E, 0xCCCCCCCCCCCCCCCCull>(v);
+    rs_dpp<1, 0xB1, 0xAAAAAAAAAAAAAAAAull>(v);
+    float a = v[0], b = v[0];
+    swap32(a, b);  // a: lanes < 32 their own half's sum, b: the other half's (lanes >= 32: swapped roles)
+    const float e = a + b;
+    return regla::lanes<0xFFFFFFFFull>() ? e : 0.f;
+}
 // at most 32 rows (<= 10 contacts): only the rows-0-31 x columns-0-31 tile is needed (one MFMA per
 // dof pair instead of four); rows >= 32 of acol are never read then
 HE_DEV void delassus_mfma32(const regla::ZVec& z, float (&acol)[MAXR], uint32_t live) {
@@ -767,12 +819,41 @@ HE_DEV void zrow_bodies(regla::ZVec& z, float (&bacc)[4], uint32_t lb, uint32_t 
         zrow_bodies<B + 1>(z, bacc, lb, anc0, anc1, cx, dd, L, nxt);
     }
 }
-template <int I>
+template <int I, int N = NG>
 HE_DEV void scale_rows(regla::ZVec& z, float sdl, float sdl2) {
-    if constexpr (I < NG) {
+    if constexpr (I < N) {
         ZV(z, I) *= I < 64 ? regla::rdlane(sdl, I < 64 ? I : 0) : regla::rdlane(sdl2, I >= 64 ? I - 64 : 0);
-        scale_rows<I + 1>(z, sdl, sdl2);
+        scale_rows<I + 1, N>(z, sdl, sdl2);
     }
+}
+// the rows' dot products over the register pairs (dof i into partial sum i mod 4) over dofs 0..N-1:
+// sum_i a_r[i] u_i with u read from LDS (J_r u0), and |zh_r|^2
+template <int N>
+HE_DEV float zdot_lds(const regla::ZVec& z, const float* u) {
+    float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+        const regla::f2v uk = *reinterpret_cast<const regla::f2v*>(&u[2 * k]);
+        regla::f2v acc = regla::f2v{bacc[(2 * k) & 3], bacc[(2 * k + 1) & 3]};
+        acc = __builtin_elementwise_fma(z.p[k], uk, acc);
+        bacc[(2 * k) & 3] = acc.x;
+        bacc[(2 * k + 1) & 3] = acc.y;
+    }
+    if constexpr (N & 1) bacc[(N - 1) & 3] = fmaf(ZV(z, N - 1), u[N - 1], bacc[(N - 1) & 3]);
+    return (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
+}
+template <int N>
+HE_DEV float znorm2(const regla::ZVec& z) {
+    float dacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+        regla::f2v acc = regla::f2v{dacc[(2 * k) & 3], dacc[(2 * k + 1) & 3]};
+        acc = __builtin_elementwise_fma(z.p[k], z.p[k], acc);
+        dacc[(2 * k) & 3] = acc.x;
+        dacc[(2 * k + 1) & 3] = acc.y;
+    }
+    if constexpr (N & 1) dacc[(N - 1) & 3] = fmaf(ZV(z, N - 1), ZV(z, N - 1), dacc[(N - 1) & 3]);
+    return (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
 }
 
 // CRBA: one row I from its IS_I (registers)
@@ -2150,13 +2231,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
         float brow = 0.f, diag = 0.f, lamv = 0.f;
         float acol[MAXR];  // lane c: A[r][c]
         regla::ZVec z;     // lane r: row r of Zh = D^-1/2 L^-T J^T, kept for du = L^-1 D^-1/2 Zh^T lambda
+        bool legs;         // every row's support inside the root and the legs (wave-uniform)
         {
             const uint32_t anc0 = act ? T.anc_mask[rb0] : 0u;
             const uint32_t anc1 = (act && rb1 >= 0) ? T.anc_mask[rb1] : 0u;
             // bodies on some row's support (wave-uniform): the only ones whose dofs can be nonzero
             const uint32_t lb = wave_or(anc0 | anc1);
+            legs = (lb & ~kLegBodies) == 0u;
             // z = J_r^T and brow = J_r u0 on the matrix cores
-            float bacc[4] = {0.f, 0.f, 0.f, 0.f};
             zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane, nr <= 32);
             // joint-limit rows: the stored row over the joint's three dofs (its support is the joint's
             // ancestor chain, anc0)
@@ -2170,16 +2252,9 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                     ZV(z, i) = limrow ? v : ZV(z, i);
                 }
             }
-#pragma unroll
-            for (int k = 0; k < NG / 2; ++k) {  // J_r u0 on the register pairs (dof i into sum i mod 4)
-                const regla::f2v u = *reinterpret_cast<const regla::f2v*>(&L.u0[2 * k]);
-                regla::f2v acc = regla::f2v{bacc[(2 * k) & 3], bacc[(2 * k + 1) & 3]};
-                acc = __builtin_elementwise_fma(z.p[k], u, acc);
-                bacc[(2 * k) & 3] = acc.x;
-                bacc[(2 * k + 1) & 3] = acc.y;
-            }
-            bacc[(NG - 1) & 3] = fmaf(ZV(z, NG - 1), L.u0[NG - 1], bacc[(NG - 1) & 3]);
-            brow = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
+            // J_r u0 on the register pairs (dof i into sum i mod 4); over the legs' dofs only when every
+            // row's support is there (the dropped terms are fma(0, u, s) = s: the same bits)
+            brow = (HE_TGS_LEGS_ROWS && legs) ? zdot_lds<KZ>(z, L.u0) : zdot_lds<NG>(z, L.u0);
             if (act && kind == 0) {
                 const float g = L.cgap[rs_];
                 // speculative: close within the solve's step; penetrating: recover at baumgarte per physics
@@ -2193,23 +2268,20 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             STAMP(21);
             // z <- D^-1/2 z: the scale of dof i is broadcast from lane i's register (no LDS)
             const float sdl = L.sDinv[lane], sdl2 = lane < NH ? L.sDinv[64 + lane] : 0.f;
-            scale_rows<0>(z, sdl, sdl2);
-            float dacc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < NG / 2; ++k) {  // |zh_r|^2 on the register pairs (dof i into sum i mod 4)
-                regla::f2v acc = regla::f2v{dacc[(2 * k) & 3], dacc[(2 * k + 1) & 3]};
-                acc = __builtin_elementwise_fma(z.p[k], z.p[k], acc);
-                dacc[(2 * k) & 3] = acc.x;
-                dacc[(2 * k + 1) & 3] = acc.y;
-            }
-            dacc[(NG - 1) & 3] = fmaf(ZV(z, NG - 1), ZV(z, NG - 1), dacc[(NG - 1) & 3]);
-            diag = (dacc[0] + dacc[1]) + (dacc[2] + dacc[3]);
-            {  // J_r (uf - u0) = zh_r . yh, yh_i broadcast from lane i (v_readlane: no LDS loads to
-               // hoist into registers at the phase's register peak), four lanes per block into four
-               // SGPRs (one hazard nop per block; through one SGPR the 75 products serialised:
-               // this phase -10 %, the launch -0.5 % by A/B, bit-identical, round 4)
-                const float yhl = L.yh[lane], yh2 = lane < NH ? L.yh[64 + lane] : 0.f;
-                brow += zdot_lanes(z, yhl, yh2);
+            // then |zh_r|^2 and J_r (uf - u0) = zh_r . yh, yh_i broadcast from lane i (v_readlane: no LDS
+            // loads to hoist into registers at the phase's register peak), four lanes per block into
+            // four SGPRs (one hazard nop per block; through one SGPR the 75 products serialised: this
+            // phase -10 %, the launch -0.5 % by A/B, bit-identical, round 4). Leg support: dofs 0..KZ-1
+            // (zh is exactly zero past them: the same bits)
+            const float yhl = L.yh[lane];
+            if (HE_TGS_LEGS_ROWS && legs) {
+                scale_rows<0, KZ>(z, sdl, sdl2);
+                diag = znorm2<KZ>(z);
+                brow += zdot_lanes_legs(z, yhl);
+            } else {
+                scale_rows<0>(z, sdl, sdl2);
+                diag = znorm2<NG>(z);
+                brow += zdot_lanes(z, yhl, lane < NH ? L.yh[64 + lane] : 0.f);
             }
             // dof groups of four touching a support body (wave-uniform, from lb)
             uint32_t live = 0u;
@@ -2260,6 +2332,11 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             // for the phases between the sweeps
             auto tgs_solve = [&](auto ncls) {
             constexpr int NC = decltype(ncls)::value;
+            // the iterations' Zh products over dofs 0..KZ-1 when every row's support is in the legs: a
+            // wave-uniform branch inside the one instantiation (its own instantiation, with Zh's other 44
+            // registers dead, ran the standing body as fast but every other env 1-2 % slower: the
+            // second copy of the loop body; profiles/r06/ab_tgs_legs.txt)
+            const bool legs_it = HE_TGS_LEGS && NC == 32 && legs;
             // the sweep's columns -A[r][lane] / A[lane][lane] of the class's rows; up to 32 rows packed
             // with their bound weights as the PGS sweep's (pgs_sweep_fix), past 32 the weights rebuilt
             // per row (pgs_sweep_tgs: 63 registers fewer)
@@ -2342,7 +2419,12 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 const float v = act ? -cd * (diag + 1e-12f) - bb : 0.f;  // J_r u after the sweep
                 float e1, e2;  // Zh^T dl, lane = dof (and 64 + lane): also the next start's A dl = Zh (Zh^T dl)
                 __builtin_amdgcn_sched_barrier(0);  // phase fences: each phase's temporaries beside the
-                reduce_scatter_z(z, dl, lane, e1, e2);  // loop's long-lived rows and columns, not several
+                if (legs_it) {                          // loop's long-lived rows and columns, not several
+                    e1 = reduce_scatter_z_legs(z, dl);
+                    e2 = 0.f;
+                } else {
+                    reduce_scatter_z(z, dl, lane, e1, e2);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 e2 = lane < NH ? e2 : 0.f;
                 tgs_velocity(L, T, lane, e1, e2);  // the working velocity: u += L^-1 D^-1/2 (yh + Zh^T dl)
@@ -2355,8 +2437,14 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
                 if (!lastit) {
                     // the next sweep's start about lambda = applied + dl: w = J u + zh . yh + bias(sep) + A dl,
                     // with zh . yh + A dl = zh . (yh + Zh^T dl), one dot product
-                    const float yhl = L.yh[lane] + e1, yh2 = lane < NH ? L.yh[64 + lane] + e2 : 0.f;
-                    const float zy = zdot_lanes(z, yhl, yh2);
+                    const float yhl = L.yh[lane] + e1;
+                    float zy;
+                    if (legs_it) {
+                        zy = zdot_lanes_legs(z, yhl);
+                    } else {
+                        const float yh2 = lane < NH ? L.yh[64 + lane] + e2 : 0.f;
+                        zy = zdot_lanes(z, yhl, yh2);
+                    }
                     bb = act && isn ? gbias(sep) : 0.f;
                     lamv = applied + dl;
                     cd = act ? -(v + zy + bb) * invd : 0.f;
