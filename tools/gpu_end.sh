@@ -18,6 +18,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -k 10 300 python tools/phase_profile.py > gpurun_out/phases_$TAG.json 2> gpurun_out/phases_$TAG.err &&
 timeout -k 10 300 python -u tools/action_regimes.py > gpurun_out/action_regimes_$TAG.json 2> gpurun_out/action_regimes_$TAG.err &&
 timeout -k 10 200 python -u tools/contact_histogram.py > gpurun_out/contact_histogram_$TAG.json 2> gpurun_out/contact_histogram_$TAG.err &&
+timeout -k 10 300 python -u tools/support_histogram.py 30 > gpurun_out/support_classes_$TAG.json 2> gpurun_out/support_classes_$TAG.err &&
 bash tools/gpu_pmc_all.sh $TAG
 rc=$?
 # keep the summaries and the engine kernels' rows of the per-dispatch CSVs: gpurun copies back <= 64 MiB
