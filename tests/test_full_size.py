@@ -94,6 +94,24 @@ def test_dispatch_order_is_a_heavy_first_stable_partition(model):
     assert np.array_equal(order[len(heavy):], light)
 
 
+def test_dispatch_order_entry_out_of_range_does_not_fault(model):
+    """A stray write into the order buffer (an index outside [0, N)) must not send a workgroup out
+    of bounds: that workgroup falls back to workgroup id = env (he_physics.hip), the launch completes
+    with finite state, and the next rebuild (every 8 launches) restores a permutation."""
+    from humanoid_amd import _abi
+    ro = _rollout("dr", model)
+    for _ in range(8):
+        ro.step()
+    raw = ro.eng.buffer(_abi.BUF_PHYS_ORDER)  # the engine's own buffer (physics_order is a copy)
+    raw[0] = 1 << 30
+    raw[1] = -5
+    for _ in range(8):
+        ro.step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(ro.eng.root_states).all() and torch.isfinite(ro.eng.dof_state).all()
+    assert np.array_equal(np.sort(ro.eng.physics_order.cpu().numpy()), np.arange(4096))
+
+
 def test_full_size_standstill_invariant(model):
     ro = _rollout("standstill", model)
     z0 = ro.eng.root_states[:, 2].clone()
