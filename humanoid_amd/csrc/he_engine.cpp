@@ -92,6 +92,9 @@ struct he_engine {
     uint32_t* cost = nullptr;    // [N]
     int order_every = 8;
     long long launches = 0;
+    // HE_TGS_LEGS=0 in the environment: no leg class (physics_kernel_tgs's Zh products over every dof
+    // for every env; the results are the same bits, tests/test_full_size.py checks it)
+    int full_dofs = 0;
     // the stream of the last order rebuild and an event behind it: a physics launch on another
     // stream waits for it, so no workgroup reads a half-written order
     hipStream_t order_stream = nullptr;
@@ -227,6 +230,7 @@ int he_create_envs(he_engine* h, int num_envs, const float* host_start_xy) {
     HE_CHECK(dalloc(&h->cost, (size_t)N));
     HE_CHECK(hipMemset(h->cost, 0, (size_t)N * sizeof(uint32_t)));
     if (const char* v = std::getenv("HE_PHYS_ORDER")) h->order_every = std::atoi(v);
+    if (const char* v = std::getenv("HE_TGS_LEGS")) h->full_dofs = std::atoi(v) == 0;
     h->num_envs = N;
     return 0;
 }
@@ -393,6 +397,7 @@ static PhysArgs phys_args(he_engine* h, int num_simulate, const float* actions) 
     const bool ordered = h->order_every > 0;
     a.order = ordered ? h->order : nullptr;
     a.cost = ordered ? h->cost : nullptr;
+    a.full_dofs = h->full_dofs;
     return a;
 }
 }  // namespace

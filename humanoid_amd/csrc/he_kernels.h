@@ -113,6 +113,7 @@ struct PhysArgs {
     const int32_t* order;        // [N] env of each workgroup (launch_physics_order), or null: env = workgroup id
     uint32_t* cost;              // [N] each env's cycles in this launch (for launch_physics_order), or null
     int fused;                   // 1: the imitation step (mode 1) runs in the epilogue (he_env_step)
+    int full_dofs;               // 1: no leg class (every env's Zh products over 75 dofs; HE_TGS_LEGS=0, tests)
     ImitArgs im;                 // its arguments when fused
 };
 

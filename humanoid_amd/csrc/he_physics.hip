@@ -2237,7 +2237,7 @@ HE_DEV void substep(Lds& L0, const PhysArgs& a0, const he_model* mp, int lane,
             const uint32_t anc1 = (act && rb1 >= 0) ? T.anc_mask[rb1] : 0u;
             // bodies on some row's support (wave-uniform): the only ones whose dofs can be nonzero
             const uint32_t lb = wave_or(anc0 | anc1);
-            legs = (lb & ~kLegBodies) == 0u;
+            legs = (lb & ~kLegBodies) == 0u && !a.full_dofs;
             // z = J_r^T and brow = J_r u0 on the matrix cores
             zrows_mfma(z, lb, anc0, anc1, rho, dd, L, lane, nr <= 32);
             // joint-limit rows: the stored row over the joint's three dofs (its support is the joint's

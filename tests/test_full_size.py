@@ -72,6 +72,27 @@ def test_dispatch_order_leaves_the_step_unchanged(model):
         assert torch.equal(x, y), "the dispatch order must not change any env's step"
 
 
+@pytest.mark.parametrize("config", ["standstill", "dr"])
+def test_leg_class_leaves_the_step_unchanged(model, config):
+    """The TGS iterations' leg class (every contact row's support in bodies 0..8: Zh products over 32
+    dofs) against every env over all 75 dofs (HE_TGS_LEGS=0): the same bits after 12
+    steps. configs[1] runs every env in the leg class, configs[4] a mix of both classes and the wide
+    row classes."""
+    outs = []
+    for v in ("0", "1"):
+        os.environ["HE_TGS_LEGS"] = v
+        try:
+            ro = _rollout(config, model)
+        finally:
+            os.environ.pop("HE_TGS_LEGS", None)
+        for _ in range(12):
+            ro.step()
+        torch.cuda.synchronize()
+        outs.append(_state(ro) + (ro.eng.contact_cache.clone(), ro.eng.rb_state.clone(), ro.eng.dof_force.clone()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y), "the leg class must not change any env's step"
+
+
 def test_dispatch_order_is_a_heavy_first_stable_partition(model):
     """configs[4], order rebuilt every 8 launches (the default): after 16 steps the order buffer is a
     permutation of the envs; it lists first, in env order, exactly the envs whose cycle count in the
