@@ -513,7 +513,7 @@ def _merge(recs):
 # (configs[2]): the GPU meets fewer events than any fp32-noise probe of the oracle.
 NEEDED_FRAC = 0.01
 PRE_BEYOND4_FRAC = 1e-4
-POST_K = 6.0
+POST_K = float(os.environ.get("HE_PARITY_POST_K", "6.0"))  # an override only exercises the escalation
 EVENT_K = 1.0
 EVENT_SLACK = 2
 
