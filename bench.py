@@ -59,7 +59,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--num-envs", type=int, default=4096)
-    ap.add_argument("--config", choices=["standstill", "imitation", "dr"], default="standstill")
+    ap.add_argument("--config", choices=["standstill", "imitation", "tracking", "dr"], default="standstill",
+                    help="standstill = configs[1]; imitation = configs[2] with one fixed action sample; tracking = "
+                         "configs[2] with the tracking action stream (computed on the device each step); dr = configs[4]")
     ap.add_argument("--clips", type=int, default=128)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,6 +98,8 @@ DATA = {
                  "one U(-1,1) action sample reused",
     "dr": "synthetic: 128 random-walk clips, actions = 0, per-env mass scale U(0.8,1.2), friction U(0.5,1.25), "
           "terrain by env % 3 (plane / 10 deg slope / steps)",
+    "tracking": "synthetic: 128 AMASS-schema random-walk clips, env i -> clip i mod 128, actions = "
+                "clip(ref_dof_pos / scale) computed on the device every step",
 }
 
 
@@ -220,7 +224,10 @@ class Rollout:
 
     def step(self, ev=None):
         """One he_env_step (fused: one launch; `--unfused`: the physics and imitation launches).
-        ev: optional (start, mid, end) torch.cuda.Events; unfused, mid splits the two kernels."""
+        ev: optional (start, mid, end) torch.cuda.Events; unfused, mid splits the two kernels.
+        configs[2]'s tracking stream (--config tracking): the actions first, outside the events."""
+        if self.args.config == "tracking":
+            self.tracking_actions()
         if ev is not None:
             ev[0].record()
         if self.fused:
@@ -734,6 +741,7 @@ def main():
             "data": DATA[args.config],
             "config": {"workload": {"standstill": "configs[1]: 4096 SMPL-neutral humanoids, PD stand-still, zero ref motion",
                                     "imitation": "configs[2]: 4096 humanoids over 128 synthetic clips, full PHC reward",
+                                    "tracking": "configs[2] with the tracking action stream (SURVEY §8d 3(ii))",
                                     "dr": "configs[4]: 4096 envs, mass/friction randomisation + 3 terrains"}[args.config],
                        "num_envs_per_gpu": n, "simulate_calls": 2, "substeps_per_simulate": int(sim_substeps(args)),
                        "sim_dt": 1 / 60, "max_contacts": args.max_contacts,

@@ -95,10 +95,13 @@ struct he_engine {
     // HE_TGS_LEGS=0 in the environment: no leg class (physics_kernel_tgs's Zh products over every dof
     // for every env; the results are the same bits, tests/test_full_size.py checks it)
     int full_dofs = 0;
-    // the stream of the last order rebuild and an event behind it: a physics launch on another
-    // stream waits for it, so no workgroup reads a half-written order
-    hipStream_t order_stream = nullptr;
+    // the order rebuild runs on the launch's stream, and order_ready is recorded behind it: a physics
+    // launch on another stream waits for it, so no workgroup reads a half-written order (a rebuild
+    // on a side stream, beside the imitation step, made both slower: r06 A/B)
     hipEvent_t order_ready = nullptr;
+    long long order_seq = 0;          // rebuilds issued
+    long long order_seen_seq = -1;    // the rebuild the last physics launch waited for, on ...
+    hipStream_t order_seen_stream = nullptr;  // ... this stream
 };
 
 extern "C" {
@@ -405,14 +408,18 @@ static PhysArgs phys_args(he_engine* h, int num_simulate, const float* actions) 
 // the physics launch, then every order_every launches the next launches' dispatch order from this
 // one's per-env cycles (heavy envs first, he_kernels.h launch_physics_order)
 static int physics_and_order(he_engine* h, const PhysArgs& a, hipStream_t stream) {
-    if (a.order && h->order_ready && h->order_stream != stream)
+    if (a.order && h->order_seq > 0 && (h->order_seen_seq != h->order_seq || h->order_seen_stream != stream)) {
         HE_CHECK(hipStreamWaitEvent(stream, h->order_ready, 0));
+        h->order_seen_seq = h->order_seq;
+        h->order_seen_stream = stream;
+    }
     HE_CHECK(launch_physics(a, stream));
     if (a.order && ++h->launches % h->order_every == 0) {
-        HE_CHECK(launch_physics_order(h->cost, h->order, h->num_envs, stream));
         if (!h->order_ready) HE_CHECK(hipEventCreateWithFlags(&h->order_ready, hipEventDisableTiming));
+        HE_CHECK(launch_physics_order(h->cost, h->order, h->num_envs, stream));
         HE_CHECK(hipEventRecord(h->order_ready, stream));
-        h->order_stream = stream;
+        h->order_seen_seq = ++h->order_seq;
+        h->order_seen_stream = stream;
     }
     return 0;
 }

@@ -125,9 +125,11 @@ hipError_t launch_physics(const PhysArgs& a, hipStream_t stream);
 // The physics launch's dispatch order, heavy envs first. A launch's 4096 one-wave workgroups fill the
 // chip's 2048 wave slots twice, and the hardware hands the second round out in workgroup order as
 // slots free: an expensive env dispatched late sets the launch's end. One 1024-thread workgroup reads
-// the envs' cycle counts of the last launch (PhysArgs.cost) and writes order[] as a stable partition:
-// the envs over the mean by 1/16 first, then the rest, each in env order. Results do not depend on the order
-// (envs never interact). The engine runs it every few physics launches (he_engine.cpp).
+// the envs' cycle counts of the last launch (PhysArgs.cost) and writes order[] as a partition into
+// 32 classes of cost / mean (steps of 1/32 from 0.5 to 1.5), the costliest class first: a
+// longest-first order, so the slots that finish their first env early take the costly second-round
+// envs and the costliest envs' slots take the cheapest last. Results do not depend on the order (envs
+// never interact). The engine runs it every few physics launches (he_engine.cpp).
 hipError_t launch_physics_order(const uint32_t* cost, int32_t* order, int num_envs, hipStream_t stream);
 // First-dispatch warm-up (he_create_envs): every product kernel of the TU launched once with no work
 // (count 0, one block that exits at its guard), so the one-time first-dispatch cost of each kernel

@@ -2888,41 +2888,107 @@ size_t physics_lds_bytes() { return (sizeof(Lds) + 15) / 16 * 16 + HE_LDS_EXTRA;
 bool physics_phase_stamps() { return HE_PHASE_STAMPS != 0; }
 
 namespace {
-// launch_physics_order (he_kernels.h): one workgroup of 1024 threads, thread t owns the contiguous
-// chunk [t c, t c + c) of envs (c = ceil(N / 1024)); the mean cost, then per chunk its heavy count,
-// a block-wide exclusive scan of the counts, and the chunk's envs written heavy-first / light-after
+// launch_physics_order (he_kernels.h): one workgroup of 1024 threads (16 waves). The mean cost, then
+// each env's class by its cost relative to the mean, kOrderClasses classes of mean / 32 from
+// 0.5 x mean to 1.5 x mean (outside: the end classes; order_class), and order[] partitioned by
+// class, the costliest class first: a longest-first order in steps of ~3 % of the mean. One pass
+// sizes the classes, the second places every env after the costlier classes (order_wave).
 constexpr int kOrderThreads = 1024;
-__global__ void __launch_bounds__(kOrderThreads) physics_order_kernel(const uint32_t* cost, int32_t* order, int n) {
-    __shared__ unsigned long long red[kOrderThreads / 64];
-    __shared__ int scan[kOrderThreads];
-    const int t = threadIdx.x;
-    const int c = (n + kOrderThreads - 1) / kOrderThreads;
-    const int b0 = t * c < n ? t * c : n, b1 = (t + 1) * c < n ? (t + 1) * c : n;
-    unsigned long long s = 0;
-    for (int i = b0; i < b1; ++i) s += cost[i];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-    if ((t & 63) == 0) red[t >> 6] = s;
-    __syncthreads();
-    unsigned long long tot = 0;
-    for (int w = 0; w < kOrderThreads / 64; ++w) tot += red[w];
-    // heavy: over the mean by 1/16 (a uniform workload keeps the identity order, and its locality)
-    const unsigned long long mean = n > 0 ? tot / (unsigned long long)n + tot / (16ull * (unsigned long long)n) : 0ull;
-    int h = 0;
-    for (int i = b0; i < b1; ++i) h += cost[i] > mean ? 1 : 0;
-    scan[t] = h;
-    __syncthreads();
-    for (int o = 1; o < kOrderThreads; o <<= 1) {  // inclusive Hillis-Steele scan of the heavy counts
-        const int v = t >= o ? scan[t - o] : 0;
-        __syncthreads();
-        scan[t] += v;
-        __syncthreads();
+constexpr int kOrderWaves = kOrderThreads / 64;
+constexpr int kOrderClasses = 32;
+// floor(32 c / mean) - 16 clamped to the classes, in integers (the host restates it exactly:
+// tests/test_full_size.py): class >= m exactly when c >= T[m] = ceil((m + 16) tot / (32 n)), so the
+// class is found by a binary search over the 31 thresholds (one 64-bit division per threshold, not
+// per env)
+__device__ __forceinline__ int order_class(uint32_t c, const uint32_t* thr) {
+    int lo = 0;  // the largest m with c >= thr[m] (thr[0] = 0)
+#pragma unroll
+    for (int step = 16; step > 0; step >>= 1)
+        if (lo + step < kOrderClasses && c >= thr[lo + step]) lo += step;
+    return lo;
+}
+// Each wave takes the classes of its lanes' kOrderPer envs (env r0 + 1024 j + 64 w + lane, j <
+// kOrderPer) one distinct class at a time (the first remaining element's class): the class's
+// elements rank themselves by its ballots, and one lane adds their count to the class's LDS cursor
+// (an atomic per distinct class and wave, not per env). The cursor's order between waves is the
+// atomics', so envs of one class are not in env order; results do not depend on the order (envs
+// never interact).
+constexpr int kOrderPer = 4;
+__device__ __forceinline__ void order_wave(const int (&k)[kOrderPer], int lane, int* cursor, int (&slot)[kOrderPer]) {
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long left[kOrderPer];
+#pragma unroll
+    for (int j = 0; j < kOrderPer; ++j) left[j] = __ballot(k[j] >= 0);
+    for (;;) {
+        int j0 = -1;
+#pragma unroll
+        for (int j = kOrderPer - 1; j >= 0; --j) j0 = left[j] ? j : j0;
+        if (j0 < 0) break;
+        int kc = 0;
+#pragma unroll
+        for (int j = 0; j < kOrderPer; ++j)
+            if (j == j0) kc = __shfl(k[j], __builtin_ctzll(left[j]), 64);
+        unsigned long long m[kOrderPer];
+        int cnt = 0, before[kOrderPer];
+#pragma unroll
+        for (int j = 0; j < kOrderPer; ++j) {
+            m[j] = __ballot(k[j] == kc);
+            before[j] = cnt;
+            cnt += __popcll(m[j]);
+            left[j] &= ~m[j];
+        }
+        int b = 0;
+        if (lane == 0) b = atomicAdd(&cursor[kc], cnt);
+        b = __shfl(b, 0, 64);
+#pragma unroll
+        for (int j = 0; j < kOrderPer; ++j)
+            if (k[j] == kc) slot[j] = b + before[j] + __popcll(m[j] & lt);
     }
-    const int heavy_before = scan[t] - h;
-    const int heavy_total = scan[kOrderThreads - 1];
-    int ph = heavy_before, pl = heavy_total + (b0 - heavy_before);  // light before = envs before - heavy before
-    for (int i = b0; i < b1; ++i) {
-        if (cost[i] > mean) order[ph++] = i;
-        else order[pl++] = i;
+}
+__global__ void __launch_bounds__(kOrderThreads) physics_order_kernel(const uint32_t* cost, int32_t* order, int n) {
+    __shared__ unsigned long long red[kOrderWaves];
+    __shared__ int hist[kOrderClasses], cursor[kOrderClasses];
+    __shared__ uint32_t thr[kOrderClasses];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    unsigned long long s = 0;
+    for (int i = t; i < n; i += kOrderThreads) s += cost[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (lane == 0) red[w] = s;
+    if (t < kOrderClasses) hist[t] = 0;
+    __syncthreads();
+    if (t < kOrderClasses) {
+        unsigned long long tot = 0;
+        for (int v = 0; v < kOrderWaves; ++v) tot += red[v];
+        const unsigned long long d = 32ull * (unsigned long long)(n > 0 ? n : 1);
+        const unsigned long long x = (unsigned long long)(t + 16) * tot;
+        const unsigned long long T = t == 0 ? 0ull : (x + d - 1) / d;
+        thr[t] = T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T;
+    }
+    __syncthreads();
+    int k[kOrderPer], slot[kOrderPer];
+    auto classes = [&](int r0) {
+#pragma unroll
+        for (int j = 0; j < kOrderPer; ++j) {
+            const int e = r0 + kOrderThreads * j + t;
+            k[j] = e < n ? order_class(cost[e], thr) : -1;
+        }
+    };
+    for (int r0 = 0; r0 < n; r0 += kOrderPer * kOrderThreads) {  // the classes' sizes
+        classes(r0);
+        order_wave(k, lane, hist, slot);
+    }
+    __syncthreads();
+    if (t == 0) {  // the costliest class first
+        int acc = 0;
+        for (int c = kOrderClasses - 1; c >= 0; --c) { cursor[c] = acc; acc += hist[c]; }
+    }
+    __syncthreads();
+    for (int r0 = 0; r0 < n; r0 += kOrderPer * kOrderThreads) {
+        classes(r0);
+        order_wave(k, lane, cursor, slot);
+#pragma unroll
+        for (int j = 0; j < kOrderPer; ++j)
+            if (k[j] >= 0) order[slot[j]] = r0 + kOrderThreads * j + t;
     }
 }
 }  // namespace
