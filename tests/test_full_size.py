@@ -102,7 +102,7 @@ def order_classes(cost):
     return np.clip(k, 0, 31)
 
 
-def test_dispatch_order_is_a_longest_first_stable_partition(model):
+def test_dispatch_order_is_a_longest_first_partition(model):
     """configs[4], order rebuilt every 8 launches (the default): after 16 steps the order buffer is a
     permutation of the envs sorted by cost class (cost / mean in steps of 1/32), costliest first
     (he_kernels.h launch_physics_order; within a class the order is the LDS atomics'). The order is
