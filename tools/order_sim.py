@@ -6,6 +6,8 @@ partition, a three-class partition (heavy, middle, light last) and the full long
 Prints one JSON object.
 
   python tools/order_sim.py [LAUNCHES]
+  python tools/order_sim.py --offline DIR   (the cycles dumped by HE_ORDER_SIM_DUMP=DIR, replayed with
+                                             stale orders: profiles/r06/order_costs/)
 """
 import argparse
 import heapq
@@ -45,7 +47,32 @@ def orders(cost):
     return out
 
 
+def offline(d):
+    """The cycles dumped by a GPU run (HE_ORDER_SIM_DUMP), replayed: each order built from the first
+    launch's cycles and kept for the next ones (as the engine keeps it for 8 launches), the makespan
+    averaged over those launches, against the shipped order of round 5 (heavy first)."""
+    res = {}
+    for f in sorted(os.listdir(d)):
+        if not f.endswith(".npy"):
+            continue
+        C = np.load(os.path.join(d, f))
+        c0 = C[0]
+        n = len(c0)
+        ids = np.arange(n)
+        cand = orders(c0)
+        # the shipped round-6 order: 32 classes floor(32 c / mean) - 16 clamped to [0, 31], costliest first
+        k = np.clip((32 * c0.astype(np.int64) * n // int(c0.sum())) - 16, 0, 31)
+        cand["32 classes, costliest first (round 6)"] = np.concatenate([ids[k == j] for j in range(31, -1, -1)])
+        spans = {name: [makespan(C[i], o) for i in range(1, C.shape[0])] for name, o in cand.items()}
+        base = np.mean(spans["heavy first (shipped)"])
+        res[f[:-4]] = {"launches_replayed": C.shape[0] - 1,
+                       "vs_round5_heavy_first": {name: round(float(np.mean(v)) / base, 4) for name, v in spans.items()}}
+    print(json.dumps(res, indent=1))
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--offline":
+        return offline(sys.argv[2])
     import torch
     import bench
     from humanoid_amd.model import load_default_model
