@@ -65,3 +65,30 @@ def test_pmc_mfma_full_grid(tmp_path):
     r = json.load(open(out))["standstill:4096"]
     assert abs(r["mfma_util"] - 4.1e7 / (1.0e6 * 1024)) < 1e-5
     assert abs(r["valu_issue_frac"] - 0.34) < 1e-4
+
+
+def test_order_class_thresholds_equal_the_class_rule():
+    """The dispatch order's class (he_physics.hip order_class): the kernel finds it by a binary search
+    over 31 integer thresholds T[m] = ceil((m + 16) tot / (32 n)); the GPU test restates the rule as
+    floor(32 c n / tot) - 16 clamped to [0, 31] (tests/test_full_size.py order_classes). Both must
+    agree on every cost, the class edges included."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    for trial in range(60):
+        n = int(rng.integers(1, 3000))
+        if trial % 3 == 0:
+            c = rng.integers(1, 2**31, n)
+        else:
+            c = rng.integers(300_000, 900_000, n)
+        tot = int(c.sum())
+        d = 32 * n
+        thr = [0] + [min(((m + 16) * tot + d - 1) // d, 2**32 - 1) for m in range(1, 32)]
+        edges = [t for t in thr[1:] if t < 2**32 - 1]
+        for x in list(c[:200]) + edges + [t - 1 for t in edges]:  # the class edges and just below them
+            x = int(x)
+            lo = 0
+            for step in (16, 8, 4, 2, 1):
+                if lo + step < 32 and x >= thr[lo + step]:
+                    lo += step
+            rule = min(max(32 * x * n // tot - 16, 0), 31)
+            assert lo == rule, (n, x, lo, rule)
