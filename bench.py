@@ -390,14 +390,15 @@ def tracking_leg(args, model, device_index, steps=50, warmup=10, l2_steps=60):
             "parity_vs_oracle": parity_record()}
 
 
-def parity_record():
-    """BASELINE's "joint-pose L2 vs ref" as parity: the fp32 engine against the fp64 oracle on a 48-env
-    sample of this workload over 30 policy steps, measured by the GPU test
-    tests/test_full_size.py::test_full_size_tracking_parity_30_steps (the bench never runs the oracle
-    outside its cpu_baseline leg); the newest committed record, profiles/r*/parity_configs2.json."""
+def parity_record(name="parity_configs2"):
+    """BASELINE's "joint-pose L2 vs ref" as parity: the fp32 engine against the fp64 oracle on 48-env
+    samples of a workload over 30 policy steps, measured by the GPU tests
+    tests/test_full_size.py::test_full_size_{tracking,standstill}_parity_30_steps (the bench never runs
+    the oracle outside its cpu_baseline leg); the newest committed record, profiles/r*/<name>.json
+    (parity_configs2: configs[2] tracking; parity_configs1: configs[1], the headline workload)."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*",
-                                          "parity_configs2.json")))
+                                          name + ".json")))
     if not files:
         return None
     with open(files[-1]) as f:
@@ -757,6 +758,8 @@ def main():
                          "dropped_mean": round(float(dropped.mean()), 4)},
             "unfused_kernels": {"physics_kernel": phys_roof, "imitation_kernel": imit_roof},
         }
+        if args.config == "standstill" and args.num_envs == 4096:
+            line["parity_vs_oracle"] = parity_record("parity_configs1")
         if not args.no_tracking and world == 1 and args.scheme == "default":
             try:
                 line["r02_scheme"] = scheme_leg(args, model, local)

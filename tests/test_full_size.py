@@ -635,6 +635,42 @@ def test_full_size_dr_sample_30_steps(model, he_model):
     assert st1.frac <= 0.005
 
 
+def test_full_size_standstill_parity_30_steps(model, he_model):
+    """configs[1], the bench's headline workload (4096 PD stand-still envs): 30 policy steps of physics
+    on all 4096 envs and the fp64 oracle on two 48-env samples from the GPU's state after 5 bench steps
+    (_trajectory_parity, 32 probes), with the one-step re-seeded check at every step. Standing bodies
+    meet few events, so nearly every env-step is held at 1e-4 per element. Recorded to
+    HE_RECORD_DIR/parity_configs1.json."""
+    from humanoid_amd import _abi
+    from test_gpu_parity import CondStats
+    ro = _rollout("standstill", model)
+    for _ in range(5):
+        ro.step()
+    torch.cuda.synchronize()
+    sp = _abi.default_sim_params(max_contacts=40)
+    zero = torch.zeros_like(ro.actions)
+    recs = []
+    one_stats = {"env_steps": 0, "contact_set_differences": 0, "max_abs_dof_pos_rad": 0.0, "max_abs_com_m": 0.0}
+    one_env = {}
+    st1 = CondStats()
+    for sample in (21, 22):
+        idx = np.sort(np.random.default_rng(sample).choice(4096, 48, replace=False))
+
+        def advance(step):
+            return _one_step(model, he_model, ro, idx, {}, sp, step, lambda: ro.eng.step_actions(zero, 2),
+                             one_stats, st1, one_env)
+
+        recs.append(_trajectory_parity(model, he_model, ro, idx, advance, {}, sp, seed=555 + sample,
+                                       one_step=one_env))
+    rec = _merge(recs)
+    _one_step_summary(rec, one_stats, st1, one_env)
+    print("standstill parity:", {k: v for k, v in rec.items() if k not in ("env_ids", "events", "definition")})
+    _record("parity_configs1", rec)
+    _assert_parity(rec)
+    assert st1.frac <= 0.005
+    assert rec["one_step"]["contact_set_differences"] == 0
+
+
 def test_full_size_tracking_parity_30_steps(model, he_model):
     """configs[2] (4096 envs over 128 clips) with the tracking action stream a = clip(ref_dof_pos /
     scale): after 5 bench steps, 30 policy steps of physics on all 4096 envs and
