@@ -47,6 +47,14 @@ def orders(cost):
     return out
 
 
+def classes32(c):
+    """The shipped round-6 order: 32 classes floor(32 c / mean) - 16 clamped to [0, 31], costliest first."""
+    n = len(c)
+    ids = np.arange(n)
+    k = np.clip((32 * c.astype(np.int64) * n // int(c.sum())) - 16, 0, 31)
+    return np.concatenate([ids[k == j] for j in range(31, -1, -1)])
+
+
 def offline(d):
     """The cycles dumped by a GPU run (HE_ORDER_SIM_DUMP), replayed: each order built from the first
     launch's cycles and kept for the next ones (as the engine keeps it for 8 launches), the makespan
@@ -60,13 +68,22 @@ def offline(d):
         n = len(c0)
         ids = np.arange(n)
         cand = orders(c0)
-        # the shipped round-6 order: 32 classes floor(32 c / mean) - 16 clamped to [0, 31], costliest first
-        k = np.clip((32 * c0.astype(np.int64) * n // int(c0.sum())) - 16, 0, 31)
-        cand["32 classes, costliest first (round 6)"] = np.concatenate([ids[k == j] for j in range(31, -1, -1)])
+        cand["32 classes, costliest first (round 6)"] = classes32(c0)
         spans = {name: [makespan(C[i], o) for i in range(1, C.shape[0])] for name, o in cand.items()}
+        # the same 32-class order rebuilt before every launch from the previous launch's cycles (what a
+        # per-launch rebuild could do), and from the launch's own cycles (unattainable: the bound of
+        # any cost-ordered dispatch)
+        spans["32 classes, rebuilt every launch from the previous one"] = [
+            makespan(C[i], classes32(C[i - 1])) for i in range(1, C.shape[0])]
+        spans["32 classes from the launch's own cycles (unattainable)"] = [
+            makespan(C[i], classes32(C[i])) for i in range(1, C.shape[0])]
         base = np.mean(spans["heavy first (shipped)"])
         res[f[:-4]] = {"launches_replayed": C.shape[0] - 1,
-                       "vs_round5_heavy_first": {name: round(float(np.mean(v)) / base, 4) for name, v in spans.items()}}
+                       "vs_round5_heavy_first": {name: round(float(np.mean(v)) / base, 4) for name, v in spans.items()},
+                       "lag1_cost_correlation": [round(float(np.corrcoef(C[i], C[i - 1])[0, 1]), 3)
+                                                 for i in range(1, C.shape[0])],
+                       "lower_bound_vs_round5": round(float(np.mean([max(C[i].sum() / SLOTS, C[i].max())
+                                                                     for i in range(1, C.shape[0])])) / base, 4)}
     print(json.dumps(res, indent=1))
 
 
