@@ -92,3 +92,20 @@ def test_order_class_thresholds_equal_the_class_rule():
                     lo += step
             rule = min(max(32 * x * n // tot - 16, 0), 31)
             assert lo == rule, (n, x, lo, rule)
+
+
+def test_committed_parity_records_belong_to_the_built_library():
+    """bench.py reports the newest committed parity records (profiles/r*/<name>.json) with a
+    device-code status; a kernel change without re-measured records would ship them as "stale".
+    The library built from this tree must carry the device code the records were measured with."""
+    import glob
+    sys.path.insert(0, ROOT)
+    from humanoid_amd import build as B
+    if not os.path.exists(B.LIB):
+        B.build()
+    here = B.device_code_id(B.LIB)
+    for name in ("parity_configs1", "parity_configs2", "dr_events"):
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name + ".json")))
+        assert files, name
+        rec = json.load(open(files[-1]))
+        assert rec.get("device_code") == here, (files[-1], rec.get("device_code"), here)
